@@ -1,0 +1,322 @@
+// so100_capi.cpp — extern "C" boundary of libso100_hip.so (declared in include/so100.h).
+//
+// so100_create converts the double-precision host model (so100_model) into the fp32 device model
+// (DevModel) with the model-constant parts of MuJoCo's constraint setup precomputed on the host
+// (frictionloss R at pos 0, solref -> K/B, pair invweight sums), uploads it once, and returns an
+// opaque handle.  Every other call only validates arguments and enqueues a kernel on the caller's
+// stream: no allocation, no synchronisation.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include "so100.h"
+#include "so100_device.h"
+
+namespace so100 {
+hipError_t launch_step(const DevModel*, const so100_buffers&, int, int, int, int, uint64_t, int, hipStream_t);
+hipError_t launch_reset(const DevModel*, const so100_buffers&, int, int, uint64_t, int, const uint8_t*, const uint32_t*,
+                        hipStream_t);
+hipError_t launch_reward(const DevModel*, int, int, const float*, const float*, const uint32_t*, float*, hipStream_t);
+hipError_t launch_spawn(const DevModel*, int, const uint32_t*, double*, hipStream_t);
+hipError_t launch_unnormalize(const DevModel*, int, const float*, float*, hipStream_t);
+hipError_t launch_goal_reward(const DevModel*, int, const float*, const float*, float*, hipStream_t);
+}  // namespace so100
+
+using so100::DevModel;
+
+struct so100_env {
+  int device;
+  int n;
+  DevModel* d_model;
+  int task;
+  int max_steps;
+  uint64_t base_seed;
+  int env_offset;
+};
+
+static thread_local std::string g_err;
+
+static int fail(const char* msg) {
+  g_err = msg;
+  return -1;
+}
+static int fail_hip(const char* where, hipError_t e) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return -2;
+}
+
+namespace {
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+void quat2mat(const double* q, double* m) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z);     m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z);     m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y);     m[7] = 2 * (y * z + w * x);     m[8] = 1 - 2 * (x * x + y * y);
+}
+void normq(const double* q, double* o) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  for (int k = 0; k < 4; k++) o[k] = q[k] / n;
+}
+double clampimp(double v) { return v < 0.0001 ? 0.0001 : (v > 0.9999 ? 0.9999 : v); }
+// MuJoCo getimpedance at pos == margin (x = 0) -> dmin (or the flat value)
+double imp_at_zero(const double* solimp) {
+  double dmin = clampimp(solimp[0]), dmax = clampimp(solimp[1]);
+  if (dmin == dmax || solimp[2] <= 1e-15) return 0.5 * (dmin + dmax);
+  return dmin;
+}
+void solref_kb(const double* solref, const double* solimp, double h, double* K, double* B) {
+  double dmax = clampimp(solimp[1]);
+  double tc = solref[0], dr = solref[1];
+  if (tc > 0) {
+    if (tc < 2 * h) tc = 2 * h;
+    double den = dmax * dmax * tc * tc * dr * dr;
+    *K = 1 / (den > 1e-15 ? den : 1e-15);
+    double db = dmax * tc;
+    *B = 2 / (db > 1e-15 ? db : 1e-15);
+  } else {
+    *K = -tc / (dmax * dmax);
+    *B = -dr / dmax;
+  }
+}
+
+int build_device_model(const so100_model* s, DevModel* d) {
+  memset(d, 0, sizeof(*d));
+  // structural assumptions of the specialised kernel
+  for (int b = 2; b <= 7; b++)
+    if (s->body_parent[b] != b - 1) return fail("model: arm bodies 2..7 must form a chain rooted at Base (1)");
+  if (s->body_parent[1] != 0 || s->body_parent[SO100_CUBE_BODY] != 0) return fail("model: Base/cube must hang off world");
+  for (int j = 0; j < SO100_NHINGE; j++)
+    if (s->jnt_body[j] != j + 2) return fail("model: hinge j must sit on body j+2");
+  for (int k = 0; k < 3; k++)
+    if (fabs(s->body_ipos[SO100_CUBE_BODY][k]) > 1e-12) return fail("model: cube COM must be at the body origin");
+  if (fabs(s->body_iquat[SO100_CUBE_BODY][0] - 1) > 1e-12) return fail("model: cube inertia must be body-aligned");
+  if (s->site_ee_body != 6 || s->site_cube_body != SO100_CUBE_BODY) return fail("model: unexpected site bodies");
+  for (int p = 0; p < SO100_NPAIR; p++)
+    if (s->pair_condim[p] != SO100_CONDIM) return fail("model: every pair must have condim 4");
+  for (int g = 0; g < SO100_NGEOM; g++) {
+    int b = s->geom_body[g];
+    if (!(b == 0 || b == 6 || b == 7 || b == SO100_CUBE_BODY)) return fail("model: geoms must be static, on the jaws or the cube");
+  }
+
+  d->timestep = (float)s->timestep;
+  d->nsubstep = s->nsubstep;
+  d->iterations = s->iterations;
+  d->tolerance = (float)s->tolerance;
+  d->impratio = (float)s->impratio;
+  for (int k = 0; k < 3; k++) d->gravity[k] = (float)s->gravity[k];
+  d->pgs_scale = (float)(1.0 / (s->meaninertia * SO100_NV));
+  double bq[4];
+  normq(s->body_quat[1], bq);
+  for (int k = 0; k < 3; k++) d->base_pos[k] = (float)s->body_pos[1][k];
+  for (int k = 0; k < 4; k++) d->base_quat[k] = (float)bq[k];
+  for (int a = 0; a < 6; a++) {
+    int b = a + 2;
+    double q[4], im[9];
+    normq(s->body_quat[b], q);
+    for (int k = 0; k < 3; k++) d->body_pos[a][k] = (float)s->body_pos[b][k];
+    for (int k = 0; k < 4; k++) d->body_quat[a][k] = (float)q[k];
+    for (int k = 0; k < 3; k++) d->body_ipos[a][k] = (float)s->body_ipos[b][k];
+    normq(s->body_iquat[b], q);
+    quat2mat(q, im);
+    for (int k = 0; k < 9; k++) d->body_imat[a][k] = (float)im[k];
+    d->body_mass[a] = (float)s->body_mass[b];
+    for (int k = 0; k < 3; k++) d->body_inertia[a][k] = (float)s->body_inertia[b][k];
+    for (int k = 0; k < 3; k++) d->jnt_axis[a][k] = (float)s->jnt_axis[a][k];
+    d->jnt_lo[a] = (float)s->jnt_range[a][0];
+    d->jnt_hi[a] = (float)s->jnt_range[a][1];
+    d->armature[a] = (float)s->dof_armature[a];
+  }
+  d->cube_mass = (float)s->body_mass[SO100_CUBE_BODY];
+  for (int k = 0; k < 3; k++) d->cube_inertia[k] = (float)s->body_inertia[SO100_CUBE_BODY][k];
+  // frictionloss rows: pos = 0 -> imp = dmin; R = (1-imp)/imp * dof_invweight0
+  double K, B;
+  const double fimp = imp_at_zero(s->dof_solimp);
+  for (int k = 0; k < SO100_NV; k++) {
+    d->fr_floss[k] = (float)s->dof_frictionloss[k];
+    double R = (1 - fimp) / fimp * s->dof_invweight0[k];
+    d->fr_R[k] = (float)(R > 1e-15 ? R : 1e-15);
+    if (!(s->dof_frictionloss[k] > 0)) return fail("model: the kernel expects frictionloss on every dof");
+  }
+  solref_kb(s->dof_solref, s->dof_solimp, s->timestep, &K, &B);
+  d->fr_B = (float)B;
+  solref_kb(s->jnt_solref, s->jnt_solimp, s->timestep, &K, &B);
+  d->lim_K = (float)K;
+  d->lim_B = (float)B;
+  for (int k = 0; k < 5; k++) d->lim_solimp[k] = (float)s->jnt_solimp[k];
+  for (int j = 0; j < 6; j++) d->lim_invw[j] = (float)s->dof_invweight0[j];
+  for (int i = 0; i < SO100_NU; i++) {
+    d->act_kp[i] = (float)s->act_kp[i];
+    d->act_kv[i] = (float)s->act_kv[i];
+    d->act_flo[i] = (float)s->act_forcerange[i][0];
+    d->act_fhi[i] = (float)s->act_forcerange[i][1];
+    d->act_clo[i] = (float)s->act_ctrlrange[i][0];
+    d->act_chi[i] = (float)s->act_ctrlrange[i][1];
+  }
+  for (int g = 0; g < SO100_NGEOM; g++) {
+    double q[4], gm[9];
+    normq(s->geom_quat[g], q);
+    quat2mat(q, gm);
+    d->geom_body[g] = s->geom_body[g];
+    for (int k = 0; k < 3; k++) d->geom_pos[g][k] = (float)s->geom_pos[g][k];
+    for (int k = 0; k < 9; k++) d->geom_mat[g][k] = (float)gm[k];
+    for (int k = 0; k < 3; k++) d->geom_size[g][k] = (float)s->geom_size[g][k];
+  }
+  for (int p = 0; p < SO100_NPAIR; p++) {
+    d->pair_g1[p] = s->pair_geom1[p];
+    d->pair_g2[p] = s->pair_geom2[p];
+    solref_kb(s->pair_solref[p], s->pair_solimp[p], s->timestep, &K, &B);
+    d->pair_K[p] = (float)K;
+    d->pair_B[p] = (float)B;
+    for (int k = 0; k < 5; k++) d->pair_solimp[p][k] = (float)s->pair_solimp[p][k];
+    d->pair_mu0[p] = (float)s->pair_friction[p][0];
+    d->pair_mu1[p] = (float)s->pair_friction[p][1];
+    d->pair_margin[p] = (float)s->pair_margin[p];
+    int b1 = s->geom_body[s->pair_geom1[p]], b2 = s->geom_body[s->pair_geom2[p]];
+    d->pair_tran[p] = (float)(s->body_invweight0[b1][0] + s->body_invweight0[b2][0]);
+    d->pair_rot[p] = (float)(s->body_invweight0[b1][1] + s->body_invweight0[b2][1]);
+  }
+  for (int k = 0; k < 3; k++) {
+    d->site_cube[k] = (float)s->site_cube_pos[k];
+    d->site_ee[k] = (float)s->site_ee_pos[k];
+    d->bin_center_f[k] = (float)s->bin_center[k];
+    d->bin_center[k] = s->bin_center[k];
+    d->spawn_lo[k] = s->spawn_lo[k];
+    d->spawn_hi[k] = s->spawn_hi[k];
+    d->goal_bin_lo[k] = (float)s->goal_bin_lo[k];
+    d->goal_bin_hi[k] = (float)s->goal_bin_hi[k];
+  }
+  d->bin_hw = s->bin_hw;
+  d->bin_h = s->bin_h;
+  d->cube_half = s->cube_half;
+  d->goal_threshold = s->goal_threshold;
+  d->max_reward = s->max_reward;
+  for (int i = 0; i < 6; i++) {
+    d->start_qpos[i] = (float)s->start_qpos[i];
+    d->action_lo[i] = (float)s->action_lo[i];
+    d->action_hi[i] = (float)s->action_hi[i];
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int so100_abi_version(void) { return SO100_ABI_VERSION; }
+const char* so100_last_error(void) { return g_err.c_str(); }
+
+so100_env* so100_create(const so100_model* model, int n_envs, int device) {
+  if (!model) { fail("so100_create: model is NULL"); return nullptr; }
+  if (n_envs <= 0) { fail("so100_create: n_envs must be > 0"); return nullptr; }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) { fail_hip("so100_create: no HIP device", e == hipSuccess ? hipErrorNoDevice : e); return nullptr; }
+  if (device < 0 || device >= ndev) { fail("so100_create: device index out of range"); return nullptr; }
+  DevModel h;
+  if (build_device_model(model, &h) != 0) return nullptr;
+  DeviceGuard g(device);
+  DevModel* dm = nullptr;
+  e = hipMalloc(&dm, sizeof(DevModel));
+  if (e != hipSuccess) { fail_hip("so100_create: hipMalloc", e); return nullptr; }
+  e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
+  so100_env* env = new so100_env{device, n_envs, dm, SO100_TASK_CUBE_TO_BIN, 700, 0, 0};
+  return env;
+}
+
+int so100_destroy(so100_env* env) {
+  if (!env) return 0;
+  DeviceGuard g(env->device);
+  hipError_t e = hipFree(env->d_model);
+  delete env;
+  return e == hipSuccess ? 0 : fail_hip("so100_destroy", e);
+}
+
+int so100_num_envs(const so100_env* env) { return env ? env->n : -1; }
+
+int so100_configure(so100_env* env, int task, int max_episode_steps, uint64_t base_seed, int env_offset) {
+  if (!env) return fail("so100_configure: env is NULL");
+  if (task < SO100_TASK_CUBE_TO_BIN || task > SO100_TASK_GOAL) return fail("so100_configure: unknown task");
+  env->task = task;
+  env->max_steps = max_episode_steps;
+  env->base_seed = base_seed;
+  if (env_offset < 0) return fail("so100_configure: env_offset < 0");
+  env->env_offset = env_offset;
+  return 0;
+}
+
+static int check_state(const so100_buffers* b) {
+  if (!b) return fail("buffers is NULL");
+  if (!b->qpos || !b->qvel || !b->qacc_warmstart) return fail("qpos/qvel/qacc_warmstart are required");
+  return 0;
+}
+
+int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, const uint32_t* seeds, void* stream) {
+  if (!env) return fail("so100_reset: env is NULL");
+  if (check_state(b)) return -1;
+  if (env->task == SO100_TASK_GOAL && !b->desired_goal) return fail("so100_reset: GoalEnv needs desired_goal");
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_reset(env->d_model, *b, env->n, env->task, env->base_seed, env->env_offset, mask, seeds,
+                                     (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_reset", e);
+}
+
+int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) {
+  if (!env) return fail("so100_step: env is NULL");
+  if (check_state(b)) return -1;
+  if (!b->action) return fail("so100_step: action is NULL");
+  if (env->task == SO100_TASK_GOAL && !b->desired_goal) return fail("so100_step: GoalEnv needs desired_goal");
+  if ((flags & SO100_FLAG_DR) && !b->dr_params) return fail("so100_step: FLAG_DR needs dr_params");
+  if ((flags & SO100_FLAG_AUTORESET) && !b->episode) return fail("so100_step: FLAG_AUTORESET needs episode");
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_step(env->d_model, *b, env->n, env->task, flags, env->max_steps, env->base_seed, env->env_offset,
+                                    (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_step", e);
+}
+
+int so100_goal_reward(so100_env* env, int n, const float* a, const float* d, float* out, void* stream) {
+  if (!env || !a || !d || !out || n < 0) return fail("so100_goal_reward: bad arguments");
+  if (n == 0) return 0;
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_goal_reward(env->d_model, n, a, d, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_goal_reward", e);
+}
+
+int so100_eval_reward(so100_env* env, int task, int n, const float* cube, const float* ee, const uint32_t* bits,
+                      float* out, void* stream) {
+  if (!env || !cube || !ee || !bits || !out || n < 0) return fail("so100_eval_reward: bad arguments");
+  if (task < SO100_TASK_CUBE_TO_BIN || task > SO100_TASK_GOAL) return fail("so100_eval_reward: unknown task");
+  if (n == 0) return 0;
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_reward(env->d_model, task, n, cube, ee, bits, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_eval_reward", e);
+}
+
+int so100_spawn_pose(so100_env* env, int n, const uint32_t* seeds, double* pose, void* stream) {
+  if (!env || !seeds || !pose || n < 0) return fail("so100_spawn_pose: bad arguments");
+  if (n == 0) return 0;
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_spawn(env->d_model, n, seeds, pose, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_spawn_pose", e);
+}
+
+int so100_unnormalize(so100_env* env, int n, const float* action, float* ctrl, void* stream) {
+  if (!env || !action || !ctrl || n < 0) return fail("so100_unnormalize: bad arguments");
+  if (n == 0) return 0;
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_unnormalize(env->d_model, n, action, ctrl, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_unnormalize", e);
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// so100_device.h — fp32 device copy of the model with host-side precomputation (internal).
+#pragma once
+#include <stdint.h>
+#include "so100_model.h"
+
+namespace so100 {
+
+constexpr int kLanes = 16;            // lanes per env ("env lane-group" = one DPP row)
+constexpr int kEnvsPerBlock = 4;      // one wave64 per workgroup
+constexpr int kThreads = kLanes * kEnvsPerBlock;
+constexpr int kNArm = SO100_NHINGE;
+constexpr int kMaxCon = SO100_MAXCON;
+
+struct DevModel {
+  // options
+  float timestep;
+  int nsubstep;
+  int iterations;
+  float tolerance;
+  float impratio;
+  float gravity[3];
+  float pgs_scale;                  // 1 / (meaninertia * nv)
+
+  // arm chain: bodies 2..7 (index a = body-2), Base (body 1) is static
+  float base_pos[3];
+  float base_quat[4];
+  float body_pos[6][3];
+  float body_quat[6][4];
+  float body_ipos[6][3];
+  float body_imat[6][9];            // inertial frame rotation (from iquat) in the body frame
+  float body_mass[6];
+  float body_inertia[6][3];
+  float jnt_axis[6][3];
+  float jnt_lo[6], jnt_hi[6];
+  float armature[6];
+
+  // cube (free body, COM at the body origin, principal axes = body axes)
+  float cube_mass;
+  float cube_inertia[3];
+
+  // frictionloss rows (pos = 0 -> imp = dmin, R constant)
+  float fr_floss[12];
+  float fr_R[12];
+  float fr_B;                       // dof_solref -> B  (aref = -B * vel)
+
+  // limit rows
+  float lim_K, lim_B;
+  float lim_solimp[5];
+  float lim_invw[6];
+
+  // actuators
+  float act_kp[6], act_kv[6];
+  float act_flo[6], act_fhi[6];
+  float act_clo[6], act_chi[6];
+
+  // geoms
+  int geom_body[SO100_NGEOM];
+  float geom_pos[SO100_NGEOM][3];   // body frame (world for static)
+  float geom_mat[SO100_NGEOM][9];
+  float geom_size[SO100_NGEOM][3];
+
+  // pairs
+  int pair_g1[SO100_NPAIR], pair_g2[SO100_NPAIR];
+  float pair_K[SO100_NPAIR], pair_B[SO100_NPAIR];
+  float pair_solimp[SO100_NPAIR][5];
+  float pair_mu0[SO100_NPAIR], pair_mu1[SO100_NPAIR];
+  float pair_margin[SO100_NPAIR];
+  float pair_tran[SO100_NPAIR], pair_rot[SO100_NPAIR];   // diagApprox (body invweight sums)
+
+  // sites
+  float site_cube[3];               // cube body frame
+  float site_ee[3];                 // Fixed_Jaw (body 6) frame
+  float bin_center_f[3];
+
+  // task (double: the reward runs in double exactly like the reference)
+  double bin_center[3];
+  double bin_hw, bin_h, cube_half;
+  double goal_threshold;
+  double max_reward;
+  float start_qpos[6];
+  float action_lo[6], action_hi[6];
+  double spawn_lo[3], spawn_hi[3];
+  float goal_bin_lo[3], goal_bin_hi[3];   // env.py:245-249
+};
+
+}  // namespace so100

@@ -1,0 +1,1562 @@
+// so100_step.hip — MI355X (gfx950) batched SO-ARM100 bin-a-cube simulator: the hot path.
+//
+// Replaces, for N envs per launch, gym_so100/env.py:172-182 SO100Env.step ->
+// single_arm.py:33-38 before_step -> dm_control Physics.step(10) (MuJoCo mj_step x10 + mj_step1)
+// -> single_arm.py get_reward / get_observation -> env.py:130-146 packing.
+//
+// Execution model:
+//   * one wave64 workgroup = 4 envs; each env owns a 16-lane "lane group" = one DPP row.
+//   * lane k of a group owns dof k (k < 12) for the solver, contact-pair k (k < 14) for collision,
+//     contact k for per-contact constraint setup; small serial work (kinematic chain, 6x6 CRBA/RNE)
+//     runs on lane 0 of the group with results staged in LDS.
+//   * per-env state lives in registers for the whole env step (10 substeps) — HBM is touched once
+//     to load the state/action and once to store state/outputs.
+//   * the constraint solve is projected Gauss-Seidel (MuJoCo mj_solPGS semantics) with
+//     J·qacc dot products reduced across the 16-lane row by DPP (quad_perm, row_half_mirror,
+//     row_mirror): 4 VALU ops per reduction, no LDS round trip.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "so100_device.h"
+#include "so100.h"
+
+namespace so100 {
+
+#define DEV __device__ __forceinline__
+constexpr float kMinVal = 1e-15f;
+constexpr float kMinImp = 0.0001f;
+constexpr float kMaxImp = 0.9999f;
+
+// ------------------------------------------------------------------ LDS layout (per env)
+struct __attribute__((aligned(16))) EnvShared {
+  float qpos[16];
+  float qvel[16];
+  float warm[16];
+  float qacc_smooth[16];
+  float vec[16];
+  float ctrl[8];
+  float minv[6][8];
+  float inv_mcube[8];
+  float anchor[6][4];
+  float axis[6][4];
+  float cube_pos[4];
+  float cube_mat[12];
+  float jaw_pos[2][4];
+  float jaw_mat[2][12];
+  float site_cube[4];
+  float site_ee[4];
+  int cnt[16];
+  int ncon;
+  int nlim;
+  int misc[2];
+  float con_pos[kMaxCon][4];     // xyz, dist
+  float con_frame[kMaxCon][12];  // normal, t1, t2
+  int con_pair[kMaxCon];
+  float4 J[kMaxCon][12];         // contact rows (normal, t1, t2, torsion) per dof
+  float4 MJ[kMaxCon][12];        // M^-1 J' per dof
+  float AR[kMaxCon][16];         // 4x4 diagonal block of A + R
+  float4 caref[kMaxCon];
+  float4 cR[kMaxCon];
+  float4 cf[kMaxCon];
+  float cmu[kMaxCon][4];
+};
+
+// ------------------------------------------------------------------ small math (same formulas as oracle)
+DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+DEV void cross3(float* r, const float* a, const float* b) {
+  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+DEV void mulmv3(float* r, const float* m, const float* v) {
+  float t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  float t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  float t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+DEV void mulmtv3(float* r, const float* m, const float* v) {
+  float t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  float t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  float t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+DEV void mulmm3(float* r, const float* a, const float* b) {
+  float t[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = t[i];
+}
+DEV void quat_mul(float* r, const float* a, const float* b) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+DEV void quat_normalize(float* q) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < kMinVal) { q[0] = 1.f; q[1] = q[2] = q[3] = 0.f; return; }
+  float inv = 1.0f / n;
+  q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv;
+}
+DEV void quat2mat(float* m, const float* q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z);     m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z);     m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y);     m[7] = 2 * (y * z + w * x);     m[8] = 1 - 2 * (x * x + y * y);
+}
+DEV void cross_motion(float* r, const float* v, const float* u) {
+  float a[3], b[3], c[3];
+  cross3(a, v, u); cross3(b, v, u + 3); cross3(c, v + 3, u);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+DEV void cross_force(float* r, const float* v, const float* f) {
+  float a[3], b[3], c[3];
+  cross3(a, v, f); cross3(b, v + 3, f + 3); cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+// spatial inertia in[13] = I(9) about the reference point, m*d (3), m
+DEV void mul_inert(float* r, const float* in, const float* v) {
+  float Iw[3], mdv[3], mdw[3];
+  mulmv3(Iw, in, v);
+  cross3(mdv, in + 9, v + 3);
+  cross3(mdw, in + 9, v);
+#pragma unroll
+  for (int k = 0; k < 3; k++) { r[k] = Iw[k] + mdv[k]; r[3 + k] = in[12] * v[3 + k] - mdw[k]; }
+}
+
+// ------------------------------------------------------------------ cross-lane (16-lane row) primitives
+template <int CTRL>
+DEV float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// sum over the 16 lanes of this DPP row; result in every lane of the row
+DEV float rowsum16(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return v;
+}
+DEV float bcast16(float v, int src) { return __shfl(v, src, kLanes); }
+DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
+
+// ------------------------------------------------------------------ impedance / reference (MuJoCo restated)
+DEV float getimpedance(const float* solimp, float pos, float margin) {
+  float dmin = fminf(fmaxf(solimp[0], kMinImp), kMaxImp);
+  float dmax = fminf(fmaxf(solimp[1], kMinImp), kMaxImp);
+  float width = solimp[2];
+  float mid = fminf(fmaxf(solimp[3], kMinImp), kMaxImp);
+  float power = fmaxf(solimp[4], 1.0f);
+  if (dmin == dmax || width <= kMinVal) return 0.5f * (dmin + dmax);
+  float x = fabsf((pos - margin) / width);
+  if (x >= 1.0f) return dmax;
+  if (x <= 0.0f) return dmin;
+  float y;
+  if (power == 1.0f) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.0f);
+  else y = 1.0f - powf(1.0f - x, power) / powf(1.0f - mid, power - 1.0f);
+  return dmin + y * (dmax - dmin);
+}
+
+// ------------------------------------------------------------------ task prologue / epilogue
+// constants.py:44-47,78-86 applied to a float32 copy (single_arm.py:33-38): float32 ops, no FMA.
+DEV float unnormalize_f32(float a, float lo, float hi) {
+  float t = __fadd_rn(a, 1.0f);
+  float u = __fdiv_rn(t, 2.0f);
+  float v = __fmul_rn(u, hi - lo);          // (max_val - min_val) rounded once to fp32
+  float w = __fadd_rn(v, lo);
+  w = w < lo ? lo : w;
+  return w > hi ? hi : w;
+}
+
+// reward ladders — single_arm.py:322-380 / :149-215 / :246-285 (double, exactly as the reference)
+DEV double task_reward(const DevModel* __restrict__ m, int task, const float* cube_f, const float* ee_f,
+                       uint32_t bits) {
+  double bmin[3], bmax[3];
+  const double hw = m->bin_hw, h = m->bin_h;
+  bmin[0] = m->bin_center[0] + -hw; bmin[1] = m->bin_center[1] + -hw; bmin[2] = m->bin_center[2] + 0.0;
+  bmax[0] = m->bin_center[0] + hw;  bmax[1] = m->bin_center[1] + hw;  bmax[2] = m->bin_center[2] + h;
+  const bool touch_gripper = (bits & ((1u << SO100_NPAIR_GRIPPER) - 1u)) != 0u;
+  const bool touch_table = ((bits >> SO100_PAIR_TABLE) & 1u) != 0u;
+  if (task == SO100_TASK_CUBE_TO_BIN || task == SO100_TASK_GOAL) {
+    double c[3] = {(double)cube_f[0], (double)cube_f[1], (double)cube_f[2]};
+    bool over = (bmin[0] < c[0] && c[0] < bmax[0]) && (bmin[1] < c[1] && c[1] < bmax[1]);
+    bool inside = true;
+    const float half = (float)m->cube_half;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float lower = __fsub_rn(cube_f[k], half), upper = __fadd_rn(cube_f[k], half);
+      inside = inside && ((double)lower > bmin[k]) && ((double)upper < bmax[k]);
+    }
+    bool released = inside && !touch_gripper;
+    double r = 0.0;
+    if (touch_gripper) r = 1.0;
+    if (touch_gripper && !touch_table) r = 2.0;
+    if (over) r = 2.5;
+    if (inside) r = 3.0;
+    if (released) r = 4.0;
+    return r;
+  }
+  double dx = (double)ee_f[0] - (double)cube_f[0], dy = (double)ee_f[1] - (double)cube_f[1];
+  double dz = (double)ee_f[2] - (double)cube_f[2];
+  double dist = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)));
+  bool success = touch_gripper && dist < 0.05;
+  if (task == SO100_TASK_TOUCH_CUBE_SPARSE) return success ? m->max_reward : -0.2;
+  double r = 0.0;
+  if (dist < 0.7) r = fmax(r, 0.1 * (1.0 - dist / 0.7));
+  if (dist < 0.5) r = fmax(r, 0.2 * (1.0 - dist / 0.5));
+  if (dist < 0.3) r = fmax(r, 0.5 * (1.0 - dist / 0.3));
+  if (dist < 0.1) r = fmax(r, 1.0 * (1.0 - dist / 0.1));
+  if (dist < 0.05) r = fmax(r, 2.0 * (1.0 - dist / 0.05));
+  if (touch_gripper) r += 1.0;
+  if (success) return m->max_reward;
+  return r - 0.2;
+}
+
+// ------------------------------------------------------------------ RNG: numpy legacy MT19937 spawn
+// RandomState(seed).uniform(lo, hi) for 3 components (utils.py:18-29): init_genrand, one twist of the
+// first 6 words (needs mt[0..6] and mt[397..402]), tempering, 53-bit doubles.
+DEV uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+DEV void spawn_pose(const DevModel* __restrict__ m, uint32_t seed, double* pose) {
+  uint32_t lo[7], hi[6];
+  uint32_t s = seed;
+  lo[0] = s;
+#pragma unroll
+  for (int i = 1; i < 7; i++) { s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i; lo[i] = s; }
+  for (int i = 7; i < 397; i++) s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
+#pragma unroll
+  for (int i = 397; i < 403; i++) { s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i; hi[i - 397] = s; }
+  uint32_t out[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    uint32_t y = (lo[i] & 0x80000000u) | (lo[i + 1] & 0x7fffffffu);
+    uint32_t v = hi[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    out[i] = mt_temper(v);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    uint32_t a = out[2 * k] >> 5, b = out[2 * k + 1] >> 6;
+    double u = ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+    pose[k] = m->spawn_lo[k] + (m->spawn_hi[k] - m->spawn_lo[k]) * u;
+  }
+  pose[3] = 1.0; pose[4] = 0.0; pose[5] = 0.0; pose[6] = 0.0;
+}
+DEV uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+DEV uint32_t episode_seed(uint64_t base, uint32_t env, uint32_t episode) {
+  return (uint32_t)splitmix64(base ^ splitmix64(((uint64_t)env << 32) | episode));
+}
+DEV float hash_uniform(uint64_t key) { return (float)(splitmix64(key) >> 40) * (1.0f / 16777216.0f); }
+DEV float hash_normal(uint64_t key) {
+  float u1 = fmaxf(hash_uniform(key), 1e-7f), u2 = hash_uniform(key ^ 0xA5A5A5A5A5A5A5A5ull);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+// ------------------------------------------------------------------ serial position/velocity stage (lane 0)
+// [3P] mj_kinematics + mj_comPos + mj_crb + factor + mj_comVel + mj_rne + actuation + qacc_smooth for
+// the 6-hinge chain; cube free body in closed form (COM at the origin, principal axes): M = diag(m,m,m,I),
+// bias = (-m g, w x I w).  Results to LDS.
+DEV void fk_chain(const DevModel* __restrict__ m, const float* q, float xp[6][3], float xm[6][9], float ax[6][3]) {
+  float pos[3] = {m->base_pos[0], m->base_pos[1], m->base_pos[2]};
+  float quat[4] = {m->base_quat[0], m->base_quat[1], m->base_quat[2], m->base_quat[3]};
+  float R[9];
+  quat2mat(R, quat);
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    float t[3];
+    mulmv3(t, R, m->body_pos[a]);
+    pos[0] += t[0]; pos[1] += t[1]; pos[2] += t[2];
+    quat_mul(quat, quat, m->body_quat[a]);
+    float R2[9];
+    quat2mat(R2, quat);
+    mulmv3(ax[a], R2, m->jnt_axis[a]);
+    float s, c;
+    sincosf(0.5f * q[a], &s, &c);
+    float qj[4] = {c, m->jnt_axis[a][0] * s, m->jnt_axis[a][1] * s, m->jnt_axis[a][2] * s};
+    quat_mul(quat, quat, qj);
+    quat_normalize(quat);
+    quat2mat(R, quat);
+    xp[a][0] = pos[0]; xp[a][1] = pos[1]; xp[a][2] = pos[2];
+#pragma unroll
+    for (int k = 0; k < 9; k++) xm[a][k] = R[k];
+  }
+}
+
+DEV void cube_frame(const float* qp, float* pos, float* mat) {
+  float q[4] = {qp[3], qp[4], qp[5], qp[6]};
+  quat_normalize(q);
+  quat2mat(mat, q);
+  pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
+}
+
+// full serial stage; writes frames, M^-1, qacc_smooth, sites into sh
+DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynamics, float mscale) {
+  float q[6], xp[6][3], xm[6][9], ax[6][3];
+#pragma unroll
+  for (int k = 0; k < 6; k++) q[k] = sh.qpos[k];
+  fk_chain(m, q, xp, xm, ax);
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) { sh.anchor[a][t] = xp[a][t]; sh.axis[a][t] = ax[a][t]; }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) sh.jaw_pos[j][t] = xp[4 + j][t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) sh.jaw_mat[j][t] = xm[4 + j][t];
+  }
+  {
+    float t[3];
+    mulmv3(t, xm[4], m->site_ee);
+#pragma unroll
+    for (int k = 0; k < 3; k++) sh.site_ee[k] = xp[4][k] + t[k];
+  }
+  float cpos[3], cmat[9];
+  {
+    float qp[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) qp[k] = sh.qpos[6 + k];
+    cube_frame(qp, cpos, cmat);
+#pragma unroll
+    for (int k = 0; k < 3; k++) sh.cube_pos[k] = cpos[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) sh.cube_mat[k] = cmat[k];
+    float t[3];
+    mulmv3(t, cmat, m->site_cube);
+#pragma unroll
+    for (int k = 0; k < 3; k++) sh.site_cube[k] = cpos[k] + t[k];
+  }
+  if (!dynamics) return;
+
+  // ---- comPos: cinert about the tree reference point r = Base xpos; cdof
+  const float* r = m->base_pos;
+  float cin[6][13], cdof[6][6];
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    float ip[3], xi[3], IM[9], diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Ib[9], RT[9], Iw[9];
+    mulmv3(ip, xm[a], m->body_ipos[a]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) xi[k] = xp[a][k] + ip[k] - r[k];
+    mulmm3(IM, xm[a], m->body_imat[a]);
+    diag[0] = m->body_inertia[a][0]; diag[4] = m->body_inertia[a][1]; diag[8] = m->body_inertia[a][2];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) RT[3 * i + j] = IM[3 * j + i];
+    mulmm3(Ib, IM, diag);
+    mulmm3(Iw, Ib, RT);
+    float mass = m->body_mass[a];
+    float dd2 = dot3(xi, xi);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) cin[a][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0.f) - xi[i] * xi[j]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) cin[a][9 + k] = mass * xi[k];
+    cin[a][12] = mass;
+    float off[3] = {r[0] - xp[a][0], r[1] - xp[a][1], r[2] - xp[a][2]};
+#pragma unroll
+    for (int k = 0; k < 3; k++) cdof[a][k] = ax[a][k];
+    cross3(&cdof[a][3], ax[a], off);
+  }
+  // ---- CRBA (chain): composite inertia bottom-up, M(i,j) = cdof_j . (crb_i cdof_i), j <= i
+  float M[6][6];
+  {
+    float crb[13];
+#pragma unroll
+    for (int k = 0; k < 13; k++) crb[k] = 0.f;
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+#pragma unroll
+      for (int k = 0; k < 13; k++) crb[k] += cin[i][k];
+      float F[6];
+      mul_inert(F, crb, cdof[i]);
+#pragma unroll
+      for (int j = 0; j <= i; j++) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) v += cdof[j][k] * F[k];
+        M[i][j] = v; M[j][i] = v;
+      }
+      M[i][i] += m->armature[i];
+    }
+  }
+  // ---- Cholesky + explicit inverse of the 6x6 arm block
+  float L[6][6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    float s = M[j][j];
+#pragma unroll
+    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+    L[j][j] = sqrtf(fmaxf(s, kMinVal));
+    float inv = 1.0f / L[j][j];
+#pragma unroll
+    for (int i = j + 1; i < 6; i++) {
+      float t = M[i][j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+      L[i][j] = t * inv;
+    }
+  }
+  float Minv[6][6];
+#pragma unroll
+  for (int c = 0; c < 6; c++) {   // solve M x = e_c
+    float z[6], x[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      float s = (i == c) ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < i; k++) s -= L[i][k] * z[k];
+      z[i] = s / L[i][i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+      float s = z[i];
+#pragma unroll
+      for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
+      x[i] = s / L[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) Minv[i][c] = x[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int j = 0; j < 6; j++) sh.minv[i][j] = 0.5f * (Minv[i][j] + Minv[j][i]);
+
+  // ---- RNE (flg_acc = 0) on the chain: cvel, cdof_dot, cacc, cfrc, backward accumulation
+  float qd[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) qd[k] = sh.qvel[k];
+  float cvel[6] = {0, 0, 0, 0, 0, 0};
+  float cacc[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+  float cfrc[6][6];
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) cvel[k] += cdof[a][k] * qd[a];
+    float cdd[6];
+    cross_motion(cdd, cvel, cdof[a]);
+#pragma unroll
+    for (int k = 0; k < 6; k++) cacc[k] += cdd[k] * qd[a];
+    float f1[6], Iv[6], f2[6];
+    mul_inert(f1, cin[a], cacc);
+    mul_inert(Iv, cin[a], cvel);
+    cross_force(f2, cvel, Iv);
+#pragma unroll
+    for (int k = 0; k < 6; k++) cfrc[a][k] = f1[k] + f2[k];
+  }
+  float bias[6];
+  {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 5; a >= 0; a--) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) acc[k] += cfrc[a][k];
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 6; k++) v += cdof[a][k] * acc[k];
+      bias[a] = v;
+    }
+  }
+  // ---- actuation: position actuators (ctrl clamped to ctrlrange, force to forcerange)
+  float tau[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    float c = fminf(fmaxf(sh.ctrl[i], m->act_clo[i]), m->act_chi[i]);
+    float f = m->act_kp[i] * c - m->act_kp[i] * q[i] - m->act_kv[i] * qd[i];
+    f = fminf(fmaxf(f, m->act_flo[i]), m->act_fhi[i]);
+    tau[i] = f - bias[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 6; j++) s += sh.minv[i][j] * tau[j];
+    sh.qacc_smooth[i] = s;
+  }
+  // ---- cube (free body)
+  const float mc = m->cube_mass * mscale;
+  float I3[3] = {m->cube_inertia[0] * mscale, m->cube_inertia[1] * mscale, m->cube_inertia[2] * mscale};
+  float w[3] = {sh.qvel[9], sh.qvel[10], sh.qvel[11]};
+  float Iw3[3] = {I3[0] * w[0], I3[1] * w[1], I3[2] * w[2]}, gyro[3];
+  cross3(gyro, w, Iw3);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    sh.qacc_smooth[6 + k] = (mc * m->gravity[k]) / mc;   // -bias/m with bias = -m g
+    sh.qacc_smooth[9 + k] = -gyro[k] / I3[k];
+    sh.inv_mcube[k] = 1.0f / mc;
+    sh.inv_mcube[3 + k] = 1.0f / I3[k];
+  }
+}
+
+// ------------------------------------------------------------------ box-box narrowphase (one pair per lane)
+struct PairContacts {
+  int n;
+  float normal[3];
+  float pos[SO100_MAXCONPAIR][3];
+  float dist[SO100_MAXCONPAIR];
+};
+
+DEV int clip_rect_quad(const float h0, const float h1, const float* quad, float* out) {
+  float bufa[16], bufb[16];
+  float* q = bufa;
+  float* r = bufb;
+  int nq = 4, nr = 0;
+  for (int i = 0; i < 8; i++) q[i] = quad[i];
+  const float h[2] = {h0, h1};
+  for (int dir = 0; dir < 2; dir++) {
+    for (int sign = -1; sign <= 1; sign += 2) {
+      nr = 0;
+      for (int i = 0; i < nq && nr < 8; i++) {
+        const float* a = q + 2 * i;
+        const float* b = q + 2 * ((i + 1) % nq);
+        bool ina = (float)sign * a[dir] < h[dir];
+        bool inb = (float)sign * b[dir] < h[dir];
+        if (ina) { r[2 * nr] = a[0]; r[2 * nr + 1] = a[1]; nr++; }
+        if (ina != inb && nr < 8) {
+          float lim = (float)sign * h[dir];
+          r[2 * nr + 1 - dir] = a[1 - dir] + (b[1 - dir] - a[1 - dir]) / (b[dir] - a[dir]) * (lim - a[dir]);
+          r[2 * nr + dir] = lim;
+          nr++;
+        }
+      }
+      float* t = q; q = r; r = t;
+      nq = nr;
+    }
+  }
+  for (int i = 0; i < 2 * nq; i++) out[i] = q[i];
+  return nq;
+}
+
+DEV void cull_points(int n, const float* p, int mm, int i0, int* iret) {
+  float cx, cy;
+  if (n == 1) { cx = p[0]; cy = p[1]; }
+  else if (n == 2) { cx = 0.5f * (p[0] + p[2]); cy = 0.5f * (p[1] + p[3]); }
+  else {
+    float a = 0.f, qq;
+    cx = 0.f; cy = 0.f;
+    for (int i = 0; i < n; i++) {
+      int j = (i + 1) % n;
+      qq = p[2 * i] * p[2 * j + 1] - p[2 * j] * p[2 * i + 1];
+      a += qq;
+      cx += qq * (p[2 * i] + p[2 * j]);
+      cy += qq * (p[2 * i + 1] + p[2 * j + 1]);
+    }
+    if (fabsf(a) > 1e-12f) { a = 1.0f / (3.0f * a); cx *= a; cy *= a; }
+    else {
+      cx = 0.f; cy = 0.f;
+      for (int i = 0; i < n; i++) { cx += p[2 * i]; cy += p[2 * i + 1]; }
+      cx /= (float)n; cy /= (float)n;
+    }
+  }
+  float A[8];
+  bool avail[8];
+  for (int i = 0; i < n; i++) { A[i] = atan2f(p[2 * i + 1] - cy, p[2 * i] - cx); avail[i] = true; }
+  avail[i0] = false;
+  iret[0] = i0;
+  const float PI = 3.14159265358979323846f;
+  for (int j = 1; j < mm; j++) {
+    float a = (float)j * (2.f * PI / (float)mm) + A[i0];
+    if (a > PI) a -= 2.f * PI;
+    float best = 1e9f;
+    iret[j] = i0;
+    for (int i = 0; i < n; i++) {
+      if (!avail[i]) continue;
+      float df = fabsf(A[i] - a);
+      if (df > PI) df = 2.f * PI - df;
+      if (df < best) { best = df; iret[j] = i; }
+    }
+    avail[iret[j]] = false;
+  }
+}
+
+DEV void box_box(const float* p1, const float* R1, const float* A, const float* p2, const float* R2,
+                 const float* B, float margin, PairContacts& out) {
+  out.n = 0;
+  float pd[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]}, pp[3], R[9], Q[9];
+  mulmtv3(pp, R1, pd);
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      R[3 * i + j] = R1[i] * R2[j] + R1[3 + i] * R2[3 + j] + R1[6 + i] * R2[6 + j];
+      Q[3 * i + j] = fabsf(R[3 * i + j]) + 1e-6f;
+    }
+  float best = -1e30f, nb[3] = {0, 0, 0};
+  int code = 0;
+  bool invert = false;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    float s = fabsf(pp[i]) - (A[i] + B[0] * Q[3 * i] + B[1] * Q[3 * i + 1] + B[2] * Q[3 * i + 2]);
+    if (s > margin) return;
+    if (s > best) { best = s; code = 1 + i; invert = pp[i] < 0; nb[0] = nb[1] = nb[2] = 0; nb[i] = 1; }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    float e = pp[0] * R[j] + pp[1] * R[3 + j] + pp[2] * R[6 + j];
+    float s = fabsf(e) - (A[0] * Q[j] + A[1] * Q[3 + j] + A[2] * Q[6 + j] + B[j]);
+    if (s > margin) return;
+    if (s > best) { best = s; code = 4 + j; invert = e < 0; nb[0] = R[j]; nb[1] = R[3 + j]; nb[2] = R[6 + j]; }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      float n[3] = {0, 0, 0};
+      n[i1] = -R[3 * i2 + j];
+      n[i2] = R[3 * i1 + j];
+      float l = sqrtf(n[i1] * n[i1] + n[i2] * n[i2]);
+      if (l < 1e-5f) continue;
+      float e = pp[i2] * R[3 * i1 + j] - pp[i1] * R[3 * i2 + j];
+      float ex = A[i1] * Q[3 * i2 + j] + A[i2] * Q[3 * i1 + j] + B[j1] * Q[3 * i + j2] + B[j2] * Q[3 * i + j1];
+      float s = (fabsf(e) - ex) / l;
+      if (s > margin) return;
+      if (s * 1.05f > best) {
+        best = s; code = 7 + 3 * i + j; invert = e < 0;
+        nb[0] = n[0] / l; nb[1] = n[1] / l; nb[2] = n[2] / l;
+      }
+    }
+  }
+  if (code == 0) return;
+  float normal[3];
+  mulmv3(normal, R1, nb);
+  if (invert) { normal[0] = -normal[0]; normal[1] = -normal[1]; normal[2] = -normal[2]; }
+  out.normal[0] = normal[0]; out.normal[1] = normal[1]; out.normal[2] = normal[2];
+  const float depth0 = -best;
+
+  if (code > 6) {
+    const int i = (code - 7) / 3, j = (code - 7) % 3;
+    float pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+    for (int k = 0; k < 3; k++) {
+      if (k != i) {
+        float ax[3] = {R1[k], R1[3 + k], R1[6 + k]};
+        float sg = dot3(normal, ax) > 0 ? 1.f : -1.f;
+        for (int t = 0; t < 3; t++) pa[t] += sg * A[k] * ax[t];
+      }
+      if (k != j) {
+        float ax[3] = {R2[k], R2[3 + k], R2[6 + k]};
+        float sg = dot3(normal, ax) > 0 ? -1.f : 1.f;
+        for (int t = 0; t < 3; t++) pb[t] += sg * B[k] * ax[t];
+      }
+    }
+    float ua[3] = {R1[i], R1[3 + i], R1[6 + i]}, ub[3] = {R2[j], R2[3 + j], R2[6 + j]};
+    float pq[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    float uaub = dot3(ua, ub), q1 = dot3(ua, pq), q2 = -dot3(ub, pq);
+    float den = 1.f - uaub * uaub, al = 0.f, be = 0.f;
+    if (den > 1e-4f) { den = 1.f / den; al = (q1 + uaub * q2) * den; be = (uaub * q1 + q2) * den; }
+    for (int t = 0; t < 3; t++) {
+      pa[t] += ua[t] * al;
+      pb[t] += ub[t] * be;
+      out.pos[0][t] = 0.5f * (pa[t] + pb[t]);
+    }
+    out.dist[0] = -depth0;
+    out.n = 1;
+    return;
+  }
+
+  const float *pR, *RR, *SR, *pI, *RI, *SI;
+  float nref[3];
+  int codeN;
+  if (code <= 3) {
+    pR = p1; RR = R1; SR = A; pI = p2; RI = R2; SI = B; codeN = code - 1;
+    nref[0] = normal[0]; nref[1] = normal[1]; nref[2] = normal[2];
+  } else {
+    pR = p2; RR = R2; SR = B; pI = p1; RI = R1; SI = A; codeN = code - 4;
+    nref[0] = -normal[0]; nref[1] = -normal[1]; nref[2] = -normal[2];
+  }
+  float nr[3], anr[3];
+  for (int k = 0; k < 3; k++) {
+    float ax[3] = {RI[k], RI[3 + k], RI[6 + k]};
+    nr[k] = dot3(nref, ax);
+    anr[k] = fabsf(nr[k]);
+  }
+  int lanr = (anr[1] > anr[0]) ? ((anr[1] > anr[2]) ? 1 : 2) : ((anr[0] > anr[2]) ? 0 : 2);
+  float center[3];
+  for (int t = 0; t < 3; t++) center[t] = pI[t] - pR[t] + (nr[lanr] < 0 ? SI[lanr] : -SI[lanr]) * RI[3 * t + lanr];
+  const int c1 = (codeN == 0) ? 1 : 0, c2 = (codeN == 2) ? 1 : 2;
+  const int a1 = (lanr == 0) ? 1 : 0, a2 = (lanr == 2) ? 1 : 2;
+  float u1[3] = {RR[c1], RR[3 + c1], RR[6 + c1]}, u2[3] = {RR[c2], RR[3 + c2], RR[6 + c2]};
+  float v1[3] = {RI[a1], RI[3 + a1], RI[6 + a1]}, v2[3] = {RI[a2], RI[3 + a2], RI[6 + a2]};
+  float cc1 = dot3(center, u1), cc2 = dot3(center, u2);
+  float m11 = dot3(u1, v1), m12 = dot3(u1, v2), m21 = dot3(u2, v1), m22 = dot3(u2, v2);
+  float k1 = m11 * SI[a1], k2 = m21 * SI[a1], k3 = m12 * SI[a2], k4 = m22 * SI[a2];
+  float quad[8] = {cc1 - k1 - k3, cc2 - k2 - k4, cc1 - k1 + k3, cc2 - k2 + k4,
+                   cc1 + k1 + k3, cc2 + k2 + k4, cc1 + k1 - k3, cc2 + k2 - k4};
+  float pts[16];
+  int n = clip_rect_quad(SR[c1], SR[c2], quad, pts);
+  if (n < 1) return;
+  float det = m11 * m22 - m12 * m21;
+  if (fabsf(det) < 1e-12f) return;
+  det = 1.f / det;
+  float i11 = m22 * det, i12 = -m12 * det, i21 = -m21 * det, i22 = m11 * det;
+  float P3[8][3], dep[8], P2[16];
+  int cnum = 0;
+  for (int k = 0; k < n; k++) {
+    float x = pts[2 * k] - cc1, y = pts[2 * k + 1] - cc2;
+    float s1 = i11 * x + i12 * y, s2 = i21 * x + i22 * y;
+    float pt[3];
+    for (int t = 0; t < 3; t++) pt[t] = center[t] + s1 * v1[t] + s2 * v2[t];
+    float dp = SR[codeN] - dot3(nref, pt);
+    if (dp > -margin) {
+      for (int t = 0; t < 3; t++) P3[cnum][t] = pt[t] + pR[t];
+      dep[cnum] = dp;
+      P2[2 * cnum] = pts[2 * k];
+      P2[2 * cnum + 1] = pts[2 * k + 1];
+      cnum++;
+    }
+  }
+  if (cnum < 1) return;
+  int idx[8], nout = cnum;
+  if (cnum > SO100_MAXCONPAIR) {
+    int i0 = 0;
+    for (int k = 1; k < cnum; k++) if (dep[k] > dep[i0]) i0 = k;
+    cull_points(cnum, P2, SO100_MAXCONPAIR, i0, idx);
+    nout = SO100_MAXCONPAIR;
+  } else {
+    for (int k = 0; k < cnum; k++) idx[k] = k;
+  }
+  for (int c = 0; c < nout; c++) {
+    int k = idx[c];
+    for (int t = 0; t < 3; t++) out.pos[c][t] = P3[k][t] + 0.5f * dep[k] * nref[t];
+    out.dist[c] = -dep[k];
+  }
+  out.n = nout;
+}
+
+// geom world pose from the staged body frames
+DEV void geom_pose(const DevModel* __restrict__ m, const EnvShared& sh, int g, float* pos, float* mat) {
+  int b = m->geom_body[g];
+  if (b == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) pos[k] = m->geom_pos[g][k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) mat[k] = m->geom_mat[g][k];
+    return;
+  }
+  const float* bp;
+  const float* bm;
+  if (b == SO100_CUBE_BODY) { bp = sh.cube_pos; bm = sh.cube_mat; }
+  else { bp = sh.jaw_pos[b - 6]; bm = sh.jaw_mat[b - 6]; }
+  float t[3];
+  mulmv3(t, bm, m->geom_pos[g]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) pos[k] = bp[k] + t[k];
+  mulmm3(mat, bm, m->geom_mat[g]);
+}
+
+DEV void collide_pair(const DevModel* __restrict__ m, const EnvShared& sh, int p, PairContacts& pc) {
+  pc.n = 0;
+  const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
+  float p1[3], R1[9], p2[3], R2[9];
+  geom_pose(m, sh, g1, p1, R1);
+  geom_pose(m, sh, g2, p2, R2);
+  const float* A = m->geom_size[g1];
+  const float* B = m->geom_size[g2];
+  float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  const float margin = m->pair_margin[p];
+  if (sqrtf(dot3(d, d)) > sqrtf(dot3(A, A)) + sqrtf(dot3(B, B)) + margin) return;
+  box_box(p1, R1, A, p2, R2, B, margin, pc);
+}
+
+DEV void make_frame(float* f) {
+  float* n = f;
+  float* t1 = f + 3;
+  float nn = sqrtf(dot3(n, n));
+  n[0] /= nn; n[1] /= nn; n[2] /= nn;
+  if (fabsf(n[1]) < 0.5f) { t1[0] = 0.f; t1[1] = 1.f; t1[2] = 0.f; }
+  else { t1[0] = 0.f; t1[1] = 0.f; t1[2] = 1.f; }
+  float pr = dot3(n, t1);
+  t1[0] -= pr * n[0]; t1[1] -= pr * n[1]; t1[2] -= pr * n[2];
+  float tn = sqrtf(dot3(t1, t1));
+  t1[0] /= tn; t1[1] /= tn; t1[2] /= tn;
+  cross3(f + 6, n, t1);
+}
+
+// ------------------------------------------------------------------ QCQP (MuJoCo mju_QCQP3 restated)
+DEV void qcqp3(float* x, const float A0[3][3], const float* b0, const float* dd, float r) {
+  float A[3][3], b[3], y[3] = {0.f, 0.f, 0.f}, la = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    b[i] = b0[i] * dd[i];
+#pragma unroll
+    for (int j = 0; j < 3; j++) A[i][j] = A0[i][j] * dd[i] * dd[j];
+  }
+  for (int it = 0; it < 20; it++) {
+    float P[3][3], Pi[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) P[i][j] = A[i][j] + (i == j ? la : 0.f);
+    Pi[0][0] = P[1][1] * P[2][2] - P[1][2] * P[2][1];
+    Pi[0][1] = P[0][2] * P[2][1] - P[0][1] * P[2][2];
+    Pi[0][2] = P[0][1] * P[1][2] - P[0][2] * P[1][1];
+    Pi[1][0] = P[1][2] * P[2][0] - P[1][0] * P[2][2];
+    Pi[1][1] = P[0][0] * P[2][2] - P[0][2] * P[2][0];
+    Pi[1][2] = P[0][2] * P[1][0] - P[0][0] * P[1][2];
+    Pi[2][0] = P[1][0] * P[2][1] - P[1][1] * P[2][0];
+    Pi[2][1] = P[0][1] * P[2][0] - P[0][0] * P[2][1];
+    Pi[2][2] = P[0][0] * P[1][1] - P[0][1] * P[1][0];
+    float det = P[0][0] * Pi[0][0] + P[0][1] * Pi[1][0] + P[0][2] * Pi[2][0];
+    if (det < kMinVal) { x[0] = x[1] = x[2] = 0.f; return; }
+    float id = 1.f / det;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) Pi[i][j] *= id;
+#pragma unroll
+    for (int i = 0; i < 3; i++) y[i] = -(Pi[i][0] * b[0] + Pi[i][1] * b[1] + Pi[i][2] * b[2]);
+    float val = y[0] * y[0] + y[1] * y[1] + y[2] * y[2] - r * r;
+    if (val < 1e-10f) break;
+    float deriv = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) deriv += y[i] * (Pi[i][0] * y[0] + Pi[i][1] * y[1] + Pi[i][2] * y[2]);
+    deriv *= -2.f;
+    float delta = -val / deriv;
+    if (delta < 1e-10f) break;
+    la += delta;
+  }
+  x[0] = y[0] * dd[0]; x[1] = y[1] * dd[1]; x[2] = y[2] * dd[2];
+}
+
+// ------------------------------------------------------------------ the step kernel
+struct StepArgs {
+  const DevModel* m;
+  so100_buffers b;
+  int n;
+  int task;
+  int flags;
+  int max_steps;
+  uint64_t base_seed;
+  int env_offset;
+};
+
+DEV int wave_max_i(int v) {
+  // max over the wave (all 4 lane groups); result uniform
+  v = max(v, __shfl_xor(v, 16));
+  v = max(v, __shfl_xor(v, 32));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// reset one env (lane-group cooperative): arm start pose, cube spawn, zero velocity/warmstart
+DEV void env_reset_state(const DevModel* __restrict__ m, EnvShared& sh, int lane, uint32_t seed, float& qpos_r,
+                         float& qvel_r, float& warm_r, double* pose_out) {
+  double pose[7];
+  spawn_pose(m, seed, pose);
+  if (pose_out) {
+#pragma unroll
+    for (int k = 0; k < 7; k++) pose_out[k] = pose[k];
+  }
+  float v = 0.f;
+  if (lane < 6) v = m->start_qpos[lane];
+#pragma unroll
+  for (int k = 0; k < 7; k++) if (lane == 6 + k) v = (float)pose[k];
+  qpos_r = v;
+  qvel_r = 0.f;
+  warm_r = 0.f;
+}
+
+// obs row: box(3) bin(3) ee(3) qpos[:6] — env.py:137-145.  qv = qpos[lane-9] gathered by the caller
+// (bcast16 in uniform control flow).
+DEV void write_obs(const DevModel* __restrict__ m, const EnvShared& sh, int lane, float qv, float* dst) {
+  float v = qv;
+  if (lane < 3) v = sh.site_cube[lane];
+  else if (lane < 6) v = m->bin_center_f[lane - 3];
+  else if (lane < 9) v = sh.site_ee[lane - 6];
+  if (lane < SO100_NOBS) dst[lane] = v;
+}
+
+__global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
+  __shared__ EnvShared shm[kEnvsPerBlock];
+  const DevModel* __restrict__ m = args.m;
+  const int tid = threadIdx.x;
+  const int grp = tid >> 4;
+  const int lane = tid & 15;
+  const int env = blockIdx.x * kEnvsPerBlock + grp;
+  const bool valid = env < args.n;
+  const int e = valid ? env : 0;          // clamp loads for the tail group; stores are guarded
+  EnvShared& sh = shm[grp];
+  const so100_buffers& B = args.b;
+
+  // ---------------- prologue: state + action -> registers
+  float qpos_r = (lane < SO100_NQ) ? B.qpos[(size_t)e * SO100_NQ + lane] : 0.f;
+  float qvel_r = (lane < SO100_NV) ? B.qvel[(size_t)e * SO100_NV + lane] : 0.f;
+  float warm_r = (lane < SO100_NV) ? B.qacc_warmstart[(size_t)e * SO100_NV + lane] : 0.f;
+  float mscale = 1.f, fscale = 1.f, sigma = 0.f;
+  if ((args.flags & SO100_FLAG_DR) && B.dr_params) {
+    mscale = B.dr_params[(size_t)e * 4 + 0];
+    fscale = B.dr_params[(size_t)e * 4 + 1];
+    sigma = B.dr_params[(size_t)e * 4 + 2];
+  }
+  const int elapsed0 = B.elapsed ? B.elapsed[e] : 0;
+  const uint32_t episode0 = B.episode ? B.episode[e] : 0u;
+  if (lane < 6) {
+    float a = B.action[(size_t)e * 6 + lane];
+    if (sigma > 0.f)
+      a += sigma * hash_normal(splitmix64(args.base_seed ^ ((uint64_t)(e + args.env_offset) << 40) ^ ((uint64_t)episode0 << 20) ^
+                                          (uint64_t)(elapsed0 * 8 + lane)));
+    sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane]);
+  }
+
+  const float h = m->timestep;
+  float dbg_iter = 0.f, dbg_impr = 0.f;
+  int dbg_nefc = 0;
+
+  for (int sub = 0; sub < m->nsubstep; sub++) {
+    // ---------------- S1: stage state in LDS
+    if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
+    if (lane < SO100_NV) { sh.qvel[lane] = qvel_r; sh.warm[lane] = warm_r; }
+    __syncthreads();
+    // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
+    if (lane == 0) serial_stage(m, sh, true, mscale);
+    __syncthreads();
+    // ---------------- S3: collision, one pair per lane, compaction in pair order
+    PairContacts pc;
+    pc.n = 0;
+    if (lane < SO100_NPAIR) collide_pair(m, sh, lane, pc);
+    sh.cnt[lane] = pc.n;
+    __syncthreads();
+    {
+      int off = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
+      for (int c = 0; c < pc.n; c++) {
+        int slot = off + c;
+        if (slot < kMaxCon) {
+          float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
+          make_frame(fr);
+#pragma unroll
+          for (int t = 0; t < 9; t++) sh.con_frame[slot][t] = fr[t];
+          sh.con_pos[slot][0] = pc.pos[c][0]; sh.con_pos[slot][1] = pc.pos[c][1];
+          sh.con_pos[slot][2] = pc.pos[c][2]; sh.con_pos[slot][3] = pc.dist[c];
+          sh.con_pair[slot] = lane;
+        }
+      }
+      if (lane == 0) sh.ncon = tot < kMaxCon ? tot : kMaxCon;
+    }
+    __syncthreads();
+    const int ncon = valid ? sh.ncon : 0;
+    const int ncon_max = wave_max_i(ncon);
+
+    // ---------------- S4: contact Jacobian rows, lane = dof
+    for (int c = 0; c < ncon_max; c++) {
+      if (c < ncon && lane < SO100_NV) {
+        const int p = sh.con_pair[c];
+        const float* cp = sh.con_pos[c];
+        const float* fr = sh.con_frame[c];
+        float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+          const int b = m->geom_body[side ? m->pair_g2[p] : m->pair_g1[p]];
+          const float sg = side ? 1.f : -1.f;
+          if (lane < 6) {
+            if (b >= 2 && b <= 7 && lane + 2 <= b) {
+              float off[3] = {cp[0] - sh.anchor[lane][0], cp[1] - sh.anchor[lane][1], cp[2] - sh.anchor[lane][2]};
+              float v[3];
+              cross3(v, sh.axis[lane], off);
+#pragma unroll
+              for (int t = 0; t < 3; t++) { jp[t] += sg * v[t]; jr[t] += sg * sh.axis[lane][t]; }
+            }
+          } else if (b == SO100_CUBE_BODY) {
+            if (lane < 9) {
+              jp[lane - 6] += sg;
+            } else {
+              const int k = lane - 9;
+              float ax[3] = {sh.cube_mat[k], sh.cube_mat[3 + k], sh.cube_mat[6 + k]};
+              float off[3] = {cp[0] - sh.cube_pos[0], cp[1] - sh.cube_pos[1], cp[2] - sh.cube_pos[2]};
+              float v[3];
+              cross3(v, ax, off);
+#pragma unroll
+              for (int t = 0; t < 3; t++) { jp[t] += sg * v[t]; jr[t] += sg * ax[t]; }
+            }
+          }
+        }
+        float4 J4;
+        J4.x = fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2];
+        J4.y = fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2];
+        J4.z = fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2];
+        J4.w = fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2];
+        sh.J[c][lane] = J4;
+      }
+    }
+    __syncthreads();
+    // ---------------- S5: MJ = M^-1 J' per dof lane; friction/limit row setup (lane = dof)
+    float minv_row[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) minv_row[j] = (lane < 6) ? sh.minv[lane][j] : 0.f;
+    const float invmc = (lane >= 6 && lane < 12) ? sh.inv_mcube[lane - 6] : 0.f;
+    for (int c = 0; c < ncon_max; c++) {
+      if (c < ncon && lane < SO100_NV) {
+        float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < 6) {
+#pragma unroll
+          for (int j = 0; j < 6; j++) {
+            float4 Jj = sh.J[c][j];
+            r4.x += minv_row[j] * Jj.x; r4.y += minv_row[j] * Jj.y;
+            r4.z += minv_row[j] * Jj.z; r4.w += minv_row[j] * Jj.w;
+          }
+        } else {
+          float4 Jk = sh.J[c][lane];
+          r4 = make_float4(Jk.x * invmc, Jk.y * invmc, Jk.z * invmc, Jk.w * invmc);
+        }
+        sh.MJ[c][lane] = r4;
+      }
+    }
+    const float qs_r = (lane < SO100_NV) ? sh.qacc_smooth[lane] : 0.f;
+    // frictionloss row of dof `lane`
+    const bool has_fr = lane < SO100_NV;
+    float fr_R = has_fr ? m->fr_R[lane] : 1.f;
+    float fr_fl = has_fr ? m->fr_floss[lane] : 0.f;
+    float fr_aref = -m->fr_B * qvel_r;
+    float mdiag = invmc;
+#pragma unroll
+    for (int j = 0; j < 6; j++) mdiag = (lane == j) ? minv_row[j] : mdiag;
+    float fr_AR = mdiag + fr_R;
+    float fr_f;
+    {
+      float jar = warm_r - fr_aref;
+      if (jar <= -fr_R * fr_fl) fr_f = fr_fl;
+      else if (jar >= fr_R * fr_fl) fr_f = -fr_fl;
+      else fr_f = -jar / fr_R;
+      if (!has_fr) fr_f = 0.f;
+    }
+    // joint-limit row of hinge `lane`
+    bool lim_on = false;
+    float lim_s = 0.f, lim_aref = 0.f, lim_R = 1.f, lim_AR = 1.f, lim_f = 0.f;
+    if (lane < 6) {
+      float dlo = qpos_r - m->jnt_lo[lane], dhi = m->jnt_hi[lane] - qpos_r;
+      float dist = 0.f;
+      if (dlo < 0.f) { lim_on = true; lim_s = 1.f; dist = dlo; }
+      else if (dhi < 0.f) { lim_on = true; lim_s = -1.f; dist = dhi; }
+      if (lim_on) {
+        float imp = getimpedance(m->lim_solimp, dist, 0.f);
+        lim_R = fmaxf(kMinVal, (1.f - imp) / imp * m->lim_invw[lane]);
+        lim_aref = -m->lim_B * (lim_s * qvel_r) - m->lim_K * imp * dist;
+        lim_AR = fr_AR - fr_R + lim_R;
+        float jar = lim_s * warm_r - lim_aref;
+        lim_f = jar < 0.f ? -jar / lim_R : 0.f;
+      }
+    }
+    const uint64_t lim_mask = __ballot(lim_on && valid);
+    __syncthreads();
+    // ---------------- S6: per-contact setup, lane = contact
+    if (lane < ncon) {
+      const int c = lane;
+      const int p = sh.con_pair[c];
+      const float dist = sh.con_pos[c][3];
+      float ARb[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+      float vel[4] = {0, 0, 0, 0}, acc[4] = {0, 0, 0, 0}, ws[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < SO100_NV; k++) {
+        float4 Jk = sh.J[c][k], Mk = sh.MJ[c][k];
+        float jv[4] = {Jk.x, Jk.y, Jk.z, Jk.w}, mv[4] = {Mk.x, Mk.y, Mk.z, Mk.w};
+        float qv = sh.qvel[k], qa = sh.qacc_smooth[k], qw = sh.warm[k];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#pragma unroll
+          for (int s = 0; s < 4; s++) ARb[r][s] += jv[r] * mv[s];
+          vel[r] += jv[r] * qv;
+          acc[r] += jv[r] * qa;
+          ws[r] += jv[r] * qw;
+        }
+      }
+      const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
+      const float K = m->pair_K[p], Bd = m->pair_B[p];
+      const float mu0 = m->pair_mu0[p] * fscale, mu1 = m->pair_mu1[p] * fscale;
+      float R[4];
+      R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
+      R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
+      R[2] = R[1];
+      R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
+      float aref[4];
+      aref[0] = -Bd * vel[0] - K * imp * (dist - m->pair_margin[p]);
+      aref[1] = -Bd * vel[1]; aref[2] = -Bd * vel[2]; aref[3] = -Bd * vel[3];
+#pragma unroll
+      for (int r = 0; r < 4; r++) ARb[r][r] += R[r];
+      // warmstart force (dual map of jar = J qacc_ws - aref), elliptic zones
+      float jar[4], f[4], mus[3] = {mu0, mu0, mu1};
+#pragma unroll
+      for (int r = 0; r < 4; r++) jar[r] = ws[r] - aref[r];
+      {
+        float mu = mu0 * sqrtf(R[1] / R[0]);
+        float U[4], T = 0.f;
+        U[0] = jar[0] * mu;
+#pragma unroll
+        for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
+        T = sqrtf(T);
+        float N = U[0];
+        if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
+          f[0] = f[1] = f[2] = f[3] = 0.f;
+        } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) f[k] = -jar[k] / R[k];
+        } else {
+          float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
+          float NmT = N - mu * T;
+          f[0] = -Dm * NmT * mu;
+#pragma unroll
+          for (int k = 1; k < 4; k++) f[k] = -f[0] / T * U[k] * mus[k - 1];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int s = 0; s < 4; s++) sh.AR[c][4 * r + s] = ARb[r][s];
+      sh.caref[c] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+      sh.cR[c] = make_float4(R[0], R[1], R[2], R[3]);
+      sh.cf[c] = make_float4(f[0], f[1], f[2], f[3]);
+      sh.cmu[c][0] = mu0; sh.cmu[c][1] = mu0; sh.cmu[c][2] = mu1;
+      // dual-cost partial of this contact's rows: 0.5 R f^2 + f b, b = J qacc_smooth - aref
+      float part = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; r++) part += 0.5f * R[r] * f[r] * f[r] + f[r] * (acc[r] - aref[r]);
+      sh.vec[c] = part;   // consumed below (indices < ncon)
+    }
+    __syncthreads();
+    // ---------------- S7: warmstart dual cost, initial qacc
+    float cost_part = 0.f;
+    if (lane < ncon) cost_part += sh.vec[lane];
+    float phi = 0.f;
+    if (lane < SO100_NV) {
+      phi = fr_f + (lim_on ? lim_s * lim_f : 0.f);
+      for (int c = 0; c < ncon_max; c++) {
+        if (c < ncon) {
+          float4 Jk = sh.J[c][lane], fc = sh.cf[c];
+          phi += Jk.x * fc.x + Jk.y * fc.y + Jk.z * fc.z + Jk.w * fc.w;
+        }
+      }
+      cost_part += 0.5f * fr_R * fr_f * fr_f + fr_f * (qs_r - fr_aref);
+      if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
+    }
+    __syncthreads();
+    if (lane < SO100_NV) sh.vec[lane] = phi;
+    __syncthreads();
+    float dq = 0.f;
+    if (lane < 6) {
+#pragma unroll
+      for (int j = 0; j < 6; j++) dq += minv_row[j] * sh.vec[j];
+    } else if (lane < 12) {
+      dq = invmc * phi;
+    }
+    cost_part += 0.5f * phi * dq;
+    const float cost = rowsum16(cost_part);
+    float qacc_c = qs_r;
+    if (cost > 0.f) {
+      fr_f = 0.f; lim_f = 0.f;
+      for (int c = 0; c < ncon_max; c++)
+        if (c < ncon) sh.cf[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      qacc_c += dq;
+    }
+    if (lane >= SO100_NV) qacc_c = 0.f;
+
+    // ---------------- S8: projected Gauss-Seidel (MuJoCo mj_solPGS order: friction | limits | contacts)
+    bool done = !valid;
+    int iters = 0;
+    float last_impr = 0.f;
+    const float fr_ARinv = 1.f / fr_AR;
+    for (int it = 0; it < m->iterations; it++) {
+      if (__ballot(!done) == 0ull) break;
+      float impr = 0.f;
+      // arm frictionloss rows, sequential (coupled through M^-1)
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        float delta = 0.f;
+        if (lane == j) {
+          float res = qacc_c - fr_aref + fr_R * fr_f;
+          float old = fr_f;
+          float fn = fr_f - res * fr_ARinv;
+          fn = fminf(fmaxf(fn, -fr_fl), fr_fl);
+          delta = fn - old;
+          if (done) delta = 0.f;
+          fr_f = old + delta;
+          impr -= delta * (res + 0.5f * fr_AR * delta);
+        }
+        float db = bcast16(delta, j);
+        qacc_c += minv_row[j] * db;
+      }
+      // cube frictionloss rows: decoupled (diagonal M), all six in parallel
+      if (lane >= 6 && lane < 12 && !done) {
+        float res = qacc_c - fr_aref + fr_R * fr_f;
+        float old = fr_f;
+        float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
+        float delta = fn - old;
+        fr_f = fn;
+        impr -= delta * (res + 0.5f * fr_AR * delta);
+        qacc_c += invmc * delta;
+      }
+      // joint-limit rows (hinge order)
+      if (lim_mask) {
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+          if (!((lim_mask >> j) & 0x0001000100010001ull)) continue;
+          float delta = 0.f;
+          if (lane == j && lim_on && !done) {
+            float res = lim_s * qacc_c - lim_aref + lim_R * lim_f;
+            float old = lim_f;
+            float fn = fmaxf(lim_f - res / lim_AR, 0.f);
+            delta = fn - old;
+            lim_f = fn;
+            impr -= delta * (res + 0.5f * lim_AR * delta);
+            delta *= lim_s;
+          }
+          float db = bcast16(delta, j);
+          qacc_c += minv_row[j] * db;
+        }
+      }
+      // contact blocks (elliptic, condim 4): normal then friction QCQP
+      for (int c = 0; c < ncon_max; c++) {
+        const bool act = (c < ncon) && !done;
+        float4 Jk = (lane < SO100_NV && c < ncon) ? sh.J[c][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float j0 = rowsum16(Jk.x * qacc_c), j1 = rowsum16(Jk.y * qacc_c);
+        float j2 = rowsum16(Jk.z * qacc_c), j3 = rowsum16(Jk.w * qacc_c);
+        float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (act) {
+          const float4 ar = sh.caref[c], R4 = sh.cR[c], f4 = sh.cf[c];
+          const float* AR = sh.AR[c];
+          float res[4] = {j0 - ar.x + R4.x * f4.x, j1 - ar.y + R4.y * f4.y, j2 - ar.z + R4.z * f4.z,
+                          j3 - ar.w + R4.w * f4.w};
+          float old[4] = {f4.x, f4.y, f4.z, f4.w}, f[4];
+          f[0] = old[0] - res[0] / AR[0];
+          if (f[0] < kMinVal) {
+            f[0] = f[1] = f[2] = f[3] = 0.f;
+          } else {
+            float Af[3][3], bf[3], x[3];
+            float mus[3] = {sh.cmu[c][0], sh.cmu[c][1], sh.cmu[c][2]};
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+              bf[a] = res[1 + a] + AR[4 * (1 + a)] * (f[0] - old[0]);
+#pragma unroll
+              for (int b2 = 0; b2 < 3; b2++) {
+                Af[a][b2] = AR[4 * (1 + a) + 1 + b2];
+                bf[a] -= Af[a][b2] * old[1 + b2];
+              }
+            }
+            qcqp3(x, Af, bf, mus, f[0]);
+            f[1] = x[0]; f[2] = x[1]; f[3] = x[2];
+          }
+          float dl[4] = {f[0] - old[0], f[1] - old[1], f[2] - old[2], f[3] - old[3]};
+          if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              float q = AR[4 * r] * dl[0] + AR[4 * r + 1] * dl[1] + AR[4 * r + 2] * dl[2] + AR[4 * r + 3] * dl[3];
+              impr -= dl[r] * (res[r] + 0.5f * q);
+            }
+          }
+          sh.cf[c] = make_float4(f[0], f[1], f[2], f[3]);
+          d4 = make_float4(dl[0], dl[1], dl[2], dl[3]);
+        }
+        if (act && lane < SO100_NV) {
+          float4 Mk = sh.MJ[c][lane];
+          qacc_c += Mk.x * d4.x + Mk.y * d4.y + Mk.z * d4.z + Mk.w * d4.w;
+        }
+      }
+      const float improvement = rowsum16(impr) * m->pgs_scale;
+      if (!done) {
+        iters = it + 1;
+        last_impr = improvement;
+        if (improvement < m->tolerance) done = true;
+      }
+    }
+    dbg_iter = (float)iters;
+    dbg_impr = last_impr;
+    dbg_nefc = 12 + __popcll(lim_mask & (0xFFFFull << (grp * 16))) + 4 * ncon;
+
+    // debug: contact normal forces of the last substep
+    if (B.debug && valid && sub == m->nsubstep - 1) {
+      float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
+      if (lane < kMaxCon) {
+        dbg[16 + lane] = lane < ncon ? sh.con_pos[lane][3] : 0.f;
+        dbg[32 + lane] = lane < ncon ? sh.cf[lane].x : 0.f;
+        dbg[48 + lane] = lane < ncon ? (float)sh.con_pair[lane] : -1.f;
+      }
+      if (lane < SO100_NV) { dbg[4 + lane] = qacc_c; dbg[64 + lane] = qs_r; dbg[76 + lane] = fr_f; }
+      if (lane == 0) { dbg[0] = (float)ncon; dbg[1] = dbg_iter; dbg[2] = dbg_impr; dbg[3] = (float)dbg_nefc; }
+    }
+
+    // ---------------- S9: semi-implicit Euler (mj_Euler): qvel += h qacc; qpos with the new qvel
+    if (lane < SO100_NV) qvel_r += h * qacc_c;
+    warm_r = (lane < SO100_NV) ? qacc_c : 0.f;
+    if (lane < 9) qpos_r += h * qvel_r;
+    __syncthreads();
+    if (lane >= 9 && lane < 12) sh.vec[lane] = qvel_r;
+    if (lane >= 9 && lane < 13) sh.qpos[lane] = qpos_r;
+    __syncthreads();
+    if (lane >= 9 && lane < 13) {
+      float q[4] = {sh.qpos[9], sh.qpos[10], sh.qpos[11], sh.qpos[12]};
+      float w[3] = {sh.vec[9], sh.vec[10], sh.vec[11]};
+      float nw = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+      if (nw > kMinVal) {
+        float s, c;
+        sincosf(0.5f * h * nw, &s, &c);
+        float qr[4] = {c, w[0] / nw * s, w[1] / nw * s, w[2] / nw * s};
+        quat_mul(q, q, qr);
+      }
+      quat_normalize(q);
+      qpos_r = q[lane - 9];
+    }
+    __syncthreads();
+  }
+
+  // ---------------- final position stage (mj_step1): sites + contact set for reward / obs
+  if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
+  if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
+  __syncthreads();
+  if (lane == 0) serial_stage(m, sh, false, mscale);
+  __syncthreads();
+  PairContacts pc;
+  pc.n = 0;
+  if (lane < SO100_NPAIR) collide_pair(m, sh, lane, pc);
+  const uint64_t hit = __ballot(pc.n > 0);
+  const uint32_t bits = (uint32_t)((hit >> (grp * 16)) & 0xFFFFull);
+
+  // divergence check (dm_control PhysicsError analogue)
+  bool bad = (lane < SO100_NQ) && !(fabsf(qpos_r) < 1e4f);
+  bad = bad || ((lane < SO100_NV) && !(fabsf(qvel_r) < 1e6f));
+  const bool diverged = ((__ballot(bad) >> (grp * 16)) & 0xFFFFull) != 0ull;
+
+  float cube_f[3] = {sh.site_cube[0], sh.site_cube[1], sh.site_cube[2]};
+  float ee_f[3] = {sh.site_ee[0], sh.site_ee[1], sh.site_ee[2]};
+  double reward = 0.0;
+  bool terminated = false, truncated = false, success = false;
+  int elapsed = elapsed0 + 1;
+  const bool goal = args.task == SO100_TASK_GOAL;
+  float goal_des[3] = {0.f, 0.f, 0.f};
+  if (goal) {
+    // SO100GoalEnv.step (env.py:372-406): sparse reward on ||achieved - desired|| < 0.01
+#pragma unroll
+    for (int k = 0; k < 3; k++) goal_des[k] = B.desired_goal[(size_t)e * 3 + k];
+    float d0 = cube_f[0] - goal_des[0], d1 = cube_f[1] - goal_des[1], d2 = cube_f[2] - goal_des[2];
+    float dist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+    success = dist < (float)m->goal_threshold;
+    reward = success ? 0.0 : -1.0;
+    terminated = success;
+    truncated = elapsed >= args.max_steps;
+  } else {
+    reward = task_reward(m, args.task, cube_f, ee_f, bits);
+    terminated = success = (reward == 4.0);              // env.py:175
+    truncated = args.max_steps > 0 && elapsed >= args.max_steps;   // TimeLimit (gym_so100/__init__.py)
+  }
+  if (diverged) truncated = true;
+  const bool doneflag = terminated || truncated;
+
+  const float qv_obs = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
+  if (valid) {
+    if (lane == 0) {
+      if (B.reward) B.reward[env] = (float)reward;
+      if (B.terminated) B.terminated[env] = terminated;
+      if (B.truncated) B.truncated[env] = truncated;
+      if (B.success) B.success[env] = success;
+      if (B.diverged) B.diverged[env] = diverged;
+      if (B.contact_bits) B.contact_bits[env] = bits;
+      if (goal && B.total_steps) B.total_steps[env] = B.total_steps[env] + 1;
+    }
+    if (goal && B.achieved_goal && lane < 3) B.achieved_goal[(size_t)env * 3 + lane] = cube_f[lane];
+    if (B.obs) write_obs(m, sh, lane, qv_obs, B.obs + (size_t)env * SO100_NOBS);
+  }
+
+  const bool autoreset = (args.flags & SO100_FLAG_AUTORESET) != 0;
+  const bool do_reset = autoreset && doneflag;
+  const uint64_t rmask = __ballot(do_reset && valid);
+  int new_elapsed = elapsed;
+  uint32_t new_episode = episode0;
+  if (rmask) {
+    if (do_reset && valid && B.final_obs && lane < SO100_NOBS && B.obs)
+      B.final_obs[(size_t)env * SO100_NOBS + lane] = B.obs[(size_t)env * SO100_NOBS + lane];
+    if (do_reset && valid) {
+      new_episode = episode0 + 1;
+      new_elapsed = 0;
+      uint32_t seed = episode_seed(args.base_seed, (uint32_t)(env + args.env_offset), new_episode);
+      env_reset_state(m, sh, lane, seed, qpos_r, qvel_r, warm_r, nullptr);
+    }
+    __syncthreads();
+    if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
+    __syncthreads();
+    if (lane == 0 && do_reset && valid) serial_stage(m, sh, false, mscale);
+    __syncthreads();
+    const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
+    if (do_reset && valid) {
+      if (B.obs) write_obs(m, sh, lane, qv_r, B.obs + (size_t)env * SO100_NOBS);
+      if (goal) {
+        // _sample_goal (env.py:322-334): lifted box around the spawn while total_steps < 5000, else bin box
+        const int tsteps = B.total_steps ? B.total_steps[env] : 0;
+        if (lane < 3) {
+          float u = hash_uniform(splitmix64(args.base_seed * 31ull + ((uint64_t)(env + args.env_offset) << 24) + new_episode * 3ull + lane));
+          float lo, hi;
+          if (tsteps < 5000) {
+            float c = lane < 2 ? sh.qpos[6 + lane] : 0.f;
+            lo = lane < 2 ? c - 0.03f : 0.01f;
+            hi = lane < 2 ? c + 0.03f : 0.05f;
+          } else {
+            lo = m->goal_bin_lo[lane];
+            hi = m->goal_bin_hi[lane];
+          }
+          B.desired_goal[(size_t)env * 3 + lane] = lo + (hi - lo) * u;
+          if (B.achieved_goal) B.achieved_goal[(size_t)env * 3 + lane] = sh.site_cube[lane];
+        }
+      }
+    }
+  }
+
+  // ---------------- store state
+  if (valid) {
+    if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
+    if (lane < SO100_NV) {
+      B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
+      B.qacc_warmstart[(size_t)env * SO100_NV + lane] = warm_r;
+    }
+    if (lane == 0) {
+      if (B.elapsed) B.elapsed[env] = new_elapsed;
+      if (B.episode) B.episode[env] = new_episode;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ reset kernel
+struct ResetArgs {
+  const DevModel* m;
+  so100_buffers b;
+  int n;
+  int task;
+  uint64_t base_seed;
+  int env_offset;
+  const uint8_t* mask;
+  const uint32_t* seeds;
+};
+
+__global__ void __launch_bounds__(kThreads) so100_reset_kernel(ResetArgs args) {
+  __shared__ EnvShared shm[kEnvsPerBlock];
+  const DevModel* __restrict__ m = args.m;
+  const int tid = threadIdx.x, grp = tid >> 4, lane = tid & 15;
+  const int env = blockIdx.x * kEnvsPerBlock + grp;
+  const bool valid = env < args.n;
+  const int e = valid ? env : 0;
+  EnvShared& sh = shm[grp];
+  const so100_buffers& B = args.b;
+  const bool act = valid && (args.mask == nullptr || args.mask[e] != 0);
+  float qpos_r = 0.f, qvel_r = 0.f, warm_r = 0.f;
+  uint32_t episode = B.episode ? B.episode[e] + (act ? 1u : 0u) : 0u;
+  if (act) {
+    uint32_t seed = args.seeds ? args.seeds[e] : episode_seed(args.base_seed, (uint32_t)(env + args.env_offset), episode);
+    env_reset_state(m, sh, lane, seed, qpos_r, qvel_r, warm_r, nullptr);
+  }
+  if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
+  __syncthreads();
+  if (lane == 0 && act) serial_stage(m, sh, false, 1.f);
+  __syncthreads();
+  const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
+  if (act) {
+    if (B.obs) write_obs(m, sh, lane, qv_r, B.obs + (size_t)env * SO100_NOBS);
+    if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
+    if (lane < SO100_NV) {
+      B.qvel[(size_t)env * SO100_NV + lane] = 0.f;
+      B.qacc_warmstart[(size_t)env * SO100_NV + lane] = 0.f;
+    }
+    if (lane == 0) {
+      if (B.elapsed) B.elapsed[env] = 0;
+      if (B.episode) B.episode[env] = episode;
+    }
+    if (args.task == SO100_TASK_GOAL && B.desired_goal && lane < 3) {
+      const int tsteps = B.total_steps ? B.total_steps[env] : 0;
+      float u = hash_uniform(splitmix64(args.base_seed * 31ull + ((uint64_t)(env + args.env_offset) << 24) + episode * 3ull + lane));
+      float lo, hi;
+      if (tsteps < 5000) {
+        float c = lane < 2 ? sh.qpos[6 + lane] : 0.f;
+        lo = lane < 2 ? c - 0.03f : 0.01f;
+        hi = lane < 2 ? c + 0.03f : 0.05f;
+      } else {
+        lo = m->goal_bin_lo[lane];
+        hi = m->goal_bin_hi[lane];
+      }
+      B.desired_goal[(size_t)env * 3 + lane] = lo + (hi - lo) * u;
+      if (B.achieved_goal) B.achieved_goal[(size_t)env * 3 + lane] = sh.site_cube[lane];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ standalone ops (parity surface)
+__global__ void so100_reward_kernel(const DevModel* m, int task, int n, const float* cube, const float* ee,
+                                    const uint32_t* bits, float* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float c[3] = {cube[3 * i], cube[3 * i + 1], cube[3 * i + 2]};
+  float x[3] = {ee[3 * i], ee[3 * i + 1], ee[3 * i + 2]};
+  out[i] = (float)task_reward(m, task, c, x, bits[i]);
+}
+
+__global__ void so100_spawn_kernel(const DevModel* m, int n, const uint32_t* seeds, double* pose) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double p[7];
+  spawn_pose(m, seeds[i], p);
+  for (int k = 0; k < 7; k++) pose[7 * i + k] = p[k];
+}
+
+__global__ void so100_unnormalize_kernel(const DevModel* m, int n, const float* a, float* c) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 6) return;
+  int k = i % 6;
+  c[i] = unnormalize_f32(a[i], m->action_lo[k], m->action_hi[k]);
+}
+
+__global__ void so100_goal_reward_kernel(const DevModel* m, int n, const float* a, const float* d, float* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // np.linalg.norm(achieved - desired, axis=1) in float32 (env.py:347-349)
+  float d0 = a[3 * i] - d[3 * i], d1 = a[3 * i + 1] - d[3 * i + 1], d2 = a[3 * i + 2] - d[3 * i + 2];
+  float dist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+  out[i] = dist < (float)m->goal_threshold ? 0.f : -1.f;
+}
+
+// ------------------------------------------------------------------ launchers (called by so100_capi.cpp)
+hipError_t launch_step(const DevModel* m, const so100_buffers& b, int n, int task, int flags, int max_steps,
+                       uint64_t base_seed, int env_offset, hipStream_t s) {
+  StepArgs a{m, b, n, task, flags, max_steps, base_seed, env_offset};
+  dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
+  hipLaunchKernelGGL(so100_step_kernel, grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_reset(const DevModel* m, const so100_buffers& b, int n, int task, uint64_t base_seed,
+                        int env_offset, const uint8_t* mask, const uint32_t* seeds, hipStream_t s) {
+  ResetArgs a{m, b, n, task, base_seed, env_offset, mask, seeds};
+  dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
+  hipLaunchKernelGGL(so100_reset_kernel, grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_reward(const DevModel* m, int task, int n, const float* c, const float* e, const uint32_t* bits,
+                         float* out, hipStream_t s) {
+  hipLaunchKernelGGL(so100_reward_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m, task, n, c, e, bits, out);
+  return hipGetLastError();
+}
+hipError_t launch_spawn(const DevModel* m, int n, const uint32_t* seeds, double* pose, hipStream_t s) {
+  hipLaunchKernelGGL(so100_spawn_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m, n, seeds, pose);
+  return hipGetLastError();
+}
+hipError_t launch_unnormalize(const DevModel* m, int n, const float* a, float* c, hipStream_t s) {
+  hipLaunchKernelGGL(so100_unnormalize_kernel, dim3((n * 6 + 255) / 256), dim3(256), 0, s, m, n, a, c);
+  return hipGetLastError();
+}
+hipError_t launch_goal_reward(const DevModel* m, int n, const float* a, const float* d, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(so100_goal_reward_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m, n, a, d, out);
+  return hipGetLastError();
+}
+
+}  // namespace so100

@@ -1,0 +1,125 @@
+"""Single-env classes with the reference's constructor/reset/step API (gym_so100/env.py).
+
+``SO100Env`` (env.py:26-185) and ``SO100GoalEnv`` (env.py:188-409) are thin views over a one-env
+``SO100VecEnv`` on the GPU: numpy in, numpy out, like the reference.  For throughput use
+``SO100VecEnv`` directly (thousands of envs per launch).
+
+Deviation: camera renders are out of scope, so ``obs_type`` must be "so100_state" and
+GoalEnv's "observation" is the 15-float state vector instead of flattened pixels + qpos.
+"""
+import numpy as np
+
+from . import spaces
+from .constants import SO100_ACTIONS, SO100_JOINTS, GOAL_DISTANCE_THRESHOLD, bin_max, bin_min
+from .vec_env import SO100VecEnv
+
+try:
+    import gymnasium as _gym
+    _Base = _gym.Env
+except ImportError:          # gymnasium is optional here
+    class _Base:
+        metadata = {}
+
+        def reset(self, seed=None, options=None):
+            return None
+
+
+class SO100Env(_Base):
+    metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
+
+    def __init__(self, task, obs_type="so100_state", render_mode="rgb_array", observation_width=640,
+                 observation_height=480, visualization_width=640, visualization_height=480, device="cuda:0",
+                 max_episode_steps=0):
+        super().__init__()
+        self.task = task
+        self.obs_type = obs_type
+        self.render_mode = render_mode
+        self.observation_width, self.observation_height = observation_width, observation_height
+        self.visualization_width, self.visualization_height = visualization_width, visualization_height
+        # TimeLimit is applied by the gymnasium registry wrapper (as in the reference); 0 = none here
+        self._venv = SO100VecEnv(1, task=task, obs_type=obs_type, device=device, autoreset=False,
+                                 max_episode_steps=max_episode_steps)
+        self.observation_space = spaces.Box(low=-100.0, high=100.0, shape=(len(SO100_JOINTS) + 3 * 3,),
+                                            dtype=np.float32)           # env.py:67-73
+        self.action_space = spaces.Box(low=-1, high=1, shape=(len(SO100_ACTIONS),), dtype=np.float32)
+
+    def reset(self, seed=None, options=None):
+        super().reset(seed=seed)
+        obs, _ = self._venv.reset(seed=None if seed is None else [int(seed)])
+        return obs[0].cpu().numpy(), {"is_success": False}              # env.py:169
+
+    def step(self, action):
+        action = np.asarray(action, dtype=np.float32)
+        assert action.ndim == 1                                          # env.py:173
+        obs, reward, terminated, truncated, info = self._venv.step(action[None, :6])
+        r = float(reward[0].item())
+        is_success = bool(info["is_success"][0].item())
+        return obs[0].cpu().numpy(), r, bool(terminated[0].item()), False, {"is_success": is_success}
+
+    def render(self):
+        raise NotImplementedError("rendering is out of scope of the GPU hot path (DESIGN.md §7)")
+
+    def close(self):
+        self._venv.close()
+
+
+class SO100GoalEnv(_Base):
+    metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
+
+    def __init__(self, render_mode="rgb_array", observation_width=640, observation_height=480,
+                 visualization_width=640, visualization_height=480, device="cuda:0"):
+        super().__init__()
+        self.max_episode_steps = 300                                     # env.py:200
+        self.current_step = 0
+        self.render_mode = render_mode
+        self._venv = SO100VecEnv(1, task="so100_goal", device=device, autoreset=False)
+        self.distance_threshold = GOAL_DISTANCE_THRESHOLD                # env.py:252
+        obs_space = spaces.Box(low=-np.inf, high=np.inf, shape=(15,), dtype=np.float32)
+        self.observation_space = spaces.Dict({
+            "observation": obs_space,
+            "achieved_goal": spaces.Box(low=-np.inf, high=np.inf, shape=(3,), dtype=np.float32),
+            "desired_goal": spaces.Box(low=-np.inf, high=np.inf, shape=(3,), dtype=np.float32)})
+        self.action_space = spaces.Box(low=-1, high=1, shape=(len(SO100_ACTIONS),), dtype=np.float32)
+        self.bin_goal_space = spaces.Box(low=np.array([bin_min[0] + 0.005, bin_min[1] + 0.005, 0.01]),
+                                         high=np.array([bin_max[0] - 0.005, bin_max[1] - 0.005, 0.05]),
+                                         dtype=np.float32)               # env.py:245-249
+
+    @property
+    def total_steps(self):
+        return int(self._venv.total_steps[0].item())
+
+    def _goal_obs(self, o):
+        return {k: v[0].cpu().numpy() for k, v in o.items()}
+
+    def reset(self, seed=None, options=None):
+        super().reset(seed=seed)
+        self.current_step = 0
+        obs, _ = self._venv.reset(seed=None if seed is None else [int(seed)])
+        return self._goal_obs(obs), {"is_success": False}
+
+    def compute_reward(self, achieved_goal, desired_goal, info):
+        """Sparse reward (env.py:341-353): batched -> float32 array, single -> python float."""
+        a = np.asarray(achieved_goal)
+        d = np.asarray(desired_goal)
+        if a.ndim > 1:
+            return self._venv.compute_reward(a, d).cpu().numpy()
+        return 0.0 if np.linalg.norm(a - d) < self.distance_threshold else -1.0
+
+    def step(self, action):
+        action = np.asarray(action, dtype=np.float32)
+        assert action.ndim == 1                                          # env.py:375
+        obs, reward, terminated, truncated, info = self._venv.step(action[None, :6])
+        self.current_step += 1
+        out = self._goal_obs(obs)
+        success = bool(info["is_success"][0].item())
+        trunc = bool(truncated[0].item())
+        inf = {"is_success": success}
+        if trunc:
+            inf["TimeLimit.truncated"] = True
+        return out, float(reward[0].item()), bool(terminated[0].item()), trunc, inf
+
+    def render(self):
+        raise NotImplementedError("rendering is out of scope of the GPU hot path (DESIGN.md §7)")
+
+    def close(self):
+        self._venv.close()

@@ -1,0 +1,141 @@
+"""Derived SO-ARM100 model table -> ``so100_model`` C struct (include/so100_model.h).
+
+The table (assets/so100_model.json) is produced by tools/compile_model.py from the reference MJCF
+(/root/reference/gym_so100/assets/so100_transfer_cube.xml, loaded by the reference at
+gym_so100/env.py:111-112).  Task constants below mirror the reference's Python module constants and
+cite them; they are data, not compute.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+from . import constants as C
+
+ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so100_model.json")
+
+NBODY, NHINGE, NQ, NV, NU, NGEOM, NPAIR = 9, 6, 13, 12, 6, 15, 14
+MAXCON, CONDIM, NOBS = 16, 4, 15
+NEFC_MAX = NV + NHINGE + MAXCON * CONDIM
+
+_d = ctypes.c_double
+_i = ctypes.c_int
+
+
+def _arr(t, *dims):
+    for n in reversed(dims):
+        t = t * n
+    return t
+
+
+class SO100Model(ctypes.Structure):
+    """Mirror of ``so100_model`` (include/so100_model.h) — field order must match exactly."""
+    _fields_ = [
+        ("timestep", _d), ("nsubstep", _i), ("iterations", _i), ("tolerance", _d), ("impratio", _d),
+        ("gravity", _arr(_d, 3)), ("meaninertia", _d),
+        ("body_parent", _arr(_i, NBODY)), ("body_pos", _arr(_d, NBODY, 3)), ("body_quat", _arr(_d, NBODY, 4)),
+        ("body_ipos", _arr(_d, NBODY, 3)), ("body_iquat", _arr(_d, NBODY, 4)), ("body_mass", _arr(_d, NBODY)),
+        ("body_inertia", _arr(_d, NBODY, 3)), ("body_invweight0", _arr(_d, NBODY, 2)),
+        ("jnt_body", _arr(_i, NHINGE)), ("jnt_axis", _arr(_d, NHINGE, 3)), ("jnt_range", _arr(_d, NHINGE, 2)),
+        ("jnt_solref", _arr(_d, 2)), ("jnt_solimp", _arr(_d, 5)),
+        ("dof_armature", _arr(_d, NV)), ("dof_frictionloss", _arr(_d, NV)), ("dof_invweight0", _arr(_d, NV)),
+        ("dof_solref", _arr(_d, 2)), ("dof_solimp", _arr(_d, 5)),
+        ("act_kp", _arr(_d, NU)), ("act_kv", _arr(_d, NU)), ("act_forcerange", _arr(_d, NU, 2)),
+        ("act_ctrlrange", _arr(_d, NU, 2)),
+        ("geom_body", _arr(_i, NGEOM)), ("geom_pos", _arr(_d, NGEOM, 3)), ("geom_quat", _arr(_d, NGEOM, 4)),
+        ("geom_size", _arr(_d, NGEOM, 3)),
+        ("pair_geom1", _arr(_i, NPAIR)), ("pair_geom2", _arr(_i, NPAIR)), ("pair_condim", _arr(_i, NPAIR)),
+        ("pair_friction", _arr(_d, NPAIR, 3)), ("pair_solref", _arr(_d, NPAIR, 2)),
+        ("pair_solimp", _arr(_d, NPAIR, 5)), ("pair_margin", _arr(_d, NPAIR)),
+        ("site_cube_body", _i), ("site_cube_pos", _arr(_d, 3)), ("site_ee_body", _i), ("site_ee_pos", _arr(_d, 3)),
+        ("bin_center", _arr(_d, 3)),
+        ("start_qpos", _arr(_d, NU)), ("action_lo", _arr(_d, NU)), ("action_hi", _arr(_d, NU)),
+        ("spawn_lo", _arr(_d, 3)), ("spawn_hi", _arr(_d, 3)),
+        ("bin_hw", _d), ("bin_h", _d), ("cube_half", _d), ("goal_threshold", _d), ("max_reward", _d),
+        ("goal_bin_lo", _arr(_d, 3)), ("goal_bin_hi", _arr(_d, 3)),
+    ]
+
+
+def _set(m, name, values):
+    f = getattr(m, name)
+    flat = np.asarray(values).reshape(-1)
+    if not hasattr(f, "_length_"):
+        setattr(m, name, type(f)(flat[0]) if not isinstance(f, float) else float(flat[0]))
+        return
+
+    def rec(arr, vals):
+        if hasattr(arr[0], "_length_"):
+            step = len(vals) // len(arr)
+            for k in range(len(arr)):
+                rec(arr[k], vals[k * step:(k + 1) * step])
+        else:
+            for k in range(len(arr)):
+                arr[k] = vals[k].item() if hasattr(vals[k], "item") else vals[k]
+    rec(f, flat)
+
+
+def load_model_dict(path=ASSET):
+    with open(path) as f:
+        return json.load(f)
+
+
+def build_model(path=ASSET, iterations=None, nsubstep=None):
+    """Return an ``SO100Model`` ctypes struct filled from the derived model table."""
+    d = load_model_dict(path)
+    m = SO100Model()
+    o = d["opt"]
+    m.timestep = o["timestep"]
+    m.nsubstep = int(round(C.DT / o["timestep"])) if nsubstep is None else int(nsubstep)   # env.py:120-127
+    m.iterations = int(o["iterations"] if iterations is None else iterations)
+    m.tolerance = o["tolerance"]
+    m.impratio = o["impratio"]
+    _set(m, "gravity", o["gravity"])
+    m.meaninertia = o["meaninertia"]
+    for k in ("body_parent",):
+        _set(m, k, np.asarray(d[k], dtype=np.int64))
+    for k in ("body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia", "body_invweight0",
+              "jnt_axis", "jnt_range", "jnt_solref", "jnt_solimp", "dof_armature", "dof_frictionloss",
+              "dof_invweight0", "dof_solref", "dof_solimp", "act_kp", "act_kv", "act_forcerange", "act_ctrlrange"):
+        _set(m, k, np.asarray(d[k], dtype=np.float64))
+    _set(m, "jnt_body", np.asarray(d["jnt_body"], dtype=np.int64))
+    g = d["geoms"]
+    _set(m, "geom_body", np.asarray([x["body"] for x in g], dtype=np.int64))
+    _set(m, "geom_pos", np.asarray([x["pos"] for x in g]))
+    _set(m, "geom_quat", np.asarray([x["quat"] for x in g]))
+    _set(m, "geom_size", np.asarray([x["size"] for x in g]))
+    p = d["pairs"]
+    _set(m, "pair_geom1", np.asarray([x["g1"] for x in p], dtype=np.int64))
+    _set(m, "pair_geom2", np.asarray([x["g2"] for x in p], dtype=np.int64))
+    _set(m, "pair_condim", np.asarray([x["condim"] for x in p], dtype=np.int64))
+    _set(m, "pair_friction", np.asarray([x["friction"] for x in p]))
+    _set(m, "pair_solref", np.asarray([x["solref"] for x in p]))
+    _set(m, "pair_solimp", np.asarray([x["solimp"] for x in p]))
+    _set(m, "pair_margin", np.asarray([x["margin"] - x["gap"] for x in p]))
+    m.site_cube_body = d["site_cube"]["body"]
+    _set(m, "site_cube_pos", d["site_cube"]["pos"])
+    m.site_ee_body = d["site_ee"]["body"]
+    _set(m, "site_ee_pos", d["site_ee"]["pos"])
+    _set(m, "bin_center", d["site_bin_center"])
+    # task constants (reference cited in constants.py)
+    _set(m, "start_qpos", C.SO100_START_ARM_POSE)
+    _set(m, "action_lo", [r[0] for r in C.SO100_ACTION_RANGES])
+    _set(m, "action_hi", [r[1] for r in C.SO100_ACTION_RANGES])
+    _set(m, "spawn_lo", [r[0] for r in C.SO100_BOX_SPAWN_RANGES])
+    _set(m, "spawn_hi", [r[1] for r in C.SO100_BOX_SPAWN_RANGES])
+    m.bin_hw = C.BIN_HALF_WIDTH
+    m.bin_h = C.BIN_INNER_HEIGHT
+    m.cube_half = C.CUBE_HALF
+    m.goal_threshold = C.GOAL_DISTANCE_THRESHOLD
+    m.max_reward = C.MAX_REWARD
+    # SO100GoalEnv.bin_goal_space (env.py:245-249): float32 bin_min/max (constants.py:29-30) +- 0.005
+    lo = [float(np.float32(C.bin_min[0]) + np.float32(0.005)), float(np.float32(C.bin_min[1]) + np.float32(0.005)), 0.01]
+    hi = [float(np.float32(C.bin_max[0]) - np.float32(0.005)), float(np.float32(C.bin_max[1]) - np.float32(0.005)), 0.05]
+    _set(m, "goal_bin_lo", lo)
+    _set(m, "goal_bin_hi", hi)
+    return m
+
+
+def pair_names(path=ASSET):
+    d = load_model_dict(path)
+    return [(p["name1"], p["name2"]) for p in d["pairs"]]

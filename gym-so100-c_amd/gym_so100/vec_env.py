@@ -1,0 +1,276 @@
+"""Batched SO-ARM100 envs on one MI355X: torch-ROCm tensors in, torch-ROCm tensors out.
+
+``SO100VecEnv`` is the batched form of the reference's ``SO100Env`` (gym_so100/env.py:26-185) and
+``SO100GoalEnv`` (env.py:188-409): N independent envs stepped by one HIP launch per env step
+(csrc/so100_step.hip).  Semantics kept from the reference:
+
+* actions [N,6] in [-1,1], un-normalised per joint with float32 write-back (single_arm.py:33-38);
+* 10 physics substeps per env step (control_timestep 0.02 / timestep 0.002, env.py:120-127);
+* reward ladders of the three tasks (single_arm.py), ``terminated = is_success = reward == 4``
+  (env.py:175), TimeLimit truncation at 700 / 300 steps (gym_so100/__init__.py:7,17,27);
+* so100_state observation = [box, bin, ee, qpos[:6]] float32 (env.py:137-145);
+* GoalEnv: sparse reward 0/-1 at 0.01 m, terminated = success, own 300-step truncation, lifted-goal
+  curriculum for the first 5000 steps (env.py:322-353, 372-406);
+* reset(seed=s) reproduces ``RandomState(s)`` cube spawns bit-for-bit (utils.py:18-29).
+
+Auto-reset follows the SB3/gymnasium-vector convention: when an env finishes, ``obs`` already holds
+the first observation of the next episode and ``info["final_observation"]`` the last one of the
+finished episode (mask in ``info["_final_observation"]``).
+
+Output tensors are persistent device buffers overwritten by the next ``step``/``reset``; clone them if
+you keep them across calls.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+from .model import NOBS, NQ, NV, build_model
+from .constants import GOAL_MAX_EPISODE_STEPS
+
+_MAX_STEPS = {"so100_cube_to_bin": 700, "so100_touch_cube": 300, "so100_touch_cube_sparse": 300,
+              "so100_goal": GOAL_MAX_EPISODE_STEPS}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class SO100VecEnv:
+    """N parallel SO-ARM100 envs on one GPU.
+
+    Args:
+        num_envs: number of envs on this device.
+        task: "so100_cube_to_bin" | "so100_touch_cube" | "so100_touch_cube_sparse" | "so100_goal".
+        obs_type: "so100_state" (pixel observations are out of scope).
+        device: torch device string ("cuda:0").
+        seed: base seed for in-kernel (auto-)reset spawns.
+        max_episode_steps: TimeLimit; default per task as registered by the reference.
+        autoreset: reset finished envs inside the step kernel.
+        domain_randomization: None or dict(mass=(lo,hi), friction=(lo,hi), action_noise=sigma):
+            per-env cube mass / friction scales (fixed per env) + Gaussian action noise.
+        env_offset: global index of this shard's first env (multi-GPU sharding); in-kernel seeds use
+            the global env id so trajectories do not depend on the number of GPUs.
+        iterations: PGS sweeps per substep (default: model's 100, MuJoCo's default).
+        debug: allocate the [N, 96] diagnostics buffer (contacts, forces, solver iterations).
+    """
+
+    def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
+                 max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
+                 iterations=None, debug=False):
+        torch = _torch()
+        if obs_type != "so100_state":
+            raise NotImplementedError(
+                f"obs_type={obs_type!r}: camera renders are out of scope of the GPU hot path "
+                "(DESIGN.md §7); use obs_type='so100_state'")
+        if task not in _native.TASKS:
+            raise NotImplementedError(task)    # env.py:117-118
+        self.lib = _native.load()
+        self.num_envs = int(num_envs)
+        self.task = task
+        self.obs_type = obs_type
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("SO100VecEnv runs on a HIP device (torch 'cuda' device on ROCm)")
+        self.autoreset = bool(autoreset)
+        self.max_episode_steps = _MAX_STEPS[task] if max_episode_steps is None else int(max_episode_steps)
+        self.base_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.env_offset = int(env_offset)
+        self.model = build_model(iterations=iterations)
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self._handle = self.lib.so100_create(ctypes.byref(self.model), self.num_envs, dev_index)
+        if not self._handle:
+            raise RuntimeError("so100_create failed: " + self.lib.so100_last_error().decode())
+        _native.check(self.lib.so100_configure(self._handle, _native.TASKS[task], self.max_episode_steps,
+                                               ctypes.c_uint64(self.base_seed), self.env_offset), "so100_configure")
+        n, d = self.num_envs, self.device
+        f32, i32 = torch.float32, torch.int32
+        self.qpos = torch.zeros(n, NQ, dtype=f32, device=d)
+        self.qvel = torch.zeros(n, NV, dtype=f32, device=d)
+        self.qacc_warmstart = torch.zeros(n, NV, dtype=f32, device=d)
+        self.elapsed = torch.zeros(n, dtype=i32, device=d)
+        self.episode = torch.zeros(n, dtype=i32, device=d)
+        self.actions = torch.zeros(n, 6, dtype=f32, device=d)
+        self.obs = torch.zeros(n, NOBS, dtype=f32, device=d)
+        self.reward = torch.zeros(n, dtype=f32, device=d)
+        self.terminated = torch.zeros(n, dtype=torch.bool, device=d)
+        self.truncated = torch.zeros(n, dtype=torch.bool, device=d)
+        self.success = torch.zeros(n, dtype=torch.bool, device=d)
+        self.diverged = torch.zeros(n, dtype=torch.bool, device=d)
+        self.final_obs = torch.zeros(n, NOBS, dtype=f32, device=d)
+        self.contact_bits = torch.zeros(n, dtype=i32, device=d)
+        self.is_goal = task == "so100_goal"
+        self.achieved_goal = torch.zeros(n, 3, dtype=f32, device=d) if self.is_goal else None
+        self.desired_goal = torch.zeros(n, 3, dtype=f32, device=d) if self.is_goal else None
+        self.total_steps = torch.zeros(n, dtype=i32, device=d) if self.is_goal else None
+        self.debug = torch.zeros(n, _native.SO100_DBG_STRIDE, dtype=f32, device=d) if debug else None
+        self.dr_params = None
+        self._flags = _native.SO100_FLAG_AUTORESET if self.autoreset else 0
+        if domain_randomization:
+            self.set_domain_randomization(**domain_randomization)
+        self._buf = _native.SO100Buffers()
+        self._fill_buffers()
+        self._seeds = torch.zeros(n, dtype=i32, device=d)
+        self._mask = torch.zeros(n, dtype=torch.uint8, device=d)
+
+    # ------------------------------------------------------------------ plumbing
+    def _fill_buffers(self):
+        P = _native.ptr
+        b = self._buf
+        for name in ("qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "obs", "reward", "terminated",
+                     "truncated", "success", "final_obs", "diverged", "contact_bits", "achieved_goal",
+                     "desired_goal", "total_steps", "dr_params", "debug"):
+            setattr(b, name, P(getattr(self, name)))
+        b.action = P(self.actions)
+
+    def _stream(self):
+        return _native.stream_ptr(_torch(), self.device)
+
+    def set_domain_randomization(self, mass=(0.8, 1.2), friction=(0.8, 1.2), action_noise=0.05, seed=None):
+        """Per-env cube mass scale, contact friction scale (fixed per env) and action-noise sigma."""
+        torch = _torch()
+        g = torch.Generator(device="cpu")
+        g.manual_seed(self.base_seed + 7919 * (self.env_offset + 1) if seed is None else int(seed))
+        n = self.num_envs
+        p = torch.empty(n, 4, dtype=torch.float32)
+        p[:, 0] = torch.empty(n).uniform_(mass[0], mass[1], generator=g)
+        p[:, 1] = torch.empty(n).uniform_(friction[0], friction[1], generator=g)
+        p[:, 2] = float(action_noise)
+        p[:, 3] = 0.0
+        self.dr_params = p.to(self.device)
+        self._flags |= _native.SO100_FLAG_DR
+        if hasattr(self, "_buf"):
+            self._fill_buffers()
+
+    # ------------------------------------------------------------------ API
+    def reset(self, seed=None, mask=None):
+        """Reset all envs (or those with mask[i] true).
+
+        seed: None -> in-kernel seeds from (base seed, global env id, episode);
+              int s -> env i uses RandomState(s + i) exactly like SB3's VecEnv.seed(s);
+              sequence/array/tensor of N ints -> per-env RandomState seeds.
+        """
+        torch = _torch()
+        seeds_p = None
+        if seed is not None:
+            if isinstance(seed, (int, np.integer)):
+                s = (int(seed) + np.arange(self.num_envs, dtype=np.int64)) & 0xFFFFFFFF
+            else:
+                s = np.asarray(seed.cpu() if hasattr(seed, "cpu") else seed, dtype=np.int64).reshape(-1) & 0xFFFFFFFF
+                if s.shape[0] != self.num_envs:
+                    raise ValueError("need one seed per env")
+            self._seeds.copy_(torch.from_numpy(s.astype(np.uint32).view(np.int32)))
+            seeds_p = _native.ptr(self._seeds)
+        mask_p = None
+        if mask is not None:
+            m = mask if isinstance(mask, torch.Tensor) else torch.as_tensor(np.asarray(mask))
+            self._mask.copy_(m.to(self.device).to(torch.uint8))
+            mask_p = _native.ptr(self._mask)
+        _native.check(self.lib.so100_reset(self._handle, ctypes.byref(self._buf), mask_p, seeds_p, self._stream()),
+                      "so100_reset")
+        info = {"is_success": torch.zeros_like(self.success)}
+        return self._observation(), info
+
+    def step(self, actions):
+        """actions: [N,6] (torch tensor on any device, or numpy) in [-1, 1]."""
+        torch = _torch()
+        if isinstance(actions, torch.Tensor):
+            if actions.shape != (self.num_envs, 6):
+                raise ValueError(f"actions must be [{self.num_envs}, 6], got {tuple(actions.shape)}")
+            if actions.device == self.device and actions.dtype == torch.float32 and actions.is_contiguous():
+                if actions.data_ptr() != self.actions.data_ptr():
+                    self.actions.copy_(actions)
+            else:
+                self.actions.copy_(actions.to(self.device, torch.float32))
+        else:
+            a = np.asarray(actions, dtype=np.float32)
+            if a.shape != (self.num_envs, 6):
+                raise ValueError(f"actions must be [{self.num_envs}, 6], got {a.shape}")
+            self.actions.copy_(torch.from_numpy(a))
+        _native.check(self.lib.so100_step(self._handle, ctypes.byref(self._buf), self._flags, self._stream()),
+                      "so100_step")
+        done = self.terminated | self.truncated
+        info = {"is_success": self.success, "diverged": self.diverged, "contact_bits": self.contact_bits}
+        if self.autoreset:
+            info["final_observation"] = self.final_obs
+            info["_final_observation"] = done
+        if self.is_goal:
+            info["TimeLimit.truncated"] = self.truncated
+        return self._observation(), self.reward, self.terminated, self.truncated, info
+
+    def step_async_raw(self):
+        """Launch one env step on the current stream using the actions already in ``self.actions``
+        (no argument handling, no output views) — the benchmark's hot loop."""
+        self.lib.so100_step(self._handle, ctypes.byref(self._buf), self._flags, self._stream())
+
+    def _observation(self):
+        if self.is_goal:
+            return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
+        return self.obs
+
+    def compute_reward(self, achieved_goal, desired_goal, info=None):
+        """Batched sparse GoalEnv reward on the device (env.py:341-353)."""
+        torch = _torch()
+        a = torch.as_tensor(achieved_goal, dtype=torch.float32, device=self.device).reshape(-1, 3).contiguous()
+        d = torch.as_tensor(desired_goal, dtype=torch.float32, device=self.device).reshape(-1, 3).contiguous()
+        out = torch.empty(a.shape[0], dtype=torch.float32, device=self.device)
+        _native.check(self.lib.so100_goal_reward(self._handle, a.shape[0], _native.ptr(a), _native.ptr(d),
+                                                 _native.ptr(out), self._stream()), "so100_goal_reward")
+        return out
+
+    # state access (checkpoint / teacher-forced parity tests)
+    def get_state(self):
+        return {"qpos": self.qpos.clone(), "qvel": self.qvel.clone(), "qacc_warmstart": self.qacc_warmstart.clone(),
+                "elapsed": self.elapsed.clone(), "episode": self.episode.clone()}
+
+    def set_state(self, qpos, qvel, qacc_warmstart=None, elapsed=None, episode=None):
+        torch = _torch()
+        self.qpos.copy_(torch.as_tensor(qpos, dtype=torch.float32))
+        self.qvel.copy_(torch.as_tensor(qvel, dtype=torch.float32))
+        if qacc_warmstart is not None:
+            self.qacc_warmstart.copy_(torch.as_tensor(qacc_warmstart, dtype=torch.float32))
+        if elapsed is not None:
+            self.elapsed.copy_(torch.as_tensor(elapsed, dtype=torch.int32))
+        if episode is not None:
+            self.episode.copy_(torch.as_tensor(episode, dtype=torch.int32))
+
+    # standalone ops exposed for parity tests
+    def eval_reward(self, task, cube_site, ee_site, pair_bits):
+        torch = _torch()
+        c = torch.as_tensor(cube_site, dtype=torch.float32, device=self.device).contiguous()
+        e = torch.as_tensor(ee_site, dtype=torch.float32, device=self.device).contiguous()
+        b = torch.as_tensor(np.asarray(pair_bits, dtype=np.uint32).view(np.int32), device=self.device).contiguous()
+        out = torch.empty(c.shape[0], dtype=torch.float32, device=self.device)
+        _native.check(self.lib.so100_eval_reward(self._handle, _native.TASKS[task], c.shape[0], _native.ptr(c),
+                                                 _native.ptr(e), _native.ptr(b), _native.ptr(out), self._stream()),
+                      "so100_eval_reward")
+        return out
+
+    def spawn_pose(self, seeds):
+        torch = _torch()
+        s = np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF
+        st = torch.as_tensor(s.astype(np.uint32).view(np.int32), device=self.device).contiguous()
+        out = torch.empty(len(s), 7, dtype=torch.float64, device=self.device)
+        _native.check(self.lib.so100_spawn_pose(self._handle, len(s), _native.ptr(st), _native.ptr(out),
+                                                self._stream()), "so100_spawn_pose")
+        return out
+
+    def unnormalize(self, actions):
+        torch = _torch()
+        a = torch.as_tensor(actions, dtype=torch.float32, device=self.device).reshape(-1, 6).contiguous()
+        out = torch.empty_like(a)
+        _native.check(self.lib.so100_unnormalize(self._handle, a.shape[0], _native.ptr(a), _native.ptr(out),
+                                                 self._stream()), "so100_unnormalize")
+        return out
+
+    def close(self):
+        if getattr(self, "_handle", None):
+            self.lib.so100_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,112 @@
+/* so100.h — C-ABI of the MI355X-native batched SO-ARM100 simulator (libso100_hip.so).
+ *
+ * This boundary replaces, for N envs at once, what the reference reaches through dm_control:
+ *   gym_so100/env.py:98-127   mujoco.Physics.from_xml_path + control.Environment   -> so100_create
+ *   gym_so100/env.py:148-170  SO100Env.reset (BOX_POSE, reset_context, mj_forward)  -> so100_reset
+ *   gym_so100/env.py:172-182  SO100Env.step -> control.Environment.step:
+ *        single_arm.py:33-38  before_step (unnormalize, fp32 ctrl)
+ *        env.py:174           Physics.step(10)  (mj_step2; mj_step x9; mj_step1)
+ *        single_arm.py:322-380/149-215/246-285 get_reward,  :82-114 get_observation
+ *        env.py:130-146,175   obs packing, terminated = reward == 4                 -> so100_step
+ *   gym_so100/env.py:341-353  SO100GoalEnv.compute_reward (batched)                 -> so100_goal_reward
+ *
+ * Conventions: plain pointers and sizes only; every array is DEVICE memory allocated by the caller
+ * (PyTorch-ROCm tensors in the Python layer); row-major [n_envs, dim].  Calls enqueue on `stream`
+ * (a hipStream_t, NULL = default stream) and never synchronise the host.  Status: 0 = ok, < 0 = error
+ * (message in so100_last_error()).  No C++ exceptions cross this boundary.
+ */
+#ifndef SO100_H
+#define SO100_H
+#include <stdint.h>
+#include "so100_model.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SO100_ABI_VERSION 1
+
+/* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
+#define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
+#define SO100_TASK_TOUCH_CUBE 1           /* gym_so100/SO100TouchCube-v0, TimeLimit 300 */
+#define SO100_TASK_TOUCH_CUBE_SPARSE 2    /* gym_so100/SO100TouchCubeSparse-v0, TimeLimit 300 */
+#define SO100_TASK_GOAL 3                 /* SO100GoalEnv (env.py:188-409), own 300-step limit */
+
+/* step flags */
+#define SO100_FLAG_AUTORESET 1            /* reset done envs in-kernel, final obs -> final_obs */
+#define SO100_FLAG_DR 2                   /* per-env domain randomisation (dr_params)          */
+
+typedef struct so100_buffers {
+  /* per-env state, updated in place */
+  float*    qpos;            /* [N,13]  hinges(6) cube pos(3) cube quat wxyz(4) */
+  float*    qvel;            /* [N,12]  hinges(6) cube linear(3, world) angular(3, body) */
+  float*    qacc_warmstart;  /* [N,12] */
+  int32_t*  elapsed;         /* [N]     steps in the current episode (TimeLimit counter) */
+  uint32_t* episode;         /* [N]     episodes started (drives in-kernel reset seeds) */
+  /* inputs */
+  const float* action;       /* [N,6]   in [-1,1] (action_space Box) */
+  /* outputs (any may be NULL) */
+  float*    obs;             /* [N,15]  box(3) bin(3) ee(3) qpos[:6] */
+  float*    reward;          /* [N] */
+  uint8_t*  terminated;      /* [N] */
+  uint8_t*  truncated;       /* [N] */
+  uint8_t*  success;         /* [N]     info["is_success"] */
+  float*    final_obs;       /* [N,15]  obs of the finished episode when auto-reset fired */
+  uint8_t*  diverged;        /* [N]     non-finite / exploding state detected (env reset) */
+  uint32_t* contact_bits;    /* [N]     bit p: contact pair p active after the step */
+  /* GoalEnv (task SO100_TASK_GOAL) */
+  float*    achieved_goal;   /* [N,3] */
+  float*    desired_goal;    /* [N,3] */
+  int32_t*  total_steps;     /* [N]     curriculum counter (env.py:324) */
+  /* domain randomisation (flag SO100_FLAG_DR): [N,4] = cube mass scale, friction scale,
+   * action-noise sigma, reserved */
+  const float* dr_params;
+  /* diagnostics: [N, SO100_DBG_STRIDE] floats or NULL */
+  float*    debug;
+} so100_buffers;
+
+#define SO100_DBG_STRIDE 96  /* ncon, solver_iter, improvement, nefc, qacc[12], contact(dist,fn)[16], ... */
+
+typedef struct so100_env so100_env;   /* opaque: device model copy + launch config */
+
+int         so100_abi_version(void);
+const char* so100_last_error(void);
+
+/* Upload the model (converted to fp32) to `device`.  n_envs > 0.  Returns NULL on error. */
+so100_env*  so100_create(const so100_model* model, int n_envs, int device);
+int         so100_destroy(so100_env* env);
+int         so100_num_envs(const so100_env* env);
+
+/* Task selection: task id, TimeLimit (max_episode_steps; <= 0 = none), base seed for in-kernel resets,
+ * global index of this shard's env 0 (multi-GPU sharding: in-kernel seeds use the global env id). */
+int so100_configure(so100_env* env, int task, int max_episode_steps, uint64_t base_seed, int env_offset);
+
+/* Reset the envs whose mask byte is non-zero (mask NULL = all).  seeds: [N] uint32 per-env seeds for
+ * the reference's RandomState(seed) cube spawn (utils.py:18-29), or NULL -> in-kernel seed from
+ * (base_seed, env, episode).  Writes obs (and GoalEnv goals). */
+int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, const uint32_t* seeds,
+                void* stream);
+
+/* One env step for all N envs (10 physics substeps + final position stage + reward/obs epilogue). */
+int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream);
+
+/* Batched sparse GoalEnv reward (env.py:341-353): out[i] = ||a_i - d_i|| < threshold ? 0 : -1. */
+int so100_goal_reward(so100_env* env, int n, const float* achieved, const float* desired, float* out,
+                      void* stream);
+
+/* Task reward epilogue as a standalone op (for parity against the reference's golden vectors):
+ * cube_site[n,3] fp32, ee_site[n,3] fp32, pair_bits[n] -> reward[n] fp32, using the same device
+ * function as the step kernel. */
+int so100_eval_reward(so100_env* env, int task, int n, const float* cube_site, const float* ee_site,
+                      const uint32_t* pair_bits, float* reward, void* stream);
+
+/* Reference spawn op: seeds[n] -> pose[n,7] (fp64) via device MT19937 (utils.py:18-29). */
+int so100_spawn_pose(so100_env* env, int n, const uint32_t* seeds, double* pose, void* stream);
+
+/* Action prologue as a standalone op: action[n,6] -> ctrl[n,6] (constants.py:78-86, fp32 write-back). */
+int so100_unnormalize(so100_env* env, int n, const float* action, float* ctrl, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,121 @@
+/* so100_model.h — plain-data layout of the derived SO-ARM100 bin-a-cube model.
+ *
+ * This is the ONLY structure that crosses the C-ABI at create time (so100_create, so100.h).
+ * It is filled on the host from gym_so100/assets/so100_model.json (written by
+ * tools/compile_model.py from /root/reference/gym_so100/assets/so100_transfer_cube.xml).
+ * Double precision on the host; the device copy is converted to fp32 inside so100_create.
+ *
+ * Numbering (build-owned, compact):
+ *   bodies 0 world | 1 Base (static, welded) | 2 Rotation_Pitch | 3 Upper_Arm | 4 Lower_Arm |
+ *          5 Wrist_Pitch_Roll | 6 Fixed_Jaw | 7 Moving_Jaw | 8 box (free joint)
+ *   dofs   0..5 arm hinges (Rotation, Pitch, Elbow, Wrist_Pitch, Wrist_Roll, Jaw),
+ *          6..8 cube linear (world frame), 9..11 cube angular (body frame)  (MuJoCo free-joint layout)
+ *   qpos   0..5 hinges, 6..8 cube position, 9..12 cube quaternion (w,x,y,z)
+ *   geoms  0 table | 1..4 fixed_jaw_pad_1..4 | 5..8 moving_jaw_pad_1..4 | 9 red_box | 10..14 bin walls+floor
+ *   pairs  0..7 pad-vs-red_box | 8 (red_box, table) | 9..13 (red_box, bin_*)
+ */
+#ifndef SO100_MODEL_H
+#define SO100_MODEL_H
+
+#define SO100_NBODY 9
+#define SO100_NHINGE 6
+#define SO100_NQ 13
+#define SO100_NV 12
+#define SO100_NU 6
+#define SO100_NGEOM 15
+#define SO100_NPAIR 14
+#define SO100_CUBE_BODY 8
+#define SO100_CUBE_GEOM 9
+#define SO100_PAIR_TABLE 8          /* ("red_box", "table") — single_arm.py:354 touch_table */
+#define SO100_NPAIR_GRIPPER 8       /* pairs 0..7 — single_arm.py:348-352 touch_gripper   */
+#define SO100_MAXCONPAIR 4          /* contacts kept per box-box pair (deepest + spread)  */
+#define SO100_MAXCON 16             /* contacts kept per env per position stage           */
+#define SO100_CONDIM 4              /* every in-scope pair mixes to condim 4 (cube condim=4) */
+#define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_MAXCON * SO100_CONDIM)
+#define SO100_NOBS 15               /* box(3) bin(3) ee(3) qpos(6) — env.py:137-145      */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct so100_model {
+  /* options (MuJoCo defaults + so_arm100.xml:4) */
+  double timestep;                  /* 0.002 */
+  int    nsubstep;                  /* control_timestep / timestep = 10 (env.py:120-127) */
+  int    iterations;                /* PGS sweeps (MuJoCo default 100) */
+  double tolerance;                 /* 1e-8 */
+  double impratio;                  /* 10 */
+  double gravity[3];
+  double meaninertia;               /* mean diag(M) at qpos0, scales the PGS improvement */
+
+  /* bodies */
+  int    body_parent[SO100_NBODY];
+  double body_pos[SO100_NBODY][3];
+  double body_quat[SO100_NBODY][4];
+  double body_ipos[SO100_NBODY][3];
+  double body_iquat[SO100_NBODY][4];
+  double body_mass[SO100_NBODY];
+  double body_inertia[SO100_NBODY][3];
+  double body_invweight0[SO100_NBODY][2];
+
+  /* hinges (one per arm body 2..7) */
+  int    jnt_body[SO100_NHINGE];
+  double jnt_axis[SO100_NHINGE][3];
+  double jnt_range[SO100_NHINGE][2];
+  double jnt_solref[2];
+  double jnt_solimp[5];
+
+  /* dofs */
+  double dof_armature[SO100_NV];
+  double dof_frictionloss[SO100_NV];
+  double dof_invweight0[SO100_NV];
+  double dof_solref[2];
+  double dof_solimp[5];
+
+  /* position actuators (gear 1 on hinge i) */
+  double act_kp[SO100_NU];
+  double act_kv[SO100_NU];
+  double act_forcerange[SO100_NU][2];
+  double act_ctrlrange[SO100_NU][2];
+
+  /* collision boxes: pos/quat in the body frame (world frame for body 0) */
+  int    geom_body[SO100_NGEOM];
+  double geom_pos[SO100_NGEOM][3];
+  double geom_quat[SO100_NGEOM][4];
+  double geom_size[SO100_NGEOM][3];
+
+  /* contact pairs with mixed parameters */
+  int    pair_geom1[SO100_NPAIR];
+  int    pair_geom2[SO100_NPAIR];
+  int    pair_condim[SO100_NPAIR];
+  double pair_friction[SO100_NPAIR][3];
+  double pair_solref[SO100_NPAIR][2];
+  double pair_solimp[SO100_NPAIR][5];
+  double pair_margin[SO100_NPAIR];
+
+  /* sites */
+  int    site_cube_body;
+  double site_cube_pos[3];
+  int    site_ee_body;
+  double site_ee_pos[3];
+  double bin_center[3];
+
+  /* task constants (reference file:line cited in gym_so100/constants.py) */
+  double start_qpos[SO100_NU];      /* constants.py:32-39 */
+  double action_lo[SO100_NU];       /* constants.py:78-86 */
+  double action_hi[SO100_NU];
+  double spawn_lo[3];               /* utils.py:18-22 */
+  double spawn_hi[3];
+  double bin_hw;                    /* single_arm.py:69 */
+  double bin_h;                     /* single_arm.py:70 */
+  double cube_half;                 /* single_arm.py:75 */
+  double goal_threshold;            /* env.py:252 */
+  double max_reward;                /* single_arm.py:130,227,297 */
+  double goal_bin_lo[3];            /* env.py:245-249 bin_goal_space (constants.py:29-30) */
+  double goal_bin_hi[3];
+} so100_model;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

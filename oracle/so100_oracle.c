@@ -1,0 +1,1136 @@
+/* so100_oracle.c — CPU restatement of the SO-ARM100 bin-a-cube hot path (TEST INFRASTRUCTURE).
+ *
+ * ORACLE ONLY: loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * checker.  Never linked into the product (gym-so100-c_amd/csrc).  See so100_oracle.h for what is
+ * pinned (task logic: golden vectors from the reference) and what is unpinned (MuJoCo physics).
+ *
+ * Written for clarity, not speed: generic dense matrices (12 dofs), one env per call, stage by stage
+ * in MuJoCo's order.  Each stage cites the reference call site that reaches it and the MuJoCo 3.3.3
+ * routine it restates ([3P] = third-party algorithm restated from its published behaviour).
+ */
+#include "so100_oracle.h"
+#include <math.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef so100o_real real;
+#define NV SO100_NV
+#define NB SO100_NBODY
+#define NEFC SO100_NEFC_MAX
+#define MINVAL ((real)1e-15)
+#define MINIMP ((real)0.0001)
+#define MAXIMP ((real)0.9999)
+
+/* ============================================================== small linear algebra */
+static void cross3(real r[3], const real a[3], const real b[3]) {
+  real t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static real dot3(const real a[3], const real b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static real norm3(const real a[3]) { return (real)sqrt((double)dot3(a, a)); }
+/* mat: row-major 3x3, columns are the frame axes in world coordinates (MuJoCo xmat) */
+static void mulmv3(real r[3], const real m[9], const real v[3]) {
+  real t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  real t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  real t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static void mulmtv3(real r[3], const real m[9], const real v[3]) {  /* m' v */
+  real t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  real t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  real t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static void mulmm3(real r[9], const real a[9], const real b[9]) {
+  real t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+  memcpy(r, t, sizeof(t));
+}
+static void quat_mul(real r[4], const real a[4], const real b[4]) {
+  real t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+               a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+               a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+               a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof(t));
+}
+static void quat_normalize(real q[4]) {
+  real n = (real)sqrt((double)(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]));
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  for (int i = 0; i < 4; i++) q[i] /= n;
+}
+static void quat2mat(real m[9], const real q[4]) {
+  real w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z);     m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z);     m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y);     m[7] = 2 * (y * z + w * x);     m[8] = 1 - 2 * (x * x + y * y);
+}
+static void axis_angle_quat(real q[4], const real axis[3], real ang) {
+  real s = (real)sin((double)ang * 0.5);
+  q[0] = (real)cos((double)ang * 0.5); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+static void load3(real r[3], const double v[3]) { r[0] = (real)v[0]; r[1] = (real)v[1]; r[2] = (real)v[2]; }
+static void load4(real r[4], const double v[4]) { for (int i = 0; i < 4; i++) r[i] = (real)v[i]; }
+
+/* spatial algebra, MuJoCo convention (angular; linear) — [3P] mju_crossMotion / mju_crossForce */
+static void cross_motion(real r[6], const real v[6], const real u[6]) {
+  real a[3], b[3], c[3];
+  cross3(a, v, u);
+  cross3(b, v, u + 3);
+  cross3(c, v + 3, u);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+static void cross_force(real r[6], const real v[6], const real f[6]) {
+  real a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+/* spatial inertia (I about ref point (9), m*d (3), m) times motion vector — [3P] mju_mulInertVec */
+static void mul_inert(real r[6], const real in[13], const real v[6]) {
+  real Iw[3], mdv[3], mdw[3];
+  mulmv3(Iw, in, v);
+  cross3(mdv, in + 9, v + 3);
+  cross3(mdw, in + 9, v);
+  for (int k = 0; k < 3; k++) {
+    r[k] = Iw[k] + mdv[k];
+    r[3 + k] = in[12] * v[3 + k] - mdw[k];
+  }
+}
+
+/* ============================================================== task layer (reference, double) */
+/* gym_so100/constants.py:44-47 unnormalize + :78-86 unnormalize_so100, applied in
+ * single_arm.py:33-38 to a float32 copy: every numpy op runs in float32 (python scalars are weak /
+ * value-cast), and the result is written back into the float32 array. */
+void so100o_unnormalize(const so100_model* m, const float action[6], float ctrl[6]) {
+  for (int i = 0; i < 6; i++) {
+    volatile float num = action[i];
+    volatile float t = num - (float)(-1);
+    volatile float u = t / (float)2;
+    volatile float v = u * (float)(m->action_hi[i] - m->action_lo[i]);
+    volatile float w = v + (float)m->action_lo[i];
+    float lo = (float)m->action_lo[i], hi = (float)m->action_hi[i];
+    float c = w < lo ? lo : w;
+    c = c > hi ? hi : c;
+    ctrl[i] = c;
+  }
+}
+
+/* numpy legacy RandomState(seed): init_genrand(seed) + mt19937 + 53-bit random_sample, then
+ * uniform(low, high) = low + (high-low)*u per component — utils.py:18-29 (sample_so100_box_pose). */
+typedef struct { uint32_t mt[624]; int pos; } mt19937;
+static void mt_seed(mt19937* s, uint32_t seed) {
+  s->mt[0] = seed;
+  for (int i = 1; i < 624; i++) s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+  s->pos = 624;
+}
+static uint32_t mt_next(mt19937* s) {
+  if (s->pos >= 624) {
+    for (int i = 0; i < 624; i++) {
+      uint32_t y = (s->mt[i] & 0x80000000u) | (s->mt[(i + 1) % 624] & 0x7fffffffu);
+      s->mt[i] = s->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    s->pos = 0;
+  }
+  uint32_t y = s->mt[s->pos++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+static double mt_double(mt19937* s) {
+  uint32_t a = mt_next(s) >> 5, b = mt_next(s) >> 6;
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+void so100o_spawn_pose(uint32_t seed, double pose[7]) {
+  static const double lo[3] = {-0.25, 0.3, 0.05}, hi[3] = {-0.15, 0.6, 0.05};   /* utils.py:19-21 */
+  mt19937 s;
+  mt_seed(&s, seed);
+  for (int k = 0; k < 3; k++) pose[k] = lo[k] + (hi[k] - lo[k]) * mt_double(&s);
+  pose[3] = 1; pose[4] = 0; pose[5] = 0; pose[6] = 0;                              /* utils.py:27 */
+}
+
+/* Reward ladders — single_arm.py:322-380 (CubeToBin), :149-215 (TouchCube), :246-285 (Sparse).
+ * pair_bits: bit p set iff contact pair p has >= 1 contact (pairs 0..7 = pad-vs-red_box either
+ * order -> touch_gripper; pair 8 = ("red_box","table") ordered -> touch_table). */
+double so100o_reward(const so100_model* m, int task, const float cube_f32[3], const double cube[3],
+                     const double ee[3], uint32_t pair_bits) {
+  double bmin[3], bmax[3];
+  const double hw = m->bin_hw, h = m->bin_h;                  /* single_arm.py:69-72 */
+  bmin[0] = m->bin_center[0] + -hw; bmin[1] = m->bin_center[1] + -hw; bmin[2] = m->bin_center[2] + 0.0;
+  bmax[0] = m->bin_center[0] + hw;  bmax[1] = m->bin_center[1] + hw;  bmax[2] = m->bin_center[2] + h;
+  int touch_gripper = (pair_bits & ((1u << SO100_NPAIR_GRIPPER) - 1u)) != 0;
+  int touch_table = (pair_bits >> SO100_PAIR_TABLE) & 1u;
+  if (task == SO100_TASK_CUBE_TO_BIN) {
+    /* cube_pos is float32 (get_cube_position :316-320); comparisons promote to float64 */
+    double c[3] = {cube_f32[0], cube_f32[1], cube_f32[2]};
+    int over = (bmin[0] < c[0] && c[0] < bmax[0]) && (bmin[1] < c[1] && c[1] < bmax[1]);
+    int inside = 1;
+    const float half = (float)m->cube_half;
+    for (int k = 0; k < 3; k++) {
+      volatile float lower = cube_f32[k] - half, upper = cube_f32[k] + half;   /* :78-80, float32 */
+      inside &= ((double)lower > bmin[k]) && ((double)upper < bmax[k]);
+    }
+    int released = inside && !touch_gripper;
+    double r = 0.0;
+    if (touch_gripper) r = 1.0;
+    if (touch_gripper && !touch_table) r = 2;
+    if (over) r = 2.5;
+    if (inside) r = 3;
+    if (released) r = 4.0;
+    return r;
+  }
+  double dv[3] = {ee[0] - cube[0], ee[1] - cube[1], ee[2] - cube[2]};
+  double dist = sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+  int success = touch_gripper && dist < 0.05;
+  if (task == SO100_TASK_TOUCH_CUBE_SPARSE) return success ? m->max_reward : -0.2;
+  double r = 0.0;
+  if (dist < 0.7) r = fmax(r, 0.1 * (1 - dist / 0.7));
+  if (dist < 0.5) r = fmax(r, 0.2 * (1 - dist / 0.5));
+  if (dist < 0.3) r = fmax(r, 0.5 * (1 - dist / 0.3));
+  if (dist < 0.1) r = fmax(r, 1.0 * (1 - dist / 0.1));
+  if (dist < 0.05) r = fmax(r, 2.0 * (1 - dist / 0.05));
+  if (touch_gripper) r += 1.0;
+  if (success) return m->max_reward;
+  r -= 0.2;
+  return r;
+}
+
+/* ============================================================== physics: position stage */
+/* [3P] mj_kinematics: body frames down the tree, hinge rotation about the pre-joint axis,
+ * free joint from qpos with normalised quaternion; geom/site frames. */
+static void kinematics(const so100_model* m, so100o_data* d) {
+  memset(d->xpos[0], 0, sizeof(d->xpos[0]));
+  d->xquat[0][0] = 1; d->xquat[0][1] = d->xquat[0][2] = d->xquat[0][3] = 0;
+  quat2mat(d->xmat[0], d->xquat[0]);
+  for (int b = 1; b < NB; b++) {
+    if (b == SO100_CUBE_BODY) {
+      for (int k = 0; k < 3; k++) d->xpos[b][k] = d->qpos[6 + k];
+      for (int k = 0; k < 4; k++) d->xquat[b][k] = d->qpos[9 + k];
+      quat_normalize(d->xquat[b]);
+    } else {
+      int p = m->body_parent[b];
+      real off[3], lq[4], t[3];
+      load3(off, m->body_pos[b]);
+      load4(lq, m->body_quat[b]);
+      mulmv3(t, d->xmat[p], off);
+      for (int k = 0; k < 3; k++) d->xpos[b][k] = d->xpos[p][k] + t[k];
+      quat_mul(d->xquat[b], d->xquat[p], lq);
+      for (int j = 0; j < SO100_NHINGE; j++) {
+        if (m->jnt_body[j] != b) continue;
+        real ax[3], R[9], qj[4];
+        load3(ax, m->jnt_axis[j]);
+        quat2mat(R, d->xquat[b]);
+        mulmv3(d->xaxis[j], R, ax);
+        memcpy(d->xanchor[j], d->xpos[b], sizeof(real) * 3);          /* jnt_pos = 0 */
+        axis_angle_quat(qj, ax, d->qpos[j]);                         /* qpos0 = 0 */
+        quat_mul(d->xquat[b], d->xquat[b], qj);
+      }
+      quat_normalize(d->xquat[b]);
+    }
+    quat2mat(d->xmat[b], d->xquat[b]);
+    real ip[3], iq[4], iR[9], t[3];
+    load3(ip, m->body_ipos[b]);
+    load4(iq, m->body_iquat[b]);
+    mulmv3(t, d->xmat[b], ip);
+    for (int k = 0; k < 3; k++) d->xipos[b][k] = d->xpos[b][k] + t[k];
+    quat2mat(iR, iq);
+    mulmm3(d->ximat[b], d->xmat[b], iR);
+  }
+  for (int g = 0; g < SO100_NGEOM; g++) {
+    int b = m->geom_body[g];
+    real gp[3], gq[4], gR[9], t[3];
+    load3(gp, m->geom_pos[g]);
+    load4(gq, m->geom_quat[g]);
+    mulmv3(t, d->xmat[b], gp);
+    for (int k = 0; k < 3; k++) d->geom_xpos[g][k] = d->xpos[b][k] + t[k];
+    quat2mat(gR, gq);
+    mulmm3(d->geom_xmat[g], d->xmat[b], gR);
+  }
+  real sp[3], t[3];
+  load3(sp, m->site_cube_pos);
+  mulmv3(t, d->xmat[m->site_cube_body], sp);
+  for (int k = 0; k < 3; k++) d->site_cube[k] = d->xpos[m->site_cube_body][k] + t[k];
+  load3(sp, m->site_ee_pos);
+  mulmv3(t, d->xmat[m->site_ee_body], sp);
+  for (int k = 0; k < 3; k++) d->site_ee[k] = d->xpos[m->site_ee_body][k] + t[k];
+}
+
+/* tree reference point: the xpos of the tree's root body (Base for the arm, the cube itself).
+ * MuJoCo uses subtree_com of the root; M, bias and qacc are invariant to this choice. */
+static const real* tree_ref(const so100o_data* d, int b) {
+  return b == SO100_CUBE_BODY ? d->xpos[SO100_CUBE_BODY] : d->xpos[1];
+}
+
+/* [3P] mj_comPos: cinert (com inertia about the reference point) and cdof (motion subspaces) */
+static void com_pos(const so100_model* m, so100o_data* d) {
+  for (int b = 1; b < NB; b++) {
+    const real* r = tree_ref(d, b);
+    real mass = (real)m->body_mass[b], dd[3], Ib[9], Iw[9], diag[9] = {0};
+    for (int k = 0; k < 3; k++) dd[k] = d->xipos[b][k] - r[k];
+    for (int k = 0; k < 3; k++) diag[4 * k] = (real)m->body_inertia[b][k];
+    real RT[9];
+    for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) RT[3 * i + j] = d->ximat[b][3 * j + i];
+    mulmm3(Ib, d->ximat[b], diag);
+    mulmm3(Iw, Ib, RT);
+    real dd2 = dot3(dd, dd);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        d->cinert[b][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0) - dd[i] * dd[j]);
+    for (int k = 0; k < 3; k++) d->cinert[b][9 + k] = mass * dd[k];
+    d->cinert[b][12] = mass;
+  }
+  for (int j = 0; j < SO100_NHINGE; j++) {
+    const real* r = tree_ref(d, m->jnt_body[j]);
+    real off[3];
+    for (int k = 0; k < 3; k++) off[k] = r[k] - d->xanchor[j][k];
+    for (int k = 0; k < 3; k++) d->cdof[j][k] = d->xaxis[j][k];
+    cross3(d->cdof[j] + 3, d->xaxis[j], off);
+  }
+  for (int k = 0; k < 3; k++) {          /* free joint: 3 translations (world), 3 rotations (body axes) */
+    real* ct = d->cdof[6 + k];
+    real* cr = d->cdof[9 + k];
+    memset(ct, 0, sizeof(real) * 6);
+    ct[3 + k] = 1;
+    for (int i = 0; i < 3; i++) cr[i] = d->xmat[SO100_CUBE_BODY][3 * i + k];
+    cr[3] = cr[4] = cr[5] = 0;          /* anchor == reference point */
+  }
+}
+
+static int dof_body(const so100_model* m, int j) { return j < SO100_NHINGE ? m->jnt_body[j] : SO100_CUBE_BODY; }
+/* dof ancestry: arm dofs form one chain 0<-1<-...<-5; the 6 free dofs form chain 6<-...<-11 */
+static int dof_parent(int j) { return (j == 0 || j == 6) ? -1 : j - 1; }
+
+/* [3P] mj_crb: composite inertias bottom-up, M(i,j) = cdof_j . (crb_i cdof_i) over ancestors */
+static void crb(const so100_model* m, so100o_data* d) {
+  real crbi[NB][13];
+  memcpy(crbi, d->cinert, sizeof(crbi));
+  for (int b = NB - 1; b > 1; b--) {
+    int p = m->body_parent[b];
+    if (p > 0) for (int k = 0; k < 13; k++) crbi[p][k] += crbi[b][k];
+  }
+  memset(d->qM, 0, sizeof(d->qM));
+  for (int i = 0; i < NV; i++) {
+    real F[6];
+    mul_inert(F, crbi[dof_body(m, i)], d->cdof[i]);
+    for (int j = i; j >= 0; j = dof_parent(j)) {
+      real v = 0;
+      for (int k = 0; k < 6; k++) v += d->cdof[j][k] * F[k];
+      d->qM[i][j] = v;
+      d->qM[j][i] = v;
+    }
+    d->qM[i][i] += (real)m->dof_armature[i];
+  }
+}
+
+/* [3P] mj_factorM: dense Cholesky here (MuJoCo uses sparse LDL'; same solves) */
+static void factor_m(so100o_data* d) {
+  memset(d->qL, 0, sizeof(d->qL));
+  for (int j = 0; j < NV; j++) {
+    real s = d->qM[j][j];
+    for (int k = 0; k < j; k++) s -= d->qL[j][k] * d->qL[j][k];
+    d->qL[j][j] = (real)sqrt((double)(s > MINVAL ? s : MINVAL));
+    for (int i = j + 1; i < NV; i++) {
+      real t = d->qM[i][j];
+      for (int k = 0; k < j; k++) t -= d->qL[i][k] * d->qL[j][k];
+      d->qL[i][j] = t / d->qL[j][j];
+    }
+  }
+}
+static void solve_m(const so100o_data* d, real x[NV], const real y[NV]) {
+  real z[NV];
+  for (int i = 0; i < NV; i++) {
+    real s = y[i];
+    for (int k = 0; k < i; k++) s -= d->qL[i][k] * z[k];
+    z[i] = s / d->qL[i][i];
+  }
+  for (int i = NV - 1; i >= 0; i--) {
+    real s = z[i];
+    for (int k = i + 1; k < NV; k++) s -= d->qL[k][i] * x[k];
+    x[i] = s / d->qL[i][i];
+  }
+}
+
+/* ---------------------------------------------------------------- box-box narrowphase
+ * Separating-axis test over the 15 axes, then (face case) clip the incident face against the
+ * reference face and keep penetrating points, culled to SO100_MAXCONPAIR by depth + angular spread;
+ * (edge case) one contact between the closest points of the two edges.  Normal points from geom1
+ * to geom2; contact position is midway between the surfaces; dist = -depth.  This is the standard
+ * box-box algorithm (ODE dBoxBox lineage) that MuJoCo's mjc_BoxBox also implements [3P]. */
+static int clip_rect_quad(const real h[2], const real quad[8], real out[16]) {
+  real bufa[16], bufb[16];
+  real* q = bufa;
+  real* r = bufb;
+  int nq = 4, nr = 0;
+  memcpy(q, quad, sizeof(real) * 8);
+  for (int dir = 0; dir < 2; dir++) {
+    for (int sign = -1; sign <= 1; sign += 2) {
+      nr = 0;
+      for (int i = 0; i < nq && nr < 8; i++) {
+        const real* a = q + 2 * i;
+        const real* b = q + 2 * ((i + 1) % nq);
+        int ina = sign * a[dir] < h[dir];
+        int inb = sign * b[dir] < h[dir];
+        if (ina) { r[2 * nr] = a[0]; r[2 * nr + 1] = a[1]; nr++; }
+        if (ina != inb && nr < 8) {
+          real lim = sign * h[dir];
+          r[2 * nr + 1 - dir] = a[1 - dir] + (b[1 - dir] - a[1 - dir]) / (b[dir] - a[dir]) * (lim - a[dir]);
+          r[2 * nr + dir] = lim;
+          nr++;
+        }
+      }
+      real* t = q; q = r; r = t;
+      nq = nr;
+    }
+  }
+  memcpy(out, q, sizeof(real) * 2 * nq);
+  return nq;
+}
+
+static void cull_points(int n, const real p[16], int m, int i0, int iret[]) {
+  real cx, cy;
+  if (n == 1) { cx = p[0]; cy = p[1]; }
+  else if (n == 2) { cx = (real)0.5 * (p[0] + p[2]); cy = (real)0.5 * (p[1] + p[3]); }
+  else {
+    real a = 0, q;
+    cx = 0; cy = 0;
+    for (int i = 0; i < n; i++) {
+      int j = (i + 1) % n;
+      q = p[2 * i] * p[2 * j + 1] - p[2 * j] * p[2 * i + 1];
+      a += q;
+      cx += q * (p[2 * i] + p[2 * j]);
+      cy += q * (p[2 * i + 1] + p[2 * j + 1]);
+    }
+    if (fabs((double)a) > 1e-12) { a = (real)1 / ((real)3 * a); cx *= a; cy *= a; }
+    else {
+      cx = 0; cy = 0;
+      for (int i = 0; i < n; i++) { cx += p[2 * i]; cy += p[2 * i + 1]; }
+      cx /= (real)n; cy /= (real)n;
+    }
+  }
+  real A[8];
+  int avail[8];
+  for (int i = 0; i < n; i++) { A[i] = (real)atan2((double)(p[2 * i + 1] - cy), (double)(p[2 * i] - cx)); avail[i] = 1; }
+  avail[i0] = 0;
+  iret[0] = i0;
+  const real PI = (real)3.14159265358979323846;
+  for (int j = 1; j < m; j++) {
+    real a = (real)j * (2 * PI / (real)m) + A[i0];
+    if (a > PI) a -= 2 * PI;
+    real best = (real)1e9;
+    iret[j] = i0;
+    for (int i = 0; i < n; i++) {
+      if (!avail[i]) continue;
+      real df = (real)fabs((double)(A[i] - a));
+      if (df > PI) df = 2 * PI - df;
+      if (df < best) { best = df; iret[j] = i; }
+    }
+    avail[iret[j]] = 0;
+  }
+}
+
+/* returns number of contacts written (<= SO100_MAXCONPAIR) */
+static int box_box(const real p1[3], const real R1[9], const real A[3], const real p2[3], const real R2[9],
+                   const real B[3], real margin, so100o_contact out[SO100_MAXCONPAIR]) {
+  real pd[3], pp[3], R[9], Q[9];
+  for (int k = 0; k < 3; k++) pd[k] = p2[k] - p1[k];
+  mulmtv3(pp, R1, pd);                               /* p in box1 frame */
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      R[3 * i + j] = R1[i] * R2[j] + R1[3 + i] * R2[3 + j] + R1[6 + i] * R2[6 + j];   /* a1_i . a2_j */
+      Q[3 * i + j] = (real)fabs((double)R[3 * i + j]) + (real)1e-6;
+    }
+  real best = -(real)1e30, nb[3] = {0, 0, 0};       /* nb: best normal in box1 frame (unsigned) */
+  int code = 0, invert = 0;
+  /* box1 faces */
+  for (int i = 0; i < 3; i++) {
+    real s = (real)fabs((double)pp[i]) - (A[i] + B[0] * Q[3 * i] + B[1] * Q[3 * i + 1] + B[2] * Q[3 * i + 2]);
+    if (s > margin) return 0;
+    if (s > best) { best = s; code = 1 + i; invert = pp[i] < 0; nb[0] = nb[1] = nb[2] = 0; nb[i] = 1; }
+  }
+  /* box2 faces */
+  for (int j = 0; j < 3; j++) {
+    real e = pp[0] * R[j] + pp[1] * R[3 + j] + pp[2] * R[6 + j];
+    real s = (real)fabs((double)e) - (A[0] * Q[j] + A[1] * Q[3 + j] + A[2] * Q[6 + j] + B[j]);
+    if (s > margin) return 0;
+    if (s > best) { best = s; code = 4 + j; invert = e < 0; nb[0] = R[j]; nb[1] = R[3 + j]; nb[2] = R[6 + j]; }
+  }
+  /* edge x edge: n = e_i x (R col j), in box1 frame; prefer faces unless clearly better (1.05) */
+  for (int i = 0; i < 3; i++) {
+    int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    for (int j = 0; j < 3; j++) {
+      int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      real n[3] = {0, 0, 0};
+      n[i1] = -R[3 * i2 + j];
+      n[i2] = R[3 * i1 + j];
+      real l = (real)sqrt((double)(n[i1] * n[i1] + n[i2] * n[i2]));
+      if (l < (real)1e-5) continue;
+      real e = pp[i2] * R[3 * i1 + j] - pp[i1] * R[3 * i2 + j];
+      real ex = A[i1] * Q[3 * i2 + j] + A[i2] * Q[3 * i1 + j] + B[j1] * Q[3 * i + j2] + B[j2] * Q[3 * i + j1];
+      real s = ((real)fabs((double)e) - ex) / l;
+      if (s > margin) return 0;
+      if (s * (real)1.05 > best) {
+        best = s; code = 7 + 3 * i + j; invert = e < 0;
+        nb[0] = n[0] / l; nb[1] = n[1] / l; nb[2] = n[2] / l;
+      }
+    }
+  }
+  if (code == 0) return 0;
+  real normal[3];
+  mulmv3(normal, R1, nb);
+  if (invert) { normal[0] = -normal[0]; normal[1] = -normal[1]; normal[2] = -normal[2]; }
+  const real depth0 = -best;
+
+  if (code > 6) {                                     /* edge-edge: single contact */
+    int i = (code - 7) / 3, j = (code - 7) % 3;
+    real pa[3], pb[3];
+    for (int k = 0; k < 3; k++) { pa[k] = p1[k]; pb[k] = p2[k]; }
+    for (int k = 0; k < 3; k++) {
+      if (k != i) {
+        real ax[3] = {R1[k], R1[3 + k], R1[6 + k]};
+        real sgn = dot3(normal, ax) > 0 ? (real)1 : (real)-1;
+        for (int t = 0; t < 3; t++) pa[t] += sgn * A[k] * ax[t];
+      }
+      if (k != j) {
+        real ax[3] = {R2[k], R2[3 + k], R2[6 + k]};
+        real sgn = dot3(normal, ax) > 0 ? (real)-1 : (real)1;
+        for (int t = 0; t < 3; t++) pb[t] += sgn * B[k] * ax[t];
+      }
+    }
+    real ua[3] = {R1[i], R1[3 + i], R1[6 + i]}, ub[3] = {R2[j], R2[3 + j], R2[6 + j]};
+    real pq[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    real uaub = dot3(ua, ub), q1 = dot3(ua, pq), q2 = -dot3(ub, pq);
+    real den = 1 - uaub * uaub, al = 0, be = 0;
+    if (den > (real)1e-4) { den = 1 / den; al = (q1 + uaub * q2) * den; be = (uaub * q1 + q2) * den; }
+    for (int t = 0; t < 3; t++) {
+      pa[t] += ua[t] * al;
+      pb[t] += ub[t] * be;
+      out[0].pos[t] = (real)0.5 * (pa[t] + pb[t]);
+      out[0].frame[t] = normal[t];
+    }
+    out[0].dist = -depth0;
+    return 1;
+  }
+
+  /* face case: reference box (face axis codeN), incident box */
+  const real *pR, *RR, *SR, *pI, *RI, *SI;
+  real nref[3];
+  int codeN;
+  if (code <= 3) { pR = p1; RR = R1; SR = A; pI = p2; RI = R2; SI = B; codeN = code - 1;
+                   for (int t = 0; t < 3; t++) nref[t] = normal[t]; }
+  else { pR = p2; RR = R2; SR = B; pI = p1; RI = R1; SI = A; codeN = code - 4;
+         for (int t = 0; t < 3; t++) nref[t] = -normal[t]; }
+  /* incident face: the face of the incident box most anti-parallel to nref */
+  real nr[3], anr[3];
+  for (int k = 0; k < 3; k++) { real ax[3] = {RI[k], RI[3 + k], RI[6 + k]}; nr[k] = dot3(nref, ax); anr[k] = (real)fabs((double)nr[k]); }
+  int lanr = (anr[1] > anr[0]) ? ((anr[1] > anr[2]) ? 1 : 2) : ((anr[0] > anr[2]) ? 0 : 2);
+  real center[3];
+  for (int t = 0; t < 3; t++) {
+    real ax = RI[3 * t + lanr];
+    center[t] = pI[t] - pR[t] + (nr[lanr] < 0 ? SI[lanr] : -SI[lanr]) * ax;
+  }
+  int c1 = (codeN == 0) ? 1 : 0, c2 = (codeN == 2) ? 1 : 2;
+  int a1 = (lanr == 0) ? 1 : 0, a2 = (lanr == 2) ? 1 : 2;
+  real u1[3] = {RR[c1], RR[3 + c1], RR[6 + c1]}, u2[3] = {RR[c2], RR[3 + c2], RR[6 + c2]};
+  real v1[3] = {RI[a1], RI[3 + a1], RI[6 + a1]}, v2[3] = {RI[a2], RI[3 + a2], RI[6 + a2]};
+  real cc1 = dot3(center, u1), cc2 = dot3(center, u2);
+  real m11 = dot3(u1, v1), m12 = dot3(u1, v2), m21 = dot3(u2, v1), m22 = dot3(u2, v2);
+  real k1 = m11 * SI[a1], k2 = m21 * SI[a1], k3 = m12 * SI[a2], k4 = m22 * SI[a2];
+  real quad[8] = {cc1 - k1 - k3, cc2 - k2 - k4, cc1 - k1 + k3, cc2 - k2 + k4,
+                  cc1 + k1 + k3, cc2 + k2 + k4, cc1 + k1 - k3, cc2 + k2 - k4};
+  real rect[2] = {SR[c1], SR[c2]};
+  real pts[16];
+  int n = clip_rect_quad(rect, quad, pts);
+  if (n < 1) return 0;
+  real det = m11 * m22 - m12 * m21;
+  if (fabs((double)det) < 1e-12) return 0;
+  det = 1 / det;
+  real i11 = m22 * det, i12 = -m12 * det, i21 = -m21 * det, i22 = m11 * det;
+  real P3[8][3], dep[8], P2[16];
+  int cnum = 0;
+  for (int k = 0; k < n; k++) {
+    real x = pts[2 * k] - cc1, y = pts[2 * k + 1] - cc2;
+    real s1 = i11 * x + i12 * y, s2 = i21 * x + i22 * y;
+    real pt[3];
+    for (int t = 0; t < 3; t++) pt[t] = center[t] + s1 * v1[t] + s2 * v2[t];
+    real dp = SR[codeN] - dot3(nref, pt);
+    if (dp > -margin) {
+      for (int t = 0; t < 3; t++) P3[cnum][t] = pt[t] + pR[t];
+      dep[cnum] = dp;
+      P2[2 * cnum] = pts[2 * k];
+      P2[2 * cnum + 1] = pts[2 * k + 1];
+      cnum++;
+    }
+  }
+  if (cnum < 1) return 0;
+  int idx[8], nout = cnum;
+  if (cnum > SO100_MAXCONPAIR) {
+    int i0 = 0;
+    for (int k = 1; k < cnum; k++) if (dep[k] > dep[i0]) i0 = k;
+    cull_points(cnum, P2, SO100_MAXCONPAIR, i0, idx);
+    nout = SO100_MAXCONPAIR;
+  } else {
+    for (int k = 0; k < cnum; k++) idx[k] = k;
+  }
+  for (int c = 0; c < nout; c++) {
+    int k = idx[c];
+    for (int t = 0; t < 3; t++) {
+      out[c].pos[t] = P3[k][t] + (real)0.5 * dep[k] * nref[t];
+      out[c].frame[t] = normal[t];
+    }
+    out[c].dist = -dep[k];
+  }
+  return nout;
+}
+
+/* [3P] mju_makeFrame: tangents from the normal (y-axis candidate (0,1,0) unless near-parallel) */
+static void make_frame(real f[9]) {
+  real* n = f;
+  real* t1 = f + 3;
+  real nn = norm3(n);
+  for (int k = 0; k < 3; k++) n[k] /= nn;
+  if (fabs((double)n[1]) < 0.5) { t1[0] = 0; t1[1] = 1; t1[2] = 0; }
+  else { t1[0] = 0; t1[1] = 0; t1[2] = 1; }
+  real pr = dot3(n, t1);
+  for (int k = 0; k < 3; k++) t1[k] -= pr * n[k];
+  real tn = norm3(t1);
+  for (int k = 0; k < 3; k++) t1[k] /= tn;
+  cross3(f + 6, n, t1);
+}
+
+/* [3P] mj_collision restricted to the in-scope pair table (mj_collideGeoms order: pair order, then
+ * contact order within the pair); bounding-sphere broadphase. */
+static void collision(const so100_model* m, so100o_data* d) {
+  d->ncon = 0;
+  d->ncon_dropped = 0;
+  for (int p = 0; p < SO100_NPAIR; p++) {
+    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+    real A[3], B[3];
+    load3(A, m->geom_size[g1]);
+    load3(B, m->geom_size[g2]);
+    real dp[3] = {d->geom_xpos[g2][0] - d->geom_xpos[g1][0], d->geom_xpos[g2][1] - d->geom_xpos[g1][1],
+                  d->geom_xpos[g2][2] - d->geom_xpos[g1][2]};
+    real margin = (real)m->pair_margin[p];
+    if (norm3(dp) > norm3(A) + norm3(B) + margin) continue;
+    so100o_contact tmp[SO100_MAXCONPAIR];
+    int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin, tmp);
+    for (int c = 0; c < n; c++) {
+      if (d->ncon >= SO100_MAXCON) { d->ncon_dropped++; continue; }
+      so100o_contact* con = &d->con[d->ncon++];
+      *con = tmp[c];
+      con->pair = p;
+      make_frame(con->frame);
+    }
+  }
+}
+
+uint32_t so100o_contact_bits(const so100o_data* d) {
+  uint32_t bits = 0;
+  for (int c = 0; c < d->ncon; c++) bits |= 1u << d->con[c].pair;
+  return bits;
+}
+
+/* [3P] engine_core_constraint.c getimpedance: sigmoid between dmin and dmax over |pos-margin|/width */
+static real getimpedance(const double solimp[5], real pos, real margin) {
+  real dmin = (real)solimp[0], dmax = (real)solimp[1], width = (real)solimp[2];
+  real mid = (real)solimp[3], power = (real)solimp[4];
+  dmin = dmin < MINIMP ? MINIMP : (dmin > MAXIMP ? MAXIMP : dmin);
+  dmax = dmax < MINIMP ? MINIMP : (dmax > MAXIMP ? MAXIMP : dmax);
+  mid = mid < MINIMP ? MINIMP : (mid > MAXIMP ? MAXIMP : mid);
+  if (power < 1) power = 1;
+  if (dmin == dmax || width <= MINVAL) return (real)0.5 * (dmin + dmax);
+  real x = (real)fabs((double)((pos - margin) / width));
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  real y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = (real)(pow((double)x, (double)power) / pow((double)mid, (double)(power - 1)));
+  else y = 1 - (real)(pow((double)(1 - x), (double)power) / pow((double)(1 - mid), (double)(power - 1)));
+  return dmin + y * (dmax - dmin);
+}
+static void solref_kb(const double solref[2], const double solimp[5], real timestep, real* K, real* B) {
+  real dmax = (real)solimp[1];
+  dmax = dmax < MINIMP ? MINIMP : (dmax > MAXIMP ? MAXIMP : dmax);
+  real tc = (real)solref[0], dr = (real)solref[1];
+  if (tc > 0) {
+    if (tc < 2 * timestep) tc = 2 * timestep;                          /* refsafe */
+    real den = dmax * dmax * tc * tc * dr * dr;
+    *K = 1 / (den > MINVAL ? den : MINVAL);
+    real db = dmax * tc;
+    *B = 2 / (db > MINVAL ? db : MINVAL);
+  } else {
+    *K = -tc / (dmax * dmax);
+    *B = -dr / dmax;
+  }
+}
+
+/* [3P] mj_makeConstraint + mj_makeImpedance: rows in MuJoCo order friction | limits | contacts */
+static void make_constraint(const so100_model* m, so100o_data* d) {
+  int r = 0;
+  const real h = (real)m->timestep;
+  memset(d->efc_J, 0, sizeof(d->efc_J));
+  /* dof frictionloss */
+  for (int k = 0; k < NV; k++) {
+    if (m->dof_frictionloss[k] <= 0) continue;
+    d->efc_type[r] = SO100O_EFC_FRICTION; d->efc_id[r] = k; d->efc_dim[r] = 1;
+    d->efc_J[r][k] = 1;
+    d->efc_pos[r] = 0; d->efc_margin[r] = 0;
+    d->efc_frictionloss[r] = (real)m->dof_frictionloss[k];
+    d->efc_diagApprox[r] = (real)m->dof_invweight0[k];
+    d->efc_imp[r] = getimpedance(m->dof_solimp, 0, 0);
+    solref_kb(m->dof_solref, m->dof_solimp, h, &d->efc_K[r], &d->efc_B[r]);
+    r++;
+  }
+  /* joint limits (hinges; margin 0: active iff dist < 0) */
+  for (int j = 0; j < SO100_NHINGE; j++) {
+    for (int side = 0; side < 2; side++) {
+      real dist = side == 0 ? d->qpos[j] - (real)m->jnt_range[j][0] : (real)m->jnt_range[j][1] - d->qpos[j];
+      if (!(dist < 0)) continue;
+      d->efc_type[r] = SO100O_EFC_LIMIT; d->efc_id[r] = j; d->efc_dim[r] = 1;
+      d->efc_J[r][j] = side == 0 ? 1 : -1;
+      d->efc_pos[r] = dist; d->efc_margin[r] = 0; d->efc_frictionloss[r] = 0;
+      d->efc_diagApprox[r] = (real)m->dof_invweight0[j];
+      d->efc_imp[r] = getimpedance(m->jnt_solimp, dist, 0);
+      solref_kb(m->jnt_solref, m->jnt_solimp, h, &d->efc_K[r], &d->efc_B[r]);
+      r++;
+    }
+  }
+  /* contacts: condim 4 elliptic, J rows = frame . (jac(body2) - jac(body1)) at the contact point */
+  for (int c = 0; c < d->ncon; c++) {
+    const so100o_contact* con = &d->con[c];
+    int p = con->pair;
+    int b1 = m->geom_body[m->pair_geom1[p]], b2 = m->geom_body[m->pair_geom2[p]];
+    real jp[3][NV], jr[3][NV];                     /* jac difference body2 - body1 */
+    memset(jp, 0, sizeof(jp)); memset(jr, 0, sizeof(jr));
+    for (int side = 0; side < 2; side++) {
+      int b = side ? b2 : b1;
+      real sg = side ? (real)1 : (real)-1;
+      if (b == 0 || b == 1) continue;              /* world / static Base: no dofs */
+      if (b == SO100_CUBE_BODY) {
+        real off[3];
+        for (int t = 0; t < 3; t++) off[t] = con->pos[t] - d->xpos[b][t];
+        for (int k = 0; k < 3; k++) {
+          jp[k][6 + k] += sg;
+          real ax[3] = {d->xmat[b][k], d->xmat[b][3 + k], d->xmat[b][6 + k]}, v[3];
+          cross3(v, ax, off);
+          for (int t = 0; t < 3; t++) { jp[t][9 + k] += sg * v[t]; jr[t][9 + k] += sg * ax[t]; }
+        }
+      } else {
+        for (int j = 0; j < SO100_NHINGE; j++) {
+          int a = b;                                 /* is hinge j an ancestor-or-self of b ? */
+          while (a > 1 && a != m->jnt_body[j]) a = m->body_parent[a];
+          if (a != m->jnt_body[j]) continue;
+          real off[3], v[3];
+          for (int t = 0; t < 3; t++) off[t] = con->pos[t] - d->xanchor[j][t];
+          cross3(v, d->xaxis[j], off);
+          for (int t = 0; t < 3; t++) { jp[t][j] += sg * v[t]; jr[t][j] += sg * d->xaxis[j][t]; }
+        }
+      }
+    }
+    const int dim = m->pair_condim[p];
+    real tran = (real)(m->body_invweight0[b1][0] + m->body_invweight0[b2][0]);
+    real rot = (real)(m->body_invweight0[b1][1] + m->body_invweight0[b2][1]);
+    real imp = getimpedance(m->pair_solimp[p], con->dist, (real)m->pair_margin[p]);
+    real K, B;
+    solref_kb(m->pair_solref[p], m->pair_solimp[p], h, &K, &B);
+    real mu[3] = {(real)m->pair_friction[p][0], (real)m->pair_friction[p][0], (real)m->pair_friction[p][1]};
+    for (int k = 0; k < dim; k++) {
+      int row = r + k;
+      d->efc_type[row] = SO100O_EFC_CONTACT; d->efc_id[row] = c; d->efc_dim[row] = k == 0 ? dim : 0;
+      for (int v = 0; v < NV; v++) {
+        if (k < 3) {
+          const real* ax = con->frame + 3 * k;
+          d->efc_J[row][v] = ax[0] * jp[0][v] + ax[1] * jp[1][v] + ax[2] * jp[2][v];
+        } else {
+          d->efc_J[row][v] = con->frame[0] * jr[0][v] + con->frame[1] * jr[1][v] + con->frame[2] * jr[2][v];
+        }
+      }
+      d->efc_pos[row] = k == 0 ? con->dist : 0;
+      d->efc_margin[row] = k == 0 ? (real)m->pair_margin[p] : 0;
+      d->efc_frictionloss[row] = 0;
+      d->efc_diagApprox[row] = k < 3 ? tran : rot;
+      d->efc_imp[row] = imp;
+      d->efc_K[row] = K; d->efc_B[row] = B;
+      d->efc_mu[row][0] = mu[0]; d->efc_mu[row][1] = mu[1]; d->efc_mu[row][2] = mu[2];
+    }
+    r += dim;
+  }
+  d->nefc = r;
+  /* impedance -> regulariser R = (1-imp)/imp * diagApprox; elliptic friction rows:
+   * R_j = R_normal * mu_0^2 / (mu_j^2 * impratio) */
+  for (int i = 0; i < r; i++) {
+    real imp = d->efc_imp[i];
+    real Ri = (1 - imp) / imp * d->efc_diagApprox[i];
+    d->efc_R[i] = Ri > MINVAL ? Ri : MINVAL;
+  }
+  for (int i = 0; i < r; i++) {
+    if (d->efc_type[i] != SO100O_EFC_CONTACT || d->efc_dim[i] < 2) continue;
+    const int dim = d->efc_dim[i];
+    for (int k = 1; k < dim; k++) {
+      real mk = d->efc_mu[i][k - 1];
+      d->efc_R[i + k] = d->efc_R[i] * d->efc_mu[i][0] * d->efc_mu[i][0] / (mk * mk * (real)m->impratio);
+    }
+  }
+  for (int i = 0; i < r; i++) d->efc_D[i] = 1 / d->efc_R[i];
+}
+
+void so100o_fwd_position(const so100_model* m, so100o_data* d) {
+  kinematics(m, d);
+  com_pos(m, d);
+  crb(m, d);
+  factor_m(d);
+  collision(m, d);
+  make_constraint(m, d);
+}
+
+/* ============================================================== physics: velocity stage */
+/* [3P] mj_comVel (incl. the free-joint cdof_dot special case) + mj_rne(flg_acc=0) */
+void so100o_fwd_velocity(const so100_model* m, so100o_data* d) {
+  memset(d->cvel, 0, sizeof(d->cvel));
+  for (int b = 1; b < NB; b++) {
+    int p = m->body_parent[b];
+    for (int k = 0; k < 6; k++) d->cvel[b][k] = d->cvel[p][k];
+    if (b == SO100_CUBE_BODY) {
+      for (int j = 6; j < 9; j++) {
+        memset(d->cdof_dot[j], 0, sizeof(real) * 6);
+        for (int k = 0; k < 6; k++) d->cvel[b][k] += d->cdof[j][k] * d->qvel[j];
+      }
+      for (int j = 9; j < 12; j++) cross_motion(d->cdof_dot[j], d->cvel[b], d->cdof[j]);
+      for (int j = 9; j < 12; j++) for (int k = 0; k < 6; k++) d->cvel[b][k] += d->cdof[j][k] * d->qvel[j];
+    } else {
+      for (int j = 0; j < SO100_NHINGE; j++) {
+        if (m->jnt_body[j] != b) continue;
+        for (int k = 0; k < 6; k++) d->cvel[b][k] += d->cdof[j][k] * d->qvel[j];
+        cross_motion(d->cdof_dot[j], d->cvel[b], d->cdof[j]);
+      }
+    }
+  }
+  /* RNE */
+  real cacc[NB][6], cfrc[NB][6];
+  memset(cacc, 0, sizeof(cacc));
+  for (int k = 0; k < 3; k++) cacc[0][3 + k] = -(real)m->gravity[k];
+  for (int b = 1; b < NB; b++) {
+    int p = m->body_parent[b];
+    for (int k = 0; k < 6; k++) cacc[b][k] = cacc[p][k];
+    for (int j = 0; j < NV; j++)
+      if (dof_body(m, j) == b) for (int k = 0; k < 6; k++) cacc[b][k] += d->cdof_dot[j][k] * d->qvel[j];
+    real f1[6], Iv[6], f2[6];
+    mul_inert(f1, d->cinert[b], cacc[b]);
+    mul_inert(Iv, d->cinert[b], d->cvel[b]);
+    cross_force(f2, d->cvel[b], Iv);
+    for (int k = 0; k < 6; k++) cfrc[b][k] = f1[k] + f2[k];
+  }
+  for (int b = NB - 1; b > 0; b--) {
+    int p = m->body_parent[b];
+    if (p > 0) for (int k = 0; k < 6; k++) cfrc[p][k] += cfrc[b][k];
+  }
+  for (int j = 0; j < NV; j++) {
+    real v = 0;
+    for (int k = 0; k < 6; k++) v += d->cdof[j][k] * cfrc[dof_body(m, j)][k];
+    d->qfrc_bias[j] = v;
+  }
+  for (int i = 0; i < d->nefc; i++) {
+    real v = 0;
+    for (int k = 0; k < NV; k++) v += d->efc_J[i][k] * d->qvel[k];
+    d->efc_vel[i] = v;
+  }
+}
+
+/* ============================================================== physics: acceleration stage */
+/* [3P] mj_QCQP2/3: min 0.5 x'Ax + x'b  s.t. sum (x_i/d_i)^2 <= r^2, Newton on the multiplier */
+static int qcqp(int n, real x[3], const real Ain[3][3], const real bin[3], const real dd[3], real r) {
+  real A[3][3], b[3], y[3], la = 0;
+  for (int i = 0; i < n; i++) {
+    b[i] = bin[i] * dd[i];
+    for (int j = 0; j < n; j++) A[i][j] = Ain[i][j] * dd[i] * dd[j];
+  }
+  for (int it = 0; it < 20; it++) {
+    real P[3][3], Pi[3][3];
+    for (int i = 0; i < n; i++) for (int j = 0; j < n; j++) P[i][j] = A[i][j] + (i == j ? la : 0);
+    real det;
+    if (n == 2) {
+      det = P[0][0] * P[1][1] - P[0][1] * P[1][0];
+      if (det < MINVAL) { for (int i = 0; i < n; i++) x[i] = 0; return 0; }
+      real id = 1 / det;
+      Pi[0][0] = P[1][1] * id; Pi[1][1] = P[0][0] * id; Pi[0][1] = -P[0][1] * id; Pi[1][0] = -P[1][0] * id;
+    } else {
+      Pi[0][0] = P[1][1] * P[2][2] - P[1][2] * P[2][1];
+      Pi[0][1] = P[0][2] * P[2][1] - P[0][1] * P[2][2];
+      Pi[0][2] = P[0][1] * P[1][2] - P[0][2] * P[1][1];
+      Pi[1][0] = P[1][2] * P[2][0] - P[1][0] * P[2][2];
+      Pi[1][1] = P[0][0] * P[2][2] - P[0][2] * P[2][0];
+      Pi[1][2] = P[0][2] * P[1][0] - P[0][0] * P[1][2];
+      Pi[2][0] = P[1][0] * P[2][1] - P[1][1] * P[2][0];
+      Pi[2][1] = P[0][1] * P[2][0] - P[0][0] * P[2][1];
+      Pi[2][2] = P[0][0] * P[1][1] - P[0][1] * P[1][0];
+      det = P[0][0] * Pi[0][0] + P[0][1] * Pi[1][0] + P[0][2] * Pi[2][0];
+      if (det < MINVAL) { for (int i = 0; i < n; i++) x[i] = 0; return 0; }
+      real id = 1 / det;
+      for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) Pi[i][j] *= id;
+    }
+    for (int i = 0; i < n; i++) {
+      real s = 0;
+      for (int j = 0; j < n; j++) s -= Pi[i][j] * b[j];
+      y[i] = s;
+    }
+    real yy = 0;
+    for (int i = 0; i < n; i++) yy += y[i] * y[i];
+    real val = yy - r * r;
+    if (val < (real)1e-10) break;
+    real Py[3], deriv = 0;
+    for (int i = 0; i < n; i++) { Py[i] = 0; for (int j = 0; j < n; j++) Py[i] += Pi[i][j] * y[j]; }
+    for (int i = 0; i < n; i++) deriv += y[i] * Py[i];
+    deriv *= -2;
+    real delta = -val / deriv;
+    if (delta < (real)1e-10) break;
+    la += delta;
+  }
+  for (int i = 0; i < n; i++) x[i] = y[i] * dd[i];
+  return la != 0;
+}
+
+/* [3P] mj_constraintUpdate (dual force from jar = J qacc - aref), used for the PGS warmstart */
+static void force_from_jar(const so100_model* m, const so100o_data* d, const real* jar, real* f) {
+  for (int i = 0; i < d->nefc;) {
+    int t = d->efc_type[i];
+    if (t == SO100O_EFC_FRICTION) {
+      real fl = d->efc_frictionloss[i], R = d->efc_R[i];
+      if (jar[i] <= -R * fl) f[i] = fl;
+      else if (jar[i] >= R * fl) f[i] = -fl;
+      else f[i] = -d->efc_D[i] * jar[i];
+      i++;
+    } else if (t == SO100O_EFC_LIMIT) {
+      f[i] = jar[i] < 0 ? -d->efc_D[i] * jar[i] : 0;
+      i++;
+    } else {
+      int dim = d->efc_dim[i];
+      real mu = d->efc_mu[i][0] * (real)sqrt((double)(d->efc_R[i + 1] / d->efc_R[i]));
+      real U[4], T = 0;
+      U[0] = jar[i] * mu;
+      for (int k = 1; k < dim; k++) { U[k] = jar[i + k] * d->efc_mu[i][k - 1]; T += U[k] * U[k]; }
+      T = (real)sqrt((double)T);
+      real N = U[0];
+      if (N >= mu * T || (T <= 0 && N >= 0)) {
+        for (int k = 0; k < dim; k++) f[i + k] = 0;
+      } else if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+        for (int k = 0; k < dim; k++) f[i + k] = -d->efc_D[i + k] * jar[i + k];
+      } else {
+        real Dm = d->efc_D[i] / (mu * mu * (1 + mu * mu));
+        real NmT = N - mu * T;
+        f[i] = -Dm * NmT * mu;
+        for (int k = 1; k < dim; k++) f[i + k] = -f[i] / T * U[k] * d->efc_mu[i][k - 1];
+      }
+      i += dim;
+    }
+  }
+}
+
+/* [3P] mj_solPGS: projected Gauss-Seidel on the dual, elliptic contact blocks (normal first, then
+ * friction by QCQP), improvement-based termination scaled by 1/(meaninertia*nv). */
+static void sol_pgs(const so100_model* m, so100o_data* d) {
+  const int nefc = d->nefc;
+  real* f = d->efc_force;
+  const real scale = 1 / ((real)m->meaninertia * (real)NV);
+  d->solver_iter = 0;
+  d->solver_improvement = 0;
+  for (int it = 0; it < m->iterations; it++) {
+    real improvement = 0;
+    for (int i = 0; i < nefc;) {
+      int dim = d->efc_type[i] == SO100O_EFC_CONTACT ? d->efc_dim[i] : 1;
+      real res[4], old[4];
+      for (int k = 0; k < dim; k++) {
+        real s = d->efc_b[i + k];
+        for (int j = 0; j < nefc; j++) s += d->efc_AR[i + k][j] * f[j];
+        res[k] = s;
+        old[k] = f[i + k];
+      }
+      if (dim == 1) {
+        f[i] -= res[0] / d->efc_AR[i][i];
+        if (d->efc_type[i] == SO100O_EFC_FRICTION) {
+          real fl = d->efc_frictionloss[i];
+          f[i] = f[i] < -fl ? -fl : (f[i] > fl ? fl : f[i]);
+        } else if (f[i] < 0) {
+          f[i] = 0;
+        }
+      } else {
+        f[i] -= res[0] / d->efc_AR[i][i];
+        if (f[i] < MINVAL) {
+          f[i] = 0;
+          for (int k = 1; k < dim; k++) f[i + k] = 0;
+        } else {
+          real Af[3][3], bf[3], x[3];
+          int nf = dim - 1;
+          for (int a = 0; a < nf; a++) {
+            bf[a] = res[1 + a] + d->efc_AR[i + 1 + a][i] * (f[i] - old[0]);
+            for (int c = 0; c < nf; c++) {
+              Af[a][c] = d->efc_AR[i + 1 + a][i + 1 + c];
+              bf[a] -= Af[a][c] * old[1 + c];
+            }
+          }
+          qcqp(nf, x, Af, bf, d->efc_mu[i], f[i]);
+          for (int a = 0; a < nf; a++) f[i + 1 + a] = x[a];
+        }
+      }
+      real delta[4];
+      for (int k = 0; k < dim; k++) delta[k] = f[i + k] - old[k];
+      for (int k = 0; k < dim; k++) {
+        real q = 0;
+        for (int c = 0; c < dim; c++) q += d->efc_AR[i + k][i + c] * delta[c];
+        improvement -= delta[k] * (res[k] + (real)0.5 * q);
+      }
+      i += dim;
+    }
+    improvement *= scale;
+    d->solver_iter = it + 1;
+    d->solver_improvement = improvement;
+    if (improvement < (real)m->tolerance) break;
+  }
+}
+
+void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
+  /* [3P] mj_fwdActuation: position actuator, ctrl clamped to ctrlrange, force clamped to forcerange */
+  memset(d->qfrc_actuator, 0, sizeof(d->qfrc_actuator));
+  for (int i = 0; i < SO100_NU; i++) {
+    real c = d->ctrl[i];
+    real lo = (real)m->act_ctrlrange[i][0], hi = (real)m->act_ctrlrange[i][1];
+    c = c < lo ? lo : (c > hi ? hi : c);
+    real kp = (real)m->act_kp[i], kv = (real)m->act_kv[i];
+    real fo = kp * c - kp * d->qpos[i] - kv * d->qvel[i];
+    real flo = (real)m->act_forcerange[i][0], fhi = (real)m->act_forcerange[i][1];
+    fo = fo < flo ? flo : (fo > fhi ? fhi : fo);
+    d->actuator_force[i] = fo;
+    d->qfrc_actuator[i] = fo;
+  }
+  /* [3P] mj_fwdAcceleration: qacc_smooth = M^-1 (qfrc_actuator - qfrc_bias) (no passive forces) */
+  real rhs[NV];
+  for (int k = 0; k < NV; k++) rhs[k] = d->qfrc_actuator[k] - d->qfrc_bias[k];
+  solve_m(d, d->qacc_smooth, rhs);
+  const int nefc = d->nefc;
+  if (nefc == 0) { memcpy(d->qacc, d->qacc_smooth, sizeof(d->qacc)); d->solver_iter = 0; return; }
+  /* [3P] mj_referenceConstraint + mj_projectConstraint: aref, b, AR = J M^-1 J' + R */
+  static __thread real MJT[NEFC][NV];
+  for (int i = 0; i < nefc; i++) {
+    d->efc_aref[i] = -d->efc_B[i] * d->efc_vel[i] - d->efc_K[i] * d->efc_imp[i] * (d->efc_pos[i] - d->efc_margin[i]);
+    real s = 0;
+    for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * d->qacc_smooth[k];
+    d->efc_b[i] = s - d->efc_aref[i];
+    solve_m(d, MJT[i], d->efc_J[i]);
+  }
+  for (int i = 0; i < nefc; i++)
+    for (int j = 0; j < nefc; j++) {
+      real s = 0;
+      for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * MJT[j][k];
+      d->efc_AR[i][j] = s + (i == j ? d->efc_R[i] : 0);
+    }
+  /* [3P] warmstart (mj_fwdConstraint, dual solver): force from jar(qacc_warmstart); keep it only if
+   * its dual cost 0.5 f'ARf + f'b is not positive */
+  real jar[NEFC];
+  for (int i = 0; i < nefc; i++) {
+    real s = 0;
+    for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * d->qacc_warmstart[k];
+    jar[i] = s - d->efc_aref[i];
+  }
+  force_from_jar(m, d, jar, d->efc_force);
+  real cost = 0;
+  for (int i = 0; i < nefc; i++) {
+    real s = 0;
+    for (int j = 0; j < nefc; j++) s += d->efc_AR[i][j] * d->efc_force[j];
+    cost += d->efc_force[i] * ((real)0.5 * s + d->efc_b[i]);
+  }
+  if (cost > 0) memset(d->efc_force, 0, sizeof(real) * nefc);
+  sol_pgs(m, d);
+  /* qacc = qacc_smooth + M^-1 J' f */
+  for (int k = 0; k < NV; k++) {
+    real s = 0;
+    for (int i = 0; i < nefc; i++) s += MJT[i][k] * d->efc_force[i];
+    d->qacc[k] = d->qacc_smooth[k] + s;
+  }
+}
+
+/* [3P] mj_Euler (no dof damping) -> mj_advance: qvel += h qacc; integratePos with the NEW qvel;
+ * free-joint quaternion via mju_quatIntegrate (body-frame angular velocity); warmstart = qacc */
+void so100o_euler(const so100_model* m, so100o_data* d) {
+  const real h = (real)m->timestep;
+  for (int k = 0; k < NV; k++) d->qvel[k] += h * d->qacc[k];
+  for (int k = 0; k < SO100_NHINGE; k++) d->qpos[k] += h * d->qvel[k];
+  for (int k = 0; k < 3; k++) d->qpos[6 + k] += h * d->qvel[6 + k];
+  real w[3] = {d->qvel[9], d->qvel[10], d->qvel[11]};
+  real nw = norm3(w);
+  if (nw > MINVAL) {
+    real ax[3] = {w[0] / nw, w[1] / nw, w[2] / nw}, qr[4];
+    axis_angle_quat(qr, ax, h * nw);
+    quat_mul(d->qpos + 9, d->qpos + 9, qr);
+  }
+  quat_normalize(d->qpos + 9);
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(d->qacc));
+}
+
+void so100o_substep(const so100_model* m, so100o_data* d) {
+  so100o_fwd_position(m, d);
+  so100o_fwd_velocity(m, d);
+  so100o_fwd_acceleration(m, d);
+  so100o_euler(m, d);
+}
+
+/* ============================================================== env layer */
+/* SO100CubeToBinTask.initialize_episode (single_arm.py:299-309) inside physics.reset_context():
+ * mj_resetData (qvel = 0, warmstart = 0) then qpos[:6] = start pose, ctrl = start pose, cube pose. */
+void so100o_reset(const so100_model* m, so100o_data* d, const double box_pose[7]) {
+  memset(d, 0, sizeof(*d));
+  for (int k = 0; k < 6; k++) { d->qpos[k] = (real)m->start_qpos[k]; d->ctrl[k] = (real)m->start_qpos[k]; }
+  for (int k = 0; k < 7; k++) d->qpos[6 + k] = (real)box_pose[k];
+  so100o_fwd_position(m, d);
+  so100o_fwd_velocity(m, d);
+}
+
+/* _format_raw_obs so100_state (env.py:137-145): box, bin, ee positions and qpos[:6], float32 */
+void so100o_observe(const so100_model* m, const so100o_data* d, float obs[SO100_NOBS]) {
+  for (int k = 0; k < 3; k++) {
+    obs[k] = (float)d->site_cube[k];
+    obs[3 + k] = (float)m->bin_center[k];
+    obs[6 + k] = (float)d->site_ee[k];
+  }
+  for (int k = 0; k < 6; k++) obs[9 + k] = (float)d->qpos[k];
+}
+
+double so100o_env_step(const so100_model* m, so100o_data* d, int task, const float action[6],
+                       float obs[SO100_NOBS], int* terminated) {
+  float ctrl[6];
+  so100o_unnormalize(m, action, ctrl);
+  for (int k = 0; k < 6; k++) d->ctrl[k] = (real)ctrl[k];
+  for (int s = 0; s < m->nsubstep; s++) so100o_substep(m, d);
+  so100o_fwd_position(m, d);                         /* dm_control legacy step ends with mj_step1 */
+  so100o_fwd_velocity(m, d);
+  float cube_f[3] = {(float)d->site_cube[0], (float)d->site_cube[1], (float)d->site_cube[2]};
+  double cube[3] = {(double)d->site_cube[0], (double)d->site_cube[1], (double)d->site_cube[2]};
+  double ee[3] = {(double)d->site_ee[0], (double)d->site_ee[1], (double)d->site_ee[2]};
+  double r = so100o_reward(m, task, cube_f, cube, ee, so100o_contact_bits(d));
+  so100o_observe(m, d, obs);
+  d->elapsed_steps++;
+  if (terminated) *terminated = (r == 4);
+  return r;
+}
+
+long so100o_batch_run(const so100_model* m, so100o_data* datas, int nenv, int steps, int task,
+                      const float* actions, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int e = 0; e < nenv; e++) {
+    float obs[SO100_NOBS];
+    int term;
+    for (int s = 0; s < steps; s++)
+      so100o_env_step(m, &datas[e], task, actions + ((size_t)s * nenv + e) * 6, obs, &term);
+  }
+  return (long)nenv * steps;
+}
+
+int so100o_sizeof_data(void) { return (int)sizeof(so100o_data); }
+int so100o_real_bytes(void) { return (int)sizeof(real); }
