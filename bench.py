@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: env steps/sec (whole node) for 65,536 parallel bin-a-cube envs on 1/2/4/8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--total-envs 65536 | --envs-per-gpu E]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one batched env step of every env on every GPU: action prologue, 10 physics substeps
+(kinematics, CRBA/RNE, box-box contacts, PGS, semi-implicit Euler), the final position stage,
+reward/obs epilogue, TimeLimit + in-kernel auto-reset — one HIP launch per GPU per step.
+Envs are sharded contiguously (global ids drive the seeds); there is no collective on the data path:
+only the barrier + max-over-ranks timing reduction around the timed region.
+Rank 0 prints ONE JSON line.  See DESIGN.md §6 for the roofline bytes and the CPU baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
+
+METRIC = "env steps/sec (whole node), 65k parallel bin-a-cube envs at 1/2/4/8 MI355X"
+# algorithmic HBM bytes per env step: reads action 24 + qpos 52 + qvel 48 + warmstart 48
+# + elapsed 4 + episode 4 = 180; writes qpos 52 + qvel 48 + warmstart 48 + obs 60 + reward 4 +
+# terminated/truncated/success/diverged 4 + contact_bits 4 + elapsed 4 + episode 4 = 228.
+BYTES_PER_ENV_STEP = 408
+HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def shard(total, world, rank):
+    """Contiguous env shard [offset, offset+count) of rank (remainder spread over the first ranks)."""
+    base, rem = divmod(total, world)
+    count = base + (1 if rank < rem else 0)
+    offset = rank * base + min(rank, rem)
+    return offset, count
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--warmup", type=int, default=30)
+    p.add_argument("--total-envs", type=int, default=65536)
+    p.add_argument("--envs-per-gpu", type=int, default=0, help="weak scaling: fixed envs per GPU")
+    p.add_argument("--task", default="so100_cube_to_bin")
+    p.add_argument("--action-pool", type=int, default=16)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample duration")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args(argv)
+
+
+def cpu_baseline(seconds):
+    """Time the oracle (fp64 C restatement, OpenMP over envs) on this host's cores — a reported,
+    non-target baseline (the reference's MuJoCo is not installed here)."""
+    import ctypes
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import Oracle
+    from gym_so100.model import build_model
+    o = Oracle(64)
+    m = build_model()
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    nenv = 4 * cores
+    datas = (o.Data * nenv)()
+    for i in range(nenv):
+        o.reset(m, datas[i], o.spawn_pose(1000 + i))
+    rng = np.random.default_rng(0)
+    steps_per_call = 5
+    done, t_used = 0, 0.0
+    while t_used < seconds:
+        acts = rng.uniform(-1, 1, size=(steps_per_call, nenv, 6)).astype(np.float32)
+        t0 = time.perf_counter()
+        done += o.batch_run(m, datas, nenv, steps_per_call, 0, acts, nthreads=cores)
+        t_used += time.perf_counter() - t0
+    return {"value": done / t_used, "unit": "env_steps/s", "cores": cores, "kind": "port",
+            "sample": f"{nenv} CubeToBin envs x {done // nenv} steps (fp64 oracle, OpenMP {cores} threads, "
+                      f"{t_used:.1f}s)"}
+
+
+def load_traffic(n_envs):
+    """HBM traffic per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if int(d.get("n_envs", -1)) != n_envs:
+            return None
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main(argv=None):
+    args = parse(argv)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    if args.envs_per_gpu > 0:
+        count, offset = args.envs_per_gpu, rank * args.envs_per_gpu
+        total = count * world
+        scaling = "weak"
+    else:
+        total = args.total_envs
+        offset, count = shard(total, world, rank)
+        scaling = "strong"
+
+    from gym_so100 import SO100VecEnv
+    env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset)
+    env.reset(seed=1000 + offset)   # env i <- RandomState(1000 + global id)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed * 1000003 + rank)
+    pool = [torch.rand(count, 6, generator=g, device=dev) * 2 - 1 for _ in range(args.action_pool)]
+    stream = torch.cuda.current_stream(dev)
+
+    for i in range(args.warmup):
+        env.set_action_buffer(pool[i % len(pool)])
+        env.step_async_raw()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(args.steps):
+        env.set_action_buffer(pool[i % len(pool)])
+        env.step_async_raw()
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms = ev[0].elapsed_time(ev[1]) / args.steps     # one step kernel per step on this stream
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    # sanity: the state stayed finite
+    assert torch.isfinite(env.qpos).all().item(), "non-finite state after the benchmark"
+
+    if rank == 0:
+        env_steps = total * args.steps
+        value = env_steps / elapsed
+        achieved = BYTES_PER_ENV_STEP * count / (kernel_ms * 1e-3)
+        traffic = load_traffic(count)
+        line = {
+            "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": (f"configs[2]: {total} bin-a-cube envs sharded over {world} GPU(s) "
+                                    f"({count} per GPU), joint-space ctrl, fp32 state, CubeToBin reward, "
+                                    "auto-reset"),
+                       "envs_total": total, "envs_per_gpu": count, "task": args.task, "substeps": 10,
+                       "pgs_iterations": env.model.iterations, "parallelism": f"env-sharded x{world}, no collectives",
+                       "actions": "U[-1,1]^6 pool resident in HBM"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK,
+                         "traffic": traffic,
+                         "kernel_ms": kernel_ms, "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                         "note": "step kernel is VALU/latency-bound (DESIGN.md §6); HBM fraction reported per north_star"},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            except Exception as e:   # baseline is reported, never required for the GPU number
+                line["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -206,6 +206,7 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->start_qpos[i] = (float)s->start_qpos[i];
     d->action_lo[i] = (float)s->action_lo[i];
     d->action_hi[i] = (float)s->action_hi[i];
+    d->action_span[i] = (float)(s->action_hi[i] - s->action_lo[i]);
   }
   return 0;
 }
@@ -215,6 +216,12 @@ extern "C" {
 
 int so100_abi_version(void) { return SO100_ABI_VERSION; }
 const char* so100_last_error(void) { return g_err.c_str(); }
+
+int so100_struct_sizes(int* model_bytes, int* buffers_bytes) {
+  if (model_bytes) *model_bytes = (int)sizeof(so100_model);
+  if (buffers_bytes) *buffers_bytes = (int)sizeof(so100_buffers);
+  return 0;
+}
 
 so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (!model) { fail("so100_create: model is NULL"); return nullptr; }

@@ -78,7 +78,7 @@ struct DevModel {
   double goal_threshold;
   double max_reward;
   float start_qpos[6];
-  float action_lo[6], action_hi[6];
+  float action_lo[6], action_hi[6], action_span[6];
   double spawn_lo[3], spawn_hi[3];
   float goal_bin_lo[3], goal_bin_hi[3];   // env.py:245-249
 };

@@ -27,6 +27,31 @@ constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;
 
 // ------------------------------------------------------------------ LDS layout (per env)
+struct __attribute__((aligned(16))) ConSolve {   // per-contact PGS data (192 B)
+  float AR[16];        // 4x4 diagonal block of A + R (normal, tangent1, tangent2, torsion)
+  float Ainv[9];       // inverse of the cone-scaled friction block (QCQP at lambda = 0)
+  float dd[3];         // cone coefficients (mu0, mu0, mu1)
+  float4 aref;
+  float4 R;
+  float4 f;            // current forces
+  float arinv0;        // 1 / AR[0][0]
+  float pad[3];
+};
+struct __attribute__((aligned(16))) ConGeom {    // per-contact geometry (collision output)
+  float pos[4];
+  float frame[12];     // normal (geom1 -> geom2), tangent1, tangent2
+};
+union ConSlot {
+  ConSolve s;
+  ConGeom g;
+};
+struct __attribute__((aligned(16))) SerialScratch {   // per-body arrays of the 6-link chain
+  float xm[6][12];     // body rotation (row-major 3x3, padded)
+  float xp[6][4];
+  float cin[6][16];    // spatial inertia about the Base origin: I(9), m*d(3), m
+  float cdof[6][8];    // motion subspace (angular; linear)
+  float cfrc[6][8];    // RNE body forces
+};
 struct __attribute__((aligned(16))) EnvShared {
   float qpos[16];
   float qvel[16];
@@ -48,16 +73,12 @@ struct __attribute__((aligned(16))) EnvShared {
   int ncon;
   int nlim;
   int misc[2];
-  float con_pos[kMaxCon][4];     // xyz, dist
-  float con_frame[kMaxCon][12];  // normal, t1, t2
   int con_pair[kMaxCon];
-  float4 J[kMaxCon][12];         // contact rows (normal, t1, t2, torsion) per dof
-  float4 MJ[kMaxCon][12];        // M^-1 J' per dof
-  float AR[kMaxCon][16];         // 4x4 diagonal block of A + R
-  float4 caref[kMaxCon];
-  float4 cR[kMaxCon];
-  float4 cf[kMaxCon];
-  float cmu[kMaxCon][4];
+  float con_dist[kMaxCon];
+  union {
+    ConSlot con[kMaxCon];        // geometry (collision -> Jacobian), then solver data (setup -> PGS)
+    SerialScratch ser;           // serial stage scratch (dead before collision writes contacts)
+  };
 };
 
 // ------------------------------------------------------------------ small math (same formulas as oracle)
@@ -164,11 +185,13 @@ DEV float getimpedance(const float* solimp, float pos, float margin) {
 
 // ------------------------------------------------------------------ task prologue / epilogue
 // constants.py:44-47,78-86 applied to a float32 copy (single_arm.py:33-38): float32 ops, no FMA.
-DEV float unnormalize_f32(float a, float lo, float hi) {
-  float t = __fadd_rn(a, 1.0f);
-  float u = __fdiv_rn(t, 2.0f);
-  float v = __fmul_rn(u, hi - lo);          // (max_val - min_val) rounded once to fp32
-  float w = __fadd_rn(v, lo);
+// span = fp32(max_val - min_val) with the subtraction in double (python floats), as numpy does.
+DEV float unnormalize_f32(float a, float lo, float hi, float span) {
+#pragma clang fp contract(off)
+  float t = a + 1.0f;
+  float u = t / 2.0f;
+  float v = u * span;
+  float w = v + lo;
   w = w < lo ? lo : w;
   return w > hi ? hi : w;
 }
@@ -176,6 +199,7 @@ DEV float unnormalize_f32(float a, float lo, float hi) {
 // reward ladders — single_arm.py:322-380 / :149-215 / :246-285 (double, exactly as the reference)
 DEV double task_reward(const DevModel* __restrict__ m, int task, const float* cube_f, const float* ee_f,
                        uint32_t bits) {
+#pragma clang fp contract(off)
   double bmin[3], bmax[3];
   const double hw = m->bin_hw, h = m->bin_h;
   bmin[0] = m->bin_center[0] + -hw; bmin[1] = m->bin_center[1] + -hw; bmin[2] = m->bin_center[2] + 0.0;
@@ -189,7 +213,7 @@ DEV double task_reward(const DevModel* __restrict__ m, int task, const float* cu
     const float half = (float)m->cube_half;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      float lower = __fsub_rn(cube_f[k], half), upper = __fadd_rn(cube_f[k], half);
+      float lower = cube_f[k] - half, upper = cube_f[k] + half;
       inside = inside && ((double)lower > bmin[k]) && ((double)upper < bmax[k]);
     }
     bool released = inside && !touch_gripper;
@@ -203,7 +227,7 @@ DEV double task_reward(const DevModel* __restrict__ m, int task, const float* cu
   }
   double dx = (double)ee_f[0] - (double)cube_f[0], dy = (double)ee_f[1] - (double)cube_f[1];
   double dz = (double)ee_f[2] - (double)cube_f[2];
-  double dist = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)));
+  double dist = sqrt(dx * dx + dy * dy + dz * dz);
   bool success = touch_gripper && dist < 0.05;
   if (task == SO100_TASK_TOUCH_CUBE_SPARSE) return success ? m->max_reward : -0.2;
   double r = 0.0;
@@ -228,6 +252,7 @@ DEV uint32_t mt_temper(uint32_t y) {
   return y;
 }
 DEV void spawn_pose(const DevModel* __restrict__ m, uint32_t seed, double* pose) {
+#pragma clang fp contract(off)
   uint32_t lo[7], hi[6];
   uint32_t s = seed;
   lo[0] = s;
@@ -246,8 +271,11 @@ DEV void spawn_pose(const DevModel* __restrict__ m, uint32_t seed, double* pose)
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     uint32_t a = out[2 * k] >> 5, b = out[2 * k + 1] >> 6;
+    // no contraction: numpy evaluates (a*2^26 + b) / 2^53 and low + (high-low)*u with rounded ops
     double u = ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
-    pose[k] = m->spawn_lo[k] + (m->spawn_hi[k] - m->spawn_lo[k]) * u;
+    double range = m->spawn_hi[k] - m->spawn_lo[k];
+    double scaled = range * u;
+    pose[k] = m->spawn_lo[k] + scaled;
   }
   pose[3] = 1.0; pose[4] = 0.0; pose[5] = 0.0; pose[6] = 0.0;
 }
@@ -270,32 +298,6 @@ DEV float hash_normal(uint64_t key) {
 // [3P] mj_kinematics + mj_comPos + mj_crb + factor + mj_comVel + mj_rne + actuation + qacc_smooth for
 // the 6-hinge chain; cube free body in closed form (COM at the origin, principal axes): M = diag(m,m,m,I),
 // bias = (-m g, w x I w).  Results to LDS.
-DEV void fk_chain(const DevModel* __restrict__ m, const float* q, float xp[6][3], float xm[6][9], float ax[6][3]) {
-  float pos[3] = {m->base_pos[0], m->base_pos[1], m->base_pos[2]};
-  float quat[4] = {m->base_quat[0], m->base_quat[1], m->base_quat[2], m->base_quat[3]};
-  float R[9];
-  quat2mat(R, quat);
-#pragma unroll
-  for (int a = 0; a < 6; a++) {
-    float t[3];
-    mulmv3(t, R, m->body_pos[a]);
-    pos[0] += t[0]; pos[1] += t[1]; pos[2] += t[2];
-    quat_mul(quat, quat, m->body_quat[a]);
-    float R2[9];
-    quat2mat(R2, quat);
-    mulmv3(ax[a], R2, m->jnt_axis[a]);
-    float s, c;
-    sincosf(0.5f * q[a], &s, &c);
-    float qj[4] = {c, m->jnt_axis[a][0] * s, m->jnt_axis[a][1] * s, m->jnt_axis[a][2] * s};
-    quat_mul(quat, quat, qj);
-    quat_normalize(quat);
-    quat2mat(R, quat);
-    xp[a][0] = pos[0]; xp[a][1] = pos[1]; xp[a][2] = pos[2];
-#pragma unroll
-    for (int k = 0; k < 9; k++) xm[a][k] = R[k];
-  }
-}
-
 DEV void cube_frame(const float* qp, float* pos, float* mat) {
   float q[4] = {qp[3], qp[4], qp[5], qp[6]};
   quat_normalize(q);
@@ -305,31 +307,48 @@ DEV void cube_frame(const float* qp, float* pos, float* mat) {
 
 // full serial stage; writes frames, M^-1, qacc_smooth, sites into sh
 DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynamics, float mscale) {
-  float q[6], xp[6][3], xm[6][9], ax[6][3];
+  // ---- forward kinematics along the chain; frames staged in LDS to bound register pressure
+  {
+    float pos[3] = {m->base_pos[0], m->base_pos[1], m->base_pos[2]};
+    float quat[4] = {m->base_quat[0], m->base_quat[1], m->base_quat[2], m->base_quat[3]};
+    float R[9];
+    quat2mat(R, quat);
+    for (int a = 0; a < 6; a++) {
+      float t[3];
+      mulmv3(t, R, m->body_pos[a]);
+      pos[0] += t[0]; pos[1] += t[1]; pos[2] += t[2];
+      quat_mul(quat, quat, m->body_quat[a]);
+      float R2[9], ax[3];
+      quat2mat(R2, quat);
+      mulmv3(ax, R2, m->jnt_axis[a]);
+      float sn, cs;
+      sincosf(0.5f * sh.qpos[a], &sn, &cs);
+      float qj[4] = {cs, m->jnt_axis[a][0] * sn, m->jnt_axis[a][1] * sn, m->jnt_axis[a][2] * sn};
+      quat_mul(quat, quat, qj);
+      quat_normalize(quat);
+      quat2mat(R, quat);
 #pragma unroll
-  for (int k = 0; k < 6; k++) q[k] = sh.qpos[k];
-  fk_chain(m, q, xp, xm, ax);
+      for (int k = 0; k < 3; k++) { sh.anchor[a][k] = pos[k]; sh.axis[a][k] = ax[k]; sh.ser.xp[a][k] = pos[k]; }
 #pragma unroll
-  for (int a = 0; a < 6; a++) {
-#pragma unroll
-    for (int t = 0; t < 3; t++) { sh.anchor[a][t] = xp[a][t]; sh.axis[a][t] = ax[a][t]; }
+      for (int k = 0; k < 9; k++) sh.ser.xm[a][k] = R[k];
+    }
   }
+  asm volatile("" ::: "memory");
 #pragma unroll
   for (int j = 0; j < 2; j++) {
 #pragma unroll
-    for (int t = 0; t < 3; t++) sh.jaw_pos[j][t] = xp[4 + j][t];
+    for (int t = 0; t < 3; t++) sh.jaw_pos[j][t] = sh.ser.xp[4 + j][t];
 #pragma unroll
-    for (int t = 0; t < 9; t++) sh.jaw_mat[j][t] = xm[4 + j][t];
+    for (int t = 0; t < 9; t++) sh.jaw_mat[j][t] = sh.ser.xm[4 + j][t];
   }
   {
     float t[3];
-    mulmv3(t, xm[4], m->site_ee);
+    mulmv3(t, sh.ser.xm[4], m->site_ee);
 #pragma unroll
-    for (int k = 0; k < 3; k++) sh.site_ee[k] = xp[4][k] + t[k];
+    for (int k = 0; k < 3; k++) sh.site_ee[k] = sh.ser.xp[4][k] + t[k];
   }
-  float cpos[3], cmat[9];
   {
-    float qp[7];
+    float qp[7], cpos[3], cmat[9];
 #pragma unroll
     for (int k = 0; k < 7; k++) qp[k] = sh.qpos[6 + k];
     cube_frame(qp, cpos, cmat);
@@ -346,14 +365,17 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
 
   // ---- comPos: cinert about the tree reference point r = Base xpos; cdof
   const float* r = m->base_pos;
-  float cin[6][13], cdof[6][6];
-#pragma unroll
   for (int a = 0; a < 6; a++) {
-    float ip[3], xi[3], IM[9], diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Ib[9], RT[9], Iw[9];
-    mulmv3(ip, xm[a], m->body_ipos[a]);
+    float xm[9], xp[3], ax[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) xi[k] = xp[a][k] + ip[k] - r[k];
-    mulmm3(IM, xm[a], m->body_imat[a]);
+    for (int k = 0; k < 9; k++) xm[k] = sh.ser.xm[a][k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { xp[k] = sh.ser.xp[a][k]; ax[k] = sh.axis[a][k]; }
+    float ip[3], xi[3], IM[9], diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Ib[9], RT[9], Iw[9];
+    mulmv3(ip, xm, m->body_ipos[a]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) xi[k] = xp[k] + ip[k] - r[k];
+    mulmm3(IM, xm, m->body_imat[a]);
     diag[0] = m->body_inertia[a][0]; diag[4] = m->body_inertia[a][1]; diag[8] = m->body_inertia[a][2];
 #pragma unroll
     for (int i = 0; i < 3; i++)
@@ -361,20 +383,21 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
       for (int j = 0; j < 3; j++) RT[3 * i + j] = IM[3 * j + i];
     mulmm3(Ib, IM, diag);
     mulmm3(Iw, Ib, RT);
-    float mass = m->body_mass[a];
-    float dd2 = dot3(xi, xi);
+    const float mass = m->body_mass[a];
+    const float dd2 = dot3(xi, xi);
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-      for (int j = 0; j < 3; j++) cin[a][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0.f) - xi[i] * xi[j]);
+      for (int j = 0; j < 3; j++) sh.ser.cin[a][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0.f) - xi[i] * xi[j]);
 #pragma unroll
-    for (int k = 0; k < 3; k++) cin[a][9 + k] = mass * xi[k];
-    cin[a][12] = mass;
-    float off[3] = {r[0] - xp[a][0], r[1] - xp[a][1], r[2] - xp[a][2]};
+    for (int k = 0; k < 3; k++) sh.ser.cin[a][9 + k] = mass * xi[k];
+    sh.ser.cin[a][12] = mass;
+    float off[3] = {r[0] - xp[0], r[1] - xp[1], r[2] - xp[2]}, lin[3];
+    cross3(lin, ax, off);
 #pragma unroll
-    for (int k = 0; k < 3; k++) cdof[a][k] = ax[a][k];
-    cross3(&cdof[a][3], ax[a], off);
+    for (int k = 0; k < 3; k++) { sh.ser.cdof[a][k] = ax[k]; sh.ser.cdof[a][3 + k] = lin[k]; }
   }
+  asm volatile("" ::: "memory");
   // ---- CRBA (chain): composite inertia bottom-up, M(i,j) = cdof_j . (crb_i cdof_i), j <= i
   float M[6][6];
   {
@@ -384,94 +407,101 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
 #pragma unroll
     for (int i = 5; i >= 0; i--) {
 #pragma unroll
-      for (int k = 0; k < 13; k++) crb[k] += cin[i][k];
-      float F[6];
-      mul_inert(F, crb, cdof[i]);
+      for (int k = 0; k < 13; k++) crb[k] += sh.ser.cin[i][k];
+      float F[6], cd[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) cd[k] = sh.ser.cdof[i][k];
+      mul_inert(F, crb, cd);
 #pragma unroll
       for (int j = 0; j <= i; j++) {
         float v = 0.f;
 #pragma unroll
-        for (int k = 0; k < 6; k++) v += cdof[j][k] * F[k];
+        for (int k = 0; k < 6; k++) v += sh.ser.cdof[j][k] * F[k];
         M[i][j] = v; M[j][i] = v;
       }
       M[i][i] += m->armature[i];
     }
   }
-  // ---- Cholesky + explicit inverse of the 6x6 arm block
-  float L[6][6];
+  // ---- Cholesky + explicit inverse of the 6x6 arm block (symmetrised) -> LDS
+  {
+    float L[6][6];
 #pragma unroll
-  for (int j = 0; j < 6; j++) {
-    float s = M[j][j];
+    for (int j = 0; j < 6; j++) {
+      float sdiag = M[j][j];
 #pragma unroll
-    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
-    L[j][j] = sqrtf(fmaxf(s, kMinVal));
-    float inv = 1.0f / L[j][j];
+      for (int k = 0; k < j; k++) sdiag -= L[j][k] * L[j][k];
+      L[j][j] = sqrtf(fmaxf(sdiag, kMinVal));
+      const float inv = 1.0f / L[j][j];
 #pragma unroll
-    for (int i = j + 1; i < 6; i++) {
-      float t = M[i][j];
+      for (int i = j + 1; i < 6; i++) {
+        float t = M[i][j];
 #pragma unroll
-      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
-      L[i][j] = t * inv;
+        for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+        L[i][j] = t * inv;
+      }
     }
+    for (int c = 0; c < 6; c++) {   // solve M x = e_c
+      float z[6], x[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        float sacc = (i == c) ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < i; k++) sacc -= L[i][k] * z[k];
+        z[i] = sacc / L[i][i];
+      }
+#pragma unroll
+      for (int i = 5; i >= 0; i--) {
+        float sacc = z[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) sacc -= L[k][i] * x[k];
+        x[i] = sacc / L[i][i];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; i++) sh.ser.cfrc[i][c] = x[i];   // temporary M^-1 column storage
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+      for (int j = 0; j < 6; j++) sh.minv[i][j] = 0.5f * (sh.ser.cfrc[i][j] + sh.ser.cfrc[j][i]);
   }
-  float Minv[6][6];
-#pragma unroll
-  for (int c = 0; c < 6; c++) {   // solve M x = e_c
-    float z[6], x[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-      float s = (i == c) ? 1.f : 0.f;
-#pragma unroll
-      for (int k = 0; k < i; k++) s -= L[i][k] * z[k];
-      z[i] = s / L[i][i];
-    }
-#pragma unroll
-    for (int i = 5; i >= 0; i--) {
-      float s = z[i];
-#pragma unroll
-      for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
-      x[i] = s / L[i][i];
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) Minv[i][c] = x[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 6; i++)
-#pragma unroll
-    for (int j = 0; j < 6; j++) sh.minv[i][j] = 0.5f * (Minv[i][j] + Minv[j][i]);
-
+  asm volatile("" ::: "memory");
   // ---- RNE (flg_acc = 0) on the chain: cvel, cdof_dot, cacc, cfrc, backward accumulation
-  float qd[6];
+  {
+    float cvel[6] = {0, 0, 0, 0, 0, 0};
+    float cacc[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+    for (int a = 0; a < 6; a++) {
+      float cd[6], cin[13];
 #pragma unroll
-  for (int k = 0; k < 6; k++) qd[k] = sh.qvel[k];
-  float cvel[6] = {0, 0, 0, 0, 0, 0};
-  float cacc[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-  float cfrc[6][6];
+      for (int k = 0; k < 6; k++) cd[k] = sh.ser.cdof[a][k];
 #pragma unroll
-  for (int a = 0; a < 6; a++) {
+      for (int k = 0; k < 13; k++) cin[k] = sh.ser.cin[a][k];
+      const float qd = sh.qvel[a];
 #pragma unroll
-    for (int k = 0; k < 6; k++) cvel[k] += cdof[a][k] * qd[a];
-    float cdd[6];
-    cross_motion(cdd, cvel, cdof[a]);
+      for (int k = 0; k < 6; k++) cvel[k] += cd[k] * qd;
+      float cdd[6];
+      cross_motion(cdd, cvel, cd);
 #pragma unroll
-    for (int k = 0; k < 6; k++) cacc[k] += cdd[k] * qd[a];
-    float f1[6], Iv[6], f2[6];
-    mul_inert(f1, cin[a], cacc);
-    mul_inert(Iv, cin[a], cvel);
-    cross_force(f2, cvel, Iv);
+      for (int k = 0; k < 6; k++) cacc[k] += cdd[k] * qd;
+      float f1[6], Iv[6], f2[6];
+      mul_inert(f1, cin, cacc);
+      mul_inert(Iv, cin, cvel);
+      cross_force(f2, cvel, Iv);
 #pragma unroll
-    for (int k = 0; k < 6; k++) cfrc[a][k] = f1[k] + f2[k];
+      for (int k = 0; k < 6; k++) sh.ser.cfrc[a][k] = f1[k] + f2[k];
+    }
   }
+  asm volatile("" ::: "memory");
   float bias[6];
   {
     float acc[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int a = 5; a >= 0; a--) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) acc[k] += cfrc[a][k];
+      for (int k = 0; k < 6; k++) acc[k] += sh.ser.cfrc[a][k];
       float v = 0.f;
 #pragma unroll
-      for (int k = 0; k < 6; k++) v += cdof[a][k] * acc[k];
+      for (int k = 0; k < 6; k++) v += sh.ser.cdof[a][k] * acc[k];
       bias[a] = v;
     }
   }
@@ -479,22 +509,22 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
   float tau[6];
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    float c = fminf(fmaxf(sh.ctrl[i], m->act_clo[i]), m->act_chi[i]);
-    float f = m->act_kp[i] * c - m->act_kp[i] * q[i] - m->act_kv[i] * qd[i];
+    const float c = fminf(fmaxf(sh.ctrl[i], m->act_clo[i]), m->act_chi[i]);
+    float f = m->act_kp[i] * c - m->act_kp[i] * sh.qpos[i] - m->act_kv[i] * sh.qvel[i];
     f = fminf(fmaxf(f, m->act_flo[i]), m->act_fhi[i]);
     tau[i] = f - bias[i];
   }
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    float s = 0.f;
+    float sacc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 6; j++) s += sh.minv[i][j] * tau[j];
-    sh.qacc_smooth[i] = s;
+    for (int j = 0; j < 6; j++) sacc += sh.minv[i][j] * tau[j];
+    sh.qacc_smooth[i] = sacc;
   }
   // ---- cube (free body)
   const float mc = m->cube_mass * mscale;
-  float I3[3] = {m->cube_inertia[0] * mscale, m->cube_inertia[1] * mscale, m->cube_inertia[2] * mscale};
-  float w[3] = {sh.qvel[9], sh.qvel[10], sh.qvel[11]};
+  const float I3[3] = {m->cube_inertia[0] * mscale, m->cube_inertia[1] * mscale, m->cube_inertia[2] * mscale};
+  const float w[3] = {sh.qvel[9], sh.qvel[10], sh.qvel[11]};
   float Iw3[3] = {I3[0] * w[0], I3[1] * w[1], I3[2] * w[2]}, gyro[3];
   cross3(gyro, w, Iw3);
 #pragma unroll
@@ -837,6 +867,149 @@ DEV void qcqp3(float* x, const float A0[3][3], const float* b0, const float* dd,
   x[0] = y[0] * dd[0]; x[1] = y[1] * dd[1]; x[2] = y[2] * dd[2];
 }
 
+// ------------------------------------------------------------------ row broadcast (DPP row_newbcast, gfx90a+)
+template <int L>
+DEV float bcast_row_c(float v) { return dpp<0x150 + L>(v); }
+// j must fold to a constant after unrolling; every lane of each 16-lane row receives lane j of that row
+DEV float bcast_row(float v, int j) {
+  switch (j) {
+    case 0: return bcast_row_c<0>(v);
+    case 1: return bcast_row_c<1>(v);
+    case 2: return bcast_row_c<2>(v);
+    case 3: return bcast_row_c<3>(v);
+    case 4: return bcast_row_c<4>(v);
+    case 5: return bcast_row_c<5>(v);
+    case 6: return bcast_row_c<6>(v);
+    case 7: return bcast_row_c<7>(v);
+    case 8: return bcast_row_c<8>(v);
+    case 9: return bcast_row_c<9>(v);
+    case 10: return bcast_row_c<10>(v);
+    case 11: return bcast_row_c<11>(v);
+    case 12: return bcast_row_c<12>(v);
+    case 13: return bcast_row_c<13>(v);
+    case 14: return bcast_row_c<14>(v);
+    default: return bcast_row_c<15>(v);
+  }
+}
+DEV float4 bcast_row4(float4 v, int j) {
+  return make_float4(bcast_row(v.x, j), bcast_row(v.y, j), bcast_row(v.z, j), bcast_row(v.w, j));
+}
+
+// (M^-1 J')[dof] for the 4 rows of a contact: arm dofs use the dense 6x6 M^-1 row (row broadcasts of
+// the other arm lanes' J), cube dofs the diagonal inverse mass.
+DEV float4 minv_times(float4 J, const float* minv_row, float invmc, int lane) {
+  float4 acc = make_float4(J.x * invmc, J.y * invmc, J.z * invmc, J.w * invmc);
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const float4 Jj = bcast_row4(J, j);
+    acc.x += minv_row[j] * Jj.x; acc.y += minv_row[j] * Jj.y;
+    acc.z += minv_row[j] * Jj.z; acc.w += minv_row[j] * Jj.w;
+  }
+  return acc;
+}
+
+// contact c's Jacobian column for dof `lane` (rows: normal, t1, t2 on the point velocity; torsion on
+// the angular velocity); J = frame . (jac(body of geom2) - jac(body of geom1)) at the contact point
+DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int c, int lane) {
+  const int p = sh.con_pair[c];
+  const float* cp = sh.con[c].g.pos;
+  const float* fr = sh.con[c].g.frame;
+  float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
+#pragma unroll
+  for (int side = 0; side < 2; side++) {
+    const int b = m->geom_body[side ? m->pair_g2[p] : m->pair_g1[p]];
+    const float sg = side ? 1.f : -1.f;
+    if (lane < 6) {
+      if (b >= 2 && b <= 7 && lane + 2 <= b) {
+        float off[3] = {cp[0] - sh.anchor[lane][0], cp[1] - sh.anchor[lane][1], cp[2] - sh.anchor[lane][2]};
+        float v[3];
+        cross3(v, sh.axis[lane], off);
+#pragma unroll
+        for (int t = 0; t < 3; t++) { jp[t] += sg * v[t]; jr[t] += sg * sh.axis[lane][t]; }
+      }
+    } else if (b == SO100_CUBE_BODY) {
+      if (lane < 9) {
+        jp[lane - 6] += sg;
+      } else {
+        const int k = lane - 9;
+        float ax[3] = {sh.cube_mat[k], sh.cube_mat[3 + k], sh.cube_mat[6 + k]};
+        float off[3] = {cp[0] - sh.cube_pos[0], cp[1] - sh.cube_pos[1], cp[2] - sh.cube_pos[2]};
+        float v[3];
+        cross3(v, ax, off);
+#pragma unroll
+        for (int t = 0; t < 3; t++) { jp[t] += sg * v[t]; jr[t] += sg * ax[t]; }
+      }
+    }
+  }
+  return make_float4(fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2], fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2],
+                     fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2], fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2]);
+}
+
+// 3x3 inverse by adjugate (det <= kMinVal -> zero matrix, the QCQP then returns 0 like the oracle)
+DEV void inv3(float Pi[3][3], const float P[3][3]) {
+  Pi[0][0] = P[1][1] * P[2][2] - P[1][2] * P[2][1];
+  Pi[0][1] = P[0][2] * P[2][1] - P[0][1] * P[2][2];
+  Pi[0][2] = P[0][1] * P[1][2] - P[0][2] * P[1][1];
+  Pi[1][0] = P[1][2] * P[2][0] - P[1][0] * P[2][2];
+  Pi[1][1] = P[0][0] * P[2][2] - P[0][2] * P[2][0];
+  Pi[1][2] = P[0][2] * P[1][0] - P[0][0] * P[1][2];
+  Pi[2][0] = P[1][0] * P[2][1] - P[1][1] * P[2][0];
+  Pi[2][1] = P[0][1] * P[2][0] - P[0][0] * P[2][1];
+  Pi[2][2] = P[0][0] * P[1][1] - P[0][1] * P[1][0];
+  const float det = P[0][0] * Pi[0][0] + P[0][1] * Pi[1][0] + P[0][2] * Pi[2][0];
+  const float id = det > kMinVal ? 1.f / det : 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) Pi[i][j] *= id;
+}
+
+// MuJoCo mju_QCQP3 restated, with the lambda = 0 inverse precomputed once per substep (Ainv): the
+// sticking case (inside the cone) costs one 3x3 mat-vec; sliding contacts continue Newton on lambda.
+DEV void qcqp3_warm(float* x, const float* Ainv, const float A0[3][3], const float* b0, const float* dd, float r) {
+  float b[3], y[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) b[i] = b0[i] * dd[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) y[i] = -(Ainv[3 * i] * b[0] + Ainv[3 * i + 1] * b[1] + Ainv[3 * i + 2] * b[2]);
+  float val = y[0] * y[0] + y[1] * y[1] + y[2] * y[2] - r * r;
+  if (val >= 1e-10f) {
+    float deriv = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) deriv += y[i] * (Ainv[3 * i] * y[0] + Ainv[3 * i + 1] * y[1] + Ainv[3 * i + 2] * y[2]);
+    deriv *= -2.f;
+    float delta = -val / deriv;
+    if (delta >= 1e-10f) {
+      float A[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) A[i][j] = A0[i][j] * dd[i] * dd[j];
+      float la = delta;
+      for (int it = 1; it < 20; it++) {
+        float P[3][3], Pi[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) P[i][j] = A[i][j] + (i == j ? la : 0.f);
+        inv3(Pi, P);
+#pragma unroll
+        for (int i = 0; i < 3; i++) y[i] = -(Pi[i][0] * b[0] + Pi[i][1] * b[1] + Pi[i][2] * b[2]);
+        val = y[0] * y[0] + y[1] * y[1] + y[2] * y[2] - r * r;
+        if (val < 1e-10f) break;
+        deriv = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; i++) deriv += y[i] * (Pi[i][0] * y[0] + Pi[i][1] * y[1] + Pi[i][2] * y[2]);
+        deriv *= -2.f;
+        delta = -val / deriv;
+        if (delta < 1e-10f) break;
+        la += delta;
+      }
+    }
+  }
+  x[0] = y[0] * dd[0]; x[1] = y[1] * dd[1]; x[2] = y[2] * dd[2];
+}
+
 // ------------------------------------------------------------------ the step kernel
 struct StepArgs {
   const DevModel* m;
@@ -913,7 +1086,7 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     if (sigma > 0.f)
       a += sigma * hash_normal(splitmix64(args.base_seed ^ ((uint64_t)(e + args.env_offset) << 40) ^ ((uint64_t)episode0 << 20) ^
                                           (uint64_t)(elapsed0 * 8 + lane)));
-    sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane]);
+    sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
   }
 
   const float h = m->timestep;
@@ -944,9 +1117,10 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
           float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
           make_frame(fr);
 #pragma unroll
-          for (int t = 0; t < 9; t++) sh.con_frame[slot][t] = fr[t];
-          sh.con_pos[slot][0] = pc.pos[c][0]; sh.con_pos[slot][1] = pc.pos[c][1];
-          sh.con_pos[slot][2] = pc.pos[c][2]; sh.con_pos[slot][3] = pc.dist[c];
+          for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
+          sh.con[slot].g.pos[0] = pc.pos[c][0]; sh.con[slot].g.pos[1] = pc.pos[c][1];
+          sh.con[slot].g.pos[2] = pc.pos[c][2]; sh.con[slot].g.pos[3] = pc.dist[c];
+          sh.con_dist[slot] = pc.dist[c];
           sh.con_pair[slot] = lane;
         }
       }
@@ -956,83 +1130,31 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
 
-    // ---------------- S4: contact Jacobian rows, lane = dof
-    for (int c = 0; c < ncon_max; c++) {
-      if (c < ncon && lane < SO100_NV) {
-        const int p = sh.con_pair[c];
-        const float* cp = sh.con_pos[c];
-        const float* fr = sh.con_frame[c];
-        float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
-#pragma unroll
-        for (int side = 0; side < 2; side++) {
-          const int b = m->geom_body[side ? m->pair_g2[p] : m->pair_g1[p]];
-          const float sg = side ? 1.f : -1.f;
-          if (lane < 6) {
-            if (b >= 2 && b <= 7 && lane + 2 <= b) {
-              float off[3] = {cp[0] - sh.anchor[lane][0], cp[1] - sh.anchor[lane][1], cp[2] - sh.anchor[lane][2]};
-              float v[3];
-              cross3(v, sh.axis[lane], off);
-#pragma unroll
-              for (int t = 0; t < 3; t++) { jp[t] += sg * v[t]; jr[t] += sg * sh.axis[lane][t]; }
-            }
-          } else if (b == SO100_CUBE_BODY) {
-            if (lane < 9) {
-              jp[lane - 6] += sg;
-            } else {
-              const int k = lane - 9;
-              float ax[3] = {sh.cube_mat[k], sh.cube_mat[3 + k], sh.cube_mat[6 + k]};
-              float off[3] = {cp[0] - sh.cube_pos[0], cp[1] - sh.cube_pos[1], cp[2] - sh.cube_pos[2]};
-              float v[3];
-              cross3(v, ax, off);
-#pragma unroll
-              for (int t = 0; t < 3; t++) { jp[t] += sg * v[t]; jr[t] += sg * ax[t]; }
-            }
-          }
-        }
-        float4 J4;
-        J4.x = fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2];
-        J4.y = fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2];
-        J4.z = fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2];
-        J4.w = fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2];
-        sh.J[c][lane] = J4;
-      }
-    }
-    __syncthreads();
-    // ---------------- S5: MJ = M^-1 J' per dof lane; friction/limit row setup (lane = dof)
+    // ---------------- S4/S5: contact Jacobian rows and M^-1 J' in registers (lane = dof, contacts unrolled)
     float minv_row[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) minv_row[j] = (lane < 6) ? sh.minv[lane][j] : 0.f;
     const float invmc = (lane >= 6 && lane < 12) ? sh.inv_mcube[lane - 6] : 0.f;
-    for (int c = 0; c < ncon_max; c++) {
-      if (c < ncon && lane < SO100_NV) {
-        float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane < 6) {
+    float4 Jr[kMaxCon];
 #pragma unroll
-          for (int j = 0; j < 6; j++) {
-            float4 Jj = sh.J[c][j];
-            r4.x += minv_row[j] * Jj.x; r4.y += minv_row[j] * Jj.y;
-            r4.z += minv_row[j] * Jj.z; r4.w += minv_row[j] * Jj.w;
-          }
-        } else {
-          float4 Jk = sh.J[c][lane];
-          r4 = make_float4(Jk.x * invmc, Jk.y * invmc, Jk.z * invmc, Jk.w * invmc);
-        }
-        sh.MJ[c][lane] = r4;
-      }
+    for (int c = 0; c < kMaxCon; c++) {
+      Jr[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c < ncon_max && c < ncon && lane < SO100_NV) Jr[c] = contact_jac(m, sh, c, lane);
     }
     const float qs_r = (lane < SO100_NV) ? sh.qacc_smooth[lane] : 0.f;
-    // frictionloss row of dof `lane`
+    // frictionloss row of dof `lane` (pos 0: aref = -B vel, R constant)
     const bool has_fr = lane < SO100_NV;
-    float fr_R = has_fr ? m->fr_R[lane] : 1.f;
-    float fr_fl = has_fr ? m->fr_floss[lane] : 0.f;
-    float fr_aref = -m->fr_B * qvel_r;
+    const float fr_R = has_fr ? m->fr_R[lane] : 1.f;
+    const float fr_fl = has_fr ? m->fr_floss[lane] : 0.f;
+    const float fr_aref = -m->fr_B * qvel_r;
     float mdiag = invmc;
 #pragma unroll
     for (int j = 0; j < 6; j++) mdiag = (lane == j) ? minv_row[j] : mdiag;
-    float fr_AR = mdiag + fr_R;
+    const float fr_AR = mdiag + fr_R;
+    const float fr_ARinv = 1.f / fr_AR;
     float fr_f;
     {
-      float jar = warm_r - fr_aref;
+      const float jar = warm_r - fr_aref;
       if (jar <= -fr_R * fr_fl) fr_f = fr_fl;
       else if (jar >= fr_R * fr_fl) fr_f = -fr_fl;
       else fr_f = -jar / fr_R;
@@ -1042,163 +1164,159 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     bool lim_on = false;
     float lim_s = 0.f, lim_aref = 0.f, lim_R = 1.f, lim_AR = 1.f, lim_f = 0.f;
     if (lane < 6) {
-      float dlo = qpos_r - m->jnt_lo[lane], dhi = m->jnt_hi[lane] - qpos_r;
+      const float dlo = qpos_r - m->jnt_lo[lane], dhi = m->jnt_hi[lane] - qpos_r;
       float dist = 0.f;
       if (dlo < 0.f) { lim_on = true; lim_s = 1.f; dist = dlo; }
       else if (dhi < 0.f) { lim_on = true; lim_s = -1.f; dist = dhi; }
       if (lim_on) {
-        float imp = getimpedance(m->lim_solimp, dist, 0.f);
+        const float imp = getimpedance(m->lim_solimp, dist, 0.f);
         lim_R = fmaxf(kMinVal, (1.f - imp) / imp * m->lim_invw[lane]);
         lim_aref = -m->lim_B * (lim_s * qvel_r) - m->lim_K * imp * dist;
-        lim_AR = fr_AR - fr_R + lim_R;
-        float jar = lim_s * warm_r - lim_aref;
+        lim_AR = mdiag + lim_R;
+        const float jar = lim_s * warm_r - lim_aref;
         lim_f = jar < 0.f ? -jar / lim_R : 0.f;
       }
     }
     const uint64_t lim_mask = __ballot(lim_on && valid);
-    __syncthreads();
-    // ---------------- S6: per-contact setup, lane = contact
-    if (lane < ncon) {
-      const int c = lane;
-      const int p = sh.con_pair[c];
-      const float dist = sh.con_pos[c][3];
-      float ARb[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-      float vel[4] = {0, 0, 0, 0}, acc[4] = {0, 0, 0, 0}, ws[4] = {0, 0, 0, 0};
+    float cost_part = 0.f;
+    float phi = has_fr ? fr_f + (lim_on ? lim_s * lim_f : 0.f) : 0.f;
+    if (has_fr) cost_part += 0.5f * fr_R * fr_f * fr_f + fr_f * (qs_r - fr_aref);
+    if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
+
+    // ---------------- S6: per-contact constraint setup (DPP row reductions; scalar part per env)
 #pragma unroll
-      for (int k = 0; k < SO100_NV; k++) {
-        float4 Jk = sh.J[c][k], Mk = sh.MJ[c][k];
-        float jv[4] = {Jk.x, Jk.y, Jk.z, Jk.w}, mv[4] = {Mk.x, Mk.y, Mk.z, Mk.w};
-        float qv = sh.qvel[k], qa = sh.qacc_smooth[k], qw = sh.warm[k];
+    for (int c = 0; c < kMaxCon; c++) {
+      if (c < ncon_max) {
+        const float4 J = Jr[c];
+        const float4 M = minv_times(J, minv_row, invmc, lane);   // M^-1 J' column of this dof
+        const float jv[4] = {J.x, J.y, J.z, J.w}, mv[4] = {M.x, M.y, M.z, M.w};
+        float ARb[4][4], vel[4], acc[4], ws[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
 #pragma unroll
-          for (int s = 0; s < 4; s++) ARb[r][s] += jv[r] * mv[s];
-          vel[r] += jv[r] * qv;
-          acc[r] += jv[r] * qa;
-          ws[r] += jv[r] * qw;
+          for (int q = r; q < 4; q++) { ARb[r][q] = rowsum16(jv[r] * mv[q]); ARb[q][r] = ARb[r][q]; }
+          vel[r] = rowsum16(jv[r] * qvel_r);
+          acc[r] = rowsum16(jv[r] * qs_r);
+          ws[r] = rowsum16(jv[r] * warm_r);
         }
-      }
-      const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
-      const float K = m->pair_K[p], Bd = m->pair_B[p];
-      const float mu0 = m->pair_mu0[p] * fscale, mu1 = m->pair_mu1[p] * fscale;
-      float R[4];
-      R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
-      R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
-      R[2] = R[1];
-      R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
-      float aref[4];
-      aref[0] = -Bd * vel[0] - K * imp * (dist - m->pair_margin[p]);
-      aref[1] = -Bd * vel[1]; aref[2] = -Bd * vel[2]; aref[3] = -Bd * vel[3];
-#pragma unroll
-      for (int r = 0; r < 4; r++) ARb[r][r] += R[r];
-      // warmstart force (dual map of jar = J qacc_ws - aref), elliptic zones
-      float jar[4], f[4], mus[3] = {mu0, mu0, mu1};
-#pragma unroll
-      for (int r = 0; r < 4; r++) jar[r] = ws[r] - aref[r];
-      {
-        float mu = mu0 * sqrtf(R[1] / R[0]);
-        float U[4], T = 0.f;
-        U[0] = jar[0] * mu;
-#pragma unroll
-        for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
-        T = sqrtf(T);
-        float N = U[0];
-        if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
-          f[0] = f[1] = f[2] = f[3] = 0.f;
-        } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
-#pragma unroll
-          for (int k = 0; k < 4; k++) f[k] = -jar[k] / R[k];
-        } else {
-          float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
-          float NmT = N - mu * T;
-          f[0] = -Dm * NmT * mu;
-#pragma unroll
-          for (int k = 1; k < 4; k++) f[k] = -f[0] / T * U[k] * mus[k - 1];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-#pragma unroll
-        for (int s = 0; s < 4; s++) sh.AR[c][4 * r + s] = ARb[r][s];
-      sh.caref[c] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-      sh.cR[c] = make_float4(R[0], R[1], R[2], R[3]);
-      sh.cf[c] = make_float4(f[0], f[1], f[2], f[3]);
-      sh.cmu[c][0] = mu0; sh.cmu[c][1] = mu0; sh.cmu[c][2] = mu1;
-      // dual-cost partial of this contact's rows: 0.5 R f^2 + f b, b = J qacc_smooth - aref
-      float part = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; r++) part += 0.5f * R[r] * f[r] * f[r] + f[r] * (acc[r] - aref[r]);
-      sh.vec[c] = part;   // consumed below (indices < ncon)
-    }
-    __syncthreads();
-    // ---------------- S7: warmstart dual cost, initial qacc
-    float cost_part = 0.f;
-    if (lane < ncon) cost_part += sh.vec[lane];
-    float phi = 0.f;
-    if (lane < SO100_NV) {
-      phi = fr_f + (lim_on ? lim_s * lim_f : 0.f);
-      for (int c = 0; c < ncon_max; c++) {
+        float f[4] = {0.f, 0.f, 0.f, 0.f};
         if (c < ncon) {
-          float4 Jk = sh.J[c][lane], fc = sh.cf[c];
-          phi += Jk.x * fc.x + Jk.y * fc.y + Jk.z * fc.z + Jk.w * fc.w;
-        }
-      }
-      cost_part += 0.5f * fr_R * fr_f * fr_f + fr_f * (qs_r - fr_aref);
-      if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
-    }
-    __syncthreads();
-    if (lane < SO100_NV) sh.vec[lane] = phi;
-    __syncthreads();
-    float dq = 0.f;
-    if (lane < 6) {
+          const int p = sh.con_pair[c];
+          const float dist = sh.con_dist[c];
+          const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
+          const float K = m->pair_K[p], Bd = m->pair_B[p];
+          const float mu0 = m->pair_mu0[p] * fscale, mu1 = m->pair_mu1[p] * fscale;
+          float R[4];
+          R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
+          R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
+          R[2] = R[1];
+          R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
+          float aref[4];
+          aref[0] = -Bd * vel[0] - K * imp * (dist - m->pair_margin[p]);
+          aref[1] = -Bd * vel[1]; aref[2] = -Bd * vel[2]; aref[3] = -Bd * vel[3];
 #pragma unroll
-      for (int j = 0; j < 6; j++) dq += minv_row[j] * sh.vec[j];
-    } else if (lane < 12) {
-      dq = invmc * phi;
+          for (int r = 0; r < 4; r++) ARb[r][r] += R[r];
+          // warmstart force: dual map of jar = J qacc_warmstart - aref (elliptic zones)
+          float jar[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) jar[r] = ws[r] - aref[r];
+          const float mus[3] = {mu0, mu0, mu1};
+          {
+            const float mu = mu0 * sqrtf(R[1] / R[0]);
+            float U[4], T = 0.f;
+            U[0] = jar[0] * mu;
+#pragma unroll
+            for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
+            T = sqrtf(T);
+            const float N = U[0];
+            if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
+              f[0] = f[1] = f[2] = f[3] = 0.f;
+            } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+#pragma unroll
+              for (int k = 0; k < 4; k++) f[k] = -jar[k] / R[k];
+            } else {
+              const float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
+              const float NmT = N - mu * T;
+              f[0] = -Dm * NmT * mu;
+#pragma unroll
+              for (int k = 1; k < 4; k++) f[k] = -f[0] / T * U[k] * mus[k - 1];
+            }
+          }
+          // QCQP at lambda = 0: inverse of the friction block scaled by the cone coefficients
+          float As[3][3], Ai[3][3];
+#pragma unroll
+          for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b2 = 0; b2 < 3; b2++) As[a][b2] = ARb[1 + a][1 + b2] * mus[a] * mus[b2];
+          inv3(Ai, As);
+          ConSolve& cs = sh.con[c].s;
+#pragma unroll
+          for (int k = 0; k < 16; k++) cs.AR[k] = ARb[k >> 2][k & 3];
+#pragma unroll
+          for (int k = 0; k < 9; k++) cs.Ainv[k] = Ai[k / 3][k % 3];
+          cs.dd[0] = mus[0]; cs.dd[1] = mus[1]; cs.dd[2] = mus[2];
+          cs.aref = make_float4(aref[0], aref[1], aref[2], aref[3]);
+          cs.R = make_float4(R[0], R[1], R[2], R[3]);
+          cs.f = make_float4(f[0], f[1], f[2], f[3]);
+          cs.arinv0 = 1.f / ARb[0][0];
+          if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * f[r] * f[r] + f[r] * (acc[r] - aref[r]);
+          }
+        }
+        phi += J.x * f[0] + J.y * f[1] + J.z * f[2] + J.w * f[3];
+      }
+    }
+    // ---------------- S7: warmstart dual cost 0.5 f'ARf + f'b (keep the warmstart only if <= 0)
+    float dq = 0.f;
+    {
+      float acc_arm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 6; j++) acc_arm += minv_row[j] * bcast_row(phi, j);
+      dq = (lane < 6) ? acc_arm : invmc * phi;
     }
     cost_part += 0.5f * phi * dq;
     const float cost = rowsum16(cost_part);
     float qacc_c = qs_r;
     if (cost > 0.f) {
-      fr_f = 0.f; lim_f = 0.f;
-      for (int c = 0; c < ncon_max; c++)
-        if (c < ncon) sh.cf[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      fr_f = 0.f;
+      lim_f = 0.f;
+#pragma unroll
+      for (int c = 0; c < kMaxCon; c++)
+        if (c < ncon_max && c < ncon) sh.con[c].s.f = make_float4(0.f, 0.f, 0.f, 0.f);
     } else {
       qacc_c += dq;
     }
     if (lane >= SO100_NV) qacc_c = 0.f;
+    __syncthreads();
 
     // ---------------- S8: projected Gauss-Seidel (MuJoCo mj_solPGS order: friction | limits | contacts)
     bool done = !valid;
     int iters = 0;
     float last_impr = 0.f;
-    const float fr_ARinv = 1.f / fr_AR;
     for (int it = 0; it < m->iterations; it++) {
       if (__ballot(!done) == 0ull) break;
       float impr = 0.f;
-      // arm frictionloss rows, sequential (coupled through M^-1)
+      // arm frictionloss rows: sequential, coupled through M^-1 (row broadcast by DPP)
 #pragma unroll
       for (int j = 0; j < 6; j++) {
         float delta = 0.f;
-        if (lane == j) {
-          float res = qacc_c - fr_aref + fr_R * fr_f;
-          float old = fr_f;
-          float fn = fr_f - res * fr_ARinv;
-          fn = fminf(fmaxf(fn, -fr_fl), fr_fl);
+        if (lane == j && !done) {
+          const float res = qacc_c - fr_aref + fr_R * fr_f;
+          const float old = fr_f;
+          const float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
           delta = fn - old;
-          if (done) delta = 0.f;
-          fr_f = old + delta;
+          fr_f = fn;
           impr -= delta * (res + 0.5f * fr_AR * delta);
         }
-        float db = bcast16(delta, j);
-        qacc_c += minv_row[j] * db;
+        qacc_c += minv_row[j] * bcast_row(delta, j);
       }
       // cube frictionloss rows: decoupled (diagonal M), all six in parallel
       if (lane >= 6 && lane < 12 && !done) {
-        float res = qacc_c - fr_aref + fr_R * fr_f;
-        float old = fr_f;
-        float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
-        float delta = fn - old;
+        const float res = qacc_c - fr_aref + fr_R * fr_f;
+        const float old = fr_f;
+        const float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
+        const float delta = fn - old;
         fr_f = fn;
         impr -= delta * (res + 0.5f * fr_AR * delta);
         qacc_c += invmc * delta;
@@ -1210,63 +1328,69 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
           if (!((lim_mask >> j) & 0x0001000100010001ull)) continue;
           float delta = 0.f;
           if (lane == j && lim_on && !done) {
-            float res = lim_s * qacc_c - lim_aref + lim_R * lim_f;
-            float old = lim_f;
-            float fn = fmaxf(lim_f - res / lim_AR, 0.f);
+            const float res = lim_s * qacc_c - lim_aref + lim_R * lim_f;
+            const float old = lim_f;
+            const float fn = fmaxf(lim_f - res / lim_AR, 0.f);
             delta = fn - old;
             lim_f = fn;
             impr -= delta * (res + 0.5f * lim_AR * delta);
             delta *= lim_s;
           }
-          float db = bcast16(delta, j);
-          qacc_c += minv_row[j] * db;
+          qacc_c += minv_row[j] * bcast_row(delta, j);
         }
       }
-      // contact blocks (elliptic, condim 4): normal then friction QCQP
-      for (int c = 0; c < ncon_max; c++) {
-        const bool act = (c < ncon) && !done;
-        float4 Jk = (lane < SO100_NV && c < ncon) ? sh.J[c][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-        float j0 = rowsum16(Jk.x * qacc_c), j1 = rowsum16(Jk.y * qacc_c);
-        float j2 = rowsum16(Jk.z * qacc_c), j3 = rowsum16(Jk.w * qacc_c);
-        float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (act) {
-          const float4 ar = sh.caref[c], R4 = sh.cR[c], f4 = sh.cf[c];
-          const float* AR = sh.AR[c];
-          float res[4] = {j0 - ar.x + R4.x * f4.x, j1 - ar.y + R4.y * f4.y, j2 - ar.z + R4.z * f4.z,
-                          j3 - ar.w + R4.w * f4.w};
-          float old[4] = {f4.x, f4.y, f4.z, f4.w}, f[4];
-          f[0] = old[0] - res[0] / AR[0];
-          if (f[0] < kMinVal) {
-            f[0] = f[1] = f[2] = f[3] = 0.f;
-          } else {
-            float Af[3][3], bf[3], x[3];
-            float mus[3] = {sh.cmu[c][0], sh.cmu[c][1], sh.cmu[c][2]};
+      // contact blocks (elliptic, condim 4): normal update, then friction QCQP on the cone
 #pragma unroll
-            for (int a = 0; a < 3; a++) {
-              bf[a] = res[1 + a] + AR[4 * (1 + a)] * (f[0] - old[0]);
+      for (int c = 0; c < kMaxCon; c++) {
+        if (c < ncon_max) {
+          // keep the per-contact LDS loads inside the sweep (no LICM of 16 contacts' blocks into VGPRs)
+          asm volatile("" ::: "memory");
+          const ConSolve& cs = sh.con[c].s;
+          const float j0 = rowsum16(Jr[c].x * qacc_c), j1 = rowsum16(Jr[c].y * qacc_c);
+          const float j2 = rowsum16(Jr[c].z * qacc_c), j3 = rowsum16(Jr[c].w * qacc_c);
+          float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (c < ncon && !done) {
+            const float4 ar = cs.aref, R4 = cs.R, f4 = cs.f;
+            const float res[4] = {j0 - ar.x + R4.x * f4.x, j1 - ar.y + R4.y * f4.y, j2 - ar.z + R4.z * f4.z,
+                                  j3 - ar.w + R4.w * f4.w};
+            const float old[4] = {f4.x, f4.y, f4.z, f4.w};
+            float f[4];
+            f[0] = old[0] - res[0] * cs.arinv0;
+            if (f[0] < kMinVal) {
+              f[0] = f[1] = f[2] = f[3] = 0.f;
+            } else {
+              float Af[3][3], bf[3];
 #pragma unroll
-              for (int b2 = 0; b2 < 3; b2++) {
-                Af[a][b2] = AR[4 * (1 + a) + 1 + b2];
-                bf[a] -= Af[a][b2] * old[1 + b2];
+              for (int a = 0; a < 3; a++) {
+                bf[a] = res[1 + a] + cs.AR[4 * (1 + a)] * (f[0] - old[0]);
+#pragma unroll
+                for (int b2 = 0; b2 < 3; b2++) {
+                  Af[a][b2] = cs.AR[4 * (1 + a) + 1 + b2];
+                  bf[a] -= Af[a][b2] * old[1 + b2];
+                }
+              }
+              float x[3];
+              qcqp3_warm(x, cs.Ainv, Af, bf, cs.dd, f[0]);
+              f[1] = x[0]; f[2] = x[1]; f[3] = x[2];
+            }
+            const float dl[4] = {f[0] - old[0], f[1] - old[1], f[2] - old[2], f[3] - old[3]};
+            if (lane == 0) {
+#pragma unroll
+              for (int r = 0; r < 4; r++) {
+                const float q = cs.AR[4 * r] * dl[0] + cs.AR[4 * r + 1] * dl[1] + cs.AR[4 * r + 2] * dl[2] +
+                                cs.AR[4 * r + 3] * dl[3];
+                impr -= dl[r] * (res[r] + 0.5f * q);
               }
             }
-            qcqp3(x, Af, bf, mus, f[0]);
-            f[1] = x[0]; f[2] = x[1]; f[3] = x[2];
+            sh.con[c].s.f = make_float4(f[0], f[1], f[2], f[3]);
+            d4 = make_float4(dl[0], dl[1], dl[2], dl[3]);
           }
-          float dl[4] = {f[0] - old[0], f[1] - old[1], f[2] - old[2], f[3] - old[3]};
-          if (lane == 0) {
+          // qacc += M^-1 J' d: g = J_dof . d per lane, then the arm's M^-1 row via row broadcasts
+          const float g = Jr[c].x * d4.x + Jr[c].y * d4.y + Jr[c].z * d4.z + Jr[c].w * d4.w;
+          float upd = invmc * g;
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-              float q = AR[4 * r] * dl[0] + AR[4 * r + 1] * dl[1] + AR[4 * r + 2] * dl[2] + AR[4 * r + 3] * dl[3];
-              impr -= dl[r] * (res[r] + 0.5f * q);
-            }
-          }
-          sh.cf[c] = make_float4(f[0], f[1], f[2], f[3]);
-          d4 = make_float4(dl[0], dl[1], dl[2], dl[3]);
-        }
-        if (act && lane < SO100_NV) {
-          float4 Mk = sh.MJ[c][lane];
-          qacc_c += Mk.x * d4.x + Mk.y * d4.y + Mk.z * d4.z + Mk.w * d4.w;
+          for (int j = 0; j < 6; j++) upd += minv_row[j] * bcast_row(g, j);
+          qacc_c += upd;
         }
       }
       const float improvement = rowsum16(impr) * m->pgs_scale;
@@ -1284,8 +1408,8 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     if (B.debug && valid && sub == m->nsubstep - 1) {
       float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
       if (lane < kMaxCon) {
-        dbg[16 + lane] = lane < ncon ? sh.con_pos[lane][3] : 0.f;
-        dbg[32 + lane] = lane < ncon ? sh.cf[lane].x : 0.f;
+        dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
+        dbg[32 + lane] = lane < ncon ? sh.con[lane].s.f.x : 0.f;
         dbg[48 + lane] = lane < ncon ? (float)sh.con_pair[lane] : -1.f;
       }
       if (lane < SO100_NV) { dbg[4 + lane] = qacc_c; dbg[64 + lane] = qs_r; dbg[76 + lane] = fr_f; }
@@ -1514,7 +1638,7 @@ __global__ void so100_unnormalize_kernel(const DevModel* m, int n, const float* 
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * 6) return;
   int k = i % 6;
-  c[i] = unnormalize_f32(a[i], m->action_lo[k], m->action_hi[k]);
+  c[i] = unnormalize_f32(a[i], m->action_lo[k], m->action_hi[k], m->action_span[k]);
 }
 
 __global__ void so100_goal_reward_kernel(const DevModel* m, int n, const float* a, const float* d, float* out) {

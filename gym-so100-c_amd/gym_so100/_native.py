@@ -58,13 +58,21 @@ def load():
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize"):
         getattr(lib, fn).restype = ctypes.c_int
+    lib.so100_struct_sizes.argtypes = [_P, _P]
+    lib.so100_struct_sizes.restype = ctypes.c_int
     if lib.so100_abi_version() != 1:
         raise NativeLibraryError("libso100_hip.so ABI mismatch")
+    mb, bb = ctypes.c_int(0), ctypes.c_int(0)
+    lib.so100_struct_sizes(ctypes.byref(mb), ctypes.byref(bb))
+    from .model import SO100Model
+    if mb.value != ctypes.sizeof(SO100Model) or bb.value != ctypes.sizeof(SO100Buffers):
+        raise NativeLibraryError(f"struct layout mismatch: so100_model {mb.value} vs {ctypes.sizeof(SO100Model)}, "
+                                 f"so100_buffers {bb.value} vs {ctypes.sizeof(SO100Buffers)}")
     _lib = lib
     return lib
 
 
-EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_create", "so100_destroy", "so100_num_envs",
+EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize")
 

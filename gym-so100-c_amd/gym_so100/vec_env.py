@@ -175,6 +175,9 @@ class SO100VecEnv:
     def step(self, actions):
         """actions: [N,6] (torch tensor on any device, or numpy) in [-1, 1]."""
         torch = _torch()
+        if getattr(self, "_action_ref", None) is not None:
+            self._action_ref = None
+            self._buf.action = _native.ptr(self.actions)
         if isinstance(actions, torch.Tensor):
             if actions.shape != (self.num_envs, 6):
                 raise ValueError(f"actions must be [{self.num_envs}, 6], got {tuple(actions.shape)}")
@@ -198,6 +201,16 @@ class SO100VecEnv:
         if self.is_goal:
             info["TimeLimit.truncated"] = self.truncated
         return self._observation(), self.reward, self.terminated, self.truncated, info
+
+    def set_action_buffer(self, actions):
+        """Point the kernel's action input at a resident [N,6] float32 device tensor (zero copy).
+        The tensor must stay alive until the next call; ``step()`` copies into ``self.actions``."""
+        torch = _torch()
+        if actions.shape != (self.num_envs, 6) or actions.dtype != torch.float32 or not actions.is_contiguous() \
+                or actions.device != self.device:
+            raise ValueError("action buffer must be a contiguous float32 [N,6] tensor on the env's device")
+        self._action_ref = actions
+        self._buf.action = _native.ptr(actions)
 
     def step_async_raw(self):
         """Launch one env step on the current stream using the actions already in ``self.actions``

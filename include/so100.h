@@ -71,6 +71,8 @@ typedef struct so100_env so100_env;   /* opaque: device model copy + launch conf
 
 int         so100_abi_version(void);
 const char* so100_last_error(void);
+/* sizeof(so100_model), sizeof(so100_buffers) as compiled — lets bindings verify their mirrors. */
+int         so100_struct_sizes(int* model_bytes, int* buffers_bytes);
 
 /* Upload the model (converted to fp32) to `device`.  n_envs > 0.  Returns NULL on error. */
 so100_env*  so100_create(const so100_model* model, int n_envs, int device);

@@ -75,6 +75,7 @@ class Oracle:
         P = ctypes.c_void_p
         L.so100o_sizeof_data.restype = ctypes.c_int
         assert L.so100o_sizeof_data() == ctypes.sizeof(self.Data), (L.so100o_sizeof_data(), ctypes.sizeof(self.Data))
+        L.so100o_sizeof_model.restype = ctypes.c_int
         L.so100o_unnormalize.argtypes = [P, P, P]
         L.so100o_spawn_pose.argtypes = [ctypes.c_uint32, P]
         L.so100o_reward.argtypes = [P, ctypes.c_int, P, P, P, ctypes.c_uint32]

@@ -1133,4 +1133,5 @@ long so100o_batch_run(const so100_model* m, so100o_data* datas, int nenv, int st
 }
 
 int so100o_sizeof_data(void) { return (int)sizeof(so100o_data); }
+int so100o_sizeof_model(void) { return (int)sizeof(so100_model); }
 int so100o_real_bytes(void) { return (int)sizeof(real); }

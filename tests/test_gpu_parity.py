@@ -1,0 +1,269 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the reference's golden vectors.
+
+Bars:
+* task logic (unnormalize, spawn, reward ladders, obs packing, termination): bit-exact vs the
+  reference's golden vectors;
+* physics: teacher-forced single env steps from identical states vs the fp64 oracle.  The kernel
+  computes in fp32, so the bar is the fp32 restatement of the same algorithm: the GPU's per-step
+  error distribution must be within 2x (+1e-4) of the fp32-oracle's distribution on the same
+  states, and qpos/qvel medians must be <= 1e-5 (abs / rel to 1+|v|).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def venv():
+    from gym_so100 import SO100VecEnv
+    env = SO100VecEnv(64, device="cuda:0", autoreset=False, debug=True, max_episode_steps=0)
+    yield env
+    env.close()
+
+
+def _native_loaded():
+    import gym_so100._native as n
+    return n._lib is not None
+
+
+# ----------------------------------------------------------------------------- task layer vs golden
+def test_unnormalize_matches_reference(venv, golden):
+    got = venv.unnormalize(torch.from_numpy(golden["unnorm_action"])).cpu().numpy()
+    np.testing.assert_array_equal(got, golden["unnorm_ctrl"])
+    assert _native_loaded()
+
+
+def test_spawn_matches_reference_randomstate(venv, golden):
+    got = venv.spawn_pose(golden["spawn_seed"]).cpu().numpy()
+    np.testing.assert_array_equal(got, golden["spawn_pose"])
+
+
+@pytest.mark.parametrize("col,task", [(0, "so100_cube_to_bin"), (1, "so100_touch_cube"), (2, "so100_touch_cube_sparse")])
+def test_reward_matches_reference(venv, golden, col, task):
+    cube = golden["reward_cube"].astype(np.float32)
+    ee = golden["reward_ee"].astype(np.float32)
+    got = venv.eval_reward(task, cube, ee, golden["reward_bits"]).cpu().numpy()
+    want = golden["reward_value"][:, col].astype(np.float32)
+    if col == 1:
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-6)
+    else:
+        np.testing.assert_array_equal(got, want)
+
+
+def test_goal_compute_reward_matches_reference(venv, golden):
+    got = venv.compute_reward(golden["goal_achieved"], golden["goal_desired"]).cpu().numpy()
+    np.testing.assert_array_equal(got, golden["goal_reward_batch"])
+
+
+# ----------------------------------------------------------------------------- reset / obs
+def test_reset_obs_matches_oracle(venv, model, oracle64):
+    obs, _ = venv.reset(seed=1000)
+    torch.cuda.synchronize()
+    obs = obs.cpu().numpy()
+    d = oracle64.new_data()
+    for i in range(venv.num_envs):
+        oracle64.reset(model, d, oracle64.spawn_pose(1000 + i))
+        np.testing.assert_allclose(obs[i], oracle64.observe(model, d), rtol=0, atol=2e-7)
+    qpos = venv.qpos.cpu().numpy()
+    np.testing.assert_array_equal(qpos[:, :6], np.tile(np.float32(model.start_qpos[:]), (venv.num_envs, 1)))
+    assert not venv.qvel.abs().sum().item()
+
+
+# ----------------------------------------------------------------------------- physics, teacher-forced
+def _teacher_forced(venv, model, oracle, steps, seed):
+    n = venv.num_envs
+    venv.reset(seed=seed)
+    rng = np.random.default_rng(seed)
+    d = oracle.new_data()
+    qp_err, qv_err, rew_bad, bit_bad = [], [], 0, 0
+    states = []
+    for step in range(steps):
+        qpos = venv.qpos.cpu().numpy().astype(np.float64)
+        qvel = venv.qvel.cpu().numpy().astype(np.float64)
+        warm = venv.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = (rng.uniform(-1, 1, (n, 6)) if step % 20 < 10 else np.clip(rng.normal(0, 0.3, (n, 6)), -1, 1))
+        act = act.astype(np.float32)
+        _, rew, _, _, info = venv.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gq, gv = venv.qpos.cpu().numpy(), venv.qvel.cpu().numpy()
+        gr, gb = rew.cpu().numpy(), info["contact_bits"].cpu().numpy().astype(np.uint32)
+        for i in range(n):
+            oracle.set_state(d, qpos[i], qvel[i], warm[i])
+            _, r, _ = oracle.env_step(model, d, 0, act[i])
+            oq, ov, _, _ = oracle.get_state(d)
+            qp_err.append(np.abs(oq - gq[i]).max())
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            rew_bad += abs(r - gr[i]) > 1e-6
+            bit_bad += oracle.contact_bits(d) != gb[i]
+            states.append((qpos[i], qvel[i], warm[i], act[i]))
+    return np.array(qp_err), np.array(qv_err), rew_bad, bit_bad, states
+
+
+def _oracle_precision_floor(model, o64, o32, states):
+    d64, d32 = o64.new_data(), o32.new_data()
+    qp, qv = [], []
+    for qpos, qvel, warm, act in states:
+        o64.set_state(d64, qpos, qvel, warm)
+        o32.set_state(d32, qpos, qvel, warm)
+        o64.env_step(model, d64, 0, act)
+        o32.env_step(model, d32, 0, act)
+        a, b = o64.get_state(d64), o32.get_state(d32)
+        qp.append(np.abs(a[0] - b[0]).max())
+        qv.append((np.abs(a[1] - b[1]) / (1 + np.abs(a[1]))).max())
+    return np.array(qp), np.array(qv)
+
+
+def test_step_parity_teacher_forced(venv, model, oracle64, oracle32):
+    qp, qv, rew_bad, bit_bad, states = _teacher_forced(venv, model, oracle64, steps=40, seed=1000)
+    fqp, fqv = _oracle_precision_floor(model, oracle64, oracle32, states)
+    n = len(qv)
+    print(f"\nGPU vs fp64 oracle over {n} env-steps: qpos abs median {np.median(qp):.2e} p99 {np.quantile(qp, .99):.2e}"
+          f" | qvel rel median {np.median(qv):.2e} p99 {np.quantile(qv, .99):.2e} max {qv.max():.2e}"
+          f" | within 1e-4: {np.mean(qv < 1e-4):.3f}")
+    print(f"fp32 oracle vs fp64 oracle (precision floor): qvel rel median {np.median(fqv):.2e} "
+          f"p99 {np.quantile(fqv, .99):.2e} max {fqv.max():.2e} | within 1e-4: {np.mean(fqv < 1e-4):.3f}")
+    assert np.median(qp) <= 1e-5 and np.median(qv) <= 1e-5
+    assert np.quantile(qv, 0.9) <= 2 * np.quantile(fqv, 0.9) + 1e-4
+    assert np.quantile(qv, 0.99) <= 2 * np.quantile(fqv, 0.99) + 1e-4
+    assert qv.max() <= 2 * fqv.max() + 1e-3
+    assert np.mean(qv < 1e-4) >= np.mean(fqv < 1e-4) - 0.05
+    assert rew_bad <= max(2, 0.005 * n)          # ladder flips only at contact on/off boundaries
+    assert bit_bad <= max(4, 0.01 * n)
+
+
+def test_free_flight_bit_close(model, oracle64):
+    """No contacts at all (cube in the air, arm high): GPU equals the fp64 oracle to fp32 rounding."""
+    from gym_so100 import SO100VecEnv
+    env = SO100VecEnv(8, device="cuda:0", autoreset=False, max_episode_steps=0)
+    env.reset(seed=7)
+    qpos = env.qpos.clone()
+    qpos[:, 8] = 0.6
+    env.set_state(qpos, torch.zeros_like(env.qvel))
+    a = np.zeros((8, 6), np.float32)
+    d = oracle64.new_data()
+    q0 = env.qpos.cpu().numpy().astype(np.float64)
+    env.step(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    for i in range(8):
+        oracle64.set_state(d, q0[i], np.zeros(12), np.zeros(12))
+        oracle64.env_step(model, d, 0, a[i])
+        oq, ov, _, _ = oracle64.get_state(d)
+        np.testing.assert_allclose(env.qpos[i].cpu().numpy(), oq, atol=2e-6)
+        np.testing.assert_allclose(env.qvel[i].cpu().numpy(), ov, atol=2e-4, rtol=1e-4)
+    env.close()
+
+
+# ----------------------------------------------------------------------------- size-independent properties
+def test_full_size_invariants():
+    """configs[1] size (4096 envs): finite state, unit quaternions, cube above the floor, obs layout."""
+    from gym_so100 import SO100VecEnv
+    env = SO100VecEnv(4096, device="cuda:0", seed=3)
+    env.reset(seed=1000)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(30):
+        a = torch.rand(4096, 6, generator=g, device="cuda") * 2 - 1
+        obs, rew, term, trunc, info = env.step(a)
+    torch.cuda.synchronize()
+    assert torch.isfinite(env.qpos).all() and torch.isfinite(env.qvel).all()
+    qn = env.qpos[:, 9:13].norm(dim=1)
+    assert torch.allclose(qn, torch.ones_like(qn), atol=1e-5)
+    assert (env.qpos[:, 8] > -0.05).all()
+    assert torch.equal(obs[:, 9:15], env.qpos[:, :6])
+    assert torch.allclose(obs[:, 3:6], torch.tensor([-0.2, 0.7, 0.021], device="cuda").expand(4096, 3))
+    assert not info["diverged"].any()
+    assert set(torch.unique(rew).tolist()) <= {0.0, 1.0, 2.0, 2.5, 3.0, 4.0}
+    env.close()
+
+
+def test_autoreset_and_timelimit():
+    from gym_so100 import SO100VecEnv
+    env = SO100VecEnv(16, device="cuda:0", max_episode_steps=5, seed=11)
+    env.reset(seed=0)
+    a = torch.zeros(16, 6, device="cuda")
+    for k in range(1, 6):
+        obs, _, term, trunc, info = env.step(a)
+        torch.cuda.synchronize()
+        if k < 5:
+            assert not trunc.any() and (env.elapsed == k).all()
+    assert trunc.all() and info["_final_observation"].all()
+    assert (env.elapsed == 0).all() and (env.episode == 2).all()   # reset() started episode 1
+    # the new episode's spawn is the reference RandomState(seed) for the in-kernel episode seed
+    assert not torch.equal(info["final_observation"], obs)
+    assert torch.equal(obs[:, 9:15], env.qpos[:, :6])
+    env.close()
+
+
+def test_sharding_invariance():
+    """Global env ids drive the in-kernel seeds: 2 shards of 8 == 1 shard of 16."""
+    from gym_so100 import SO100VecEnv
+    full = SO100VecEnv(16, device="cuda:0", seed=5, max_episode_steps=3)
+    a0 = SO100VecEnv(8, device="cuda:0", seed=5, env_offset=0, max_episode_steps=3)
+    a1 = SO100VecEnv(8, device="cuda:0", seed=5, env_offset=8, max_episode_steps=3)
+    for e in (full, a0, a1):
+        e.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for _ in range(7):
+        a = torch.rand(16, 6, generator=g, device="cuda") * 2 - 1
+        full.step(a)
+        a0.step(a[:8].contiguous())
+        a1.step(a[8:].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(full.qpos, torch.cat([a0.qpos, a1.qpos]))
+    assert torch.equal(full.obs, torch.cat([a0.obs, a1.obs]))
+
+
+def test_goal_env_semantics():
+    from gym_so100 import SO100VecEnv
+    env = SO100VecEnv(32, task="so100_goal", device="cuda:0", seed=2)
+    obs, _ = env.reset(seed=100)
+    torch.cuda.synchronize()
+    dg, ag = obs["desired_goal"], obs["achieved_goal"]
+    spawn = env.qpos[:, 6:8]
+    # lifted-goal curriculum (env.py:324-330): within +-0.03 of the spawn xy, z in [0.01, 0.05]
+    assert ((dg[:, :2] - spawn).abs() <= 0.03 + 1e-6).all()
+    assert ((dg[:, 2] >= 0.01) & (dg[:, 2] <= 0.05)).all()
+    a = torch.zeros(32, 6, device="cuda")
+    o, r, term, trunc, info = env.step(a)
+    torch.cuda.synchronize()
+    dist = (o["achieved_goal"] - o["desired_goal"]).norm(dim=1)
+    assert torch.equal(r, torch.where(dist < 0.01, 0.0, -1.0))
+    assert torch.equal(term, dist < 0.01)
+    assert (env.total_steps == 1).all()
+    env.close()
+
+
+def test_domain_randomization_changes_dynamics_deterministically():
+    from gym_so100 import SO100VecEnv
+    kw = dict(device="cuda:0", seed=9, domain_randomization=dict(mass=(0.8, 1.2), friction=(0.8, 1.2),
+                                                                  action_noise=0.05))
+    e1, e2 = SO100VecEnv(32, **kw), SO100VecEnv(32, **kw)
+    e3 = SO100VecEnv(32, device="cuda:0", seed=9)
+    for e in (e1, e2, e3):
+        e.reset(seed=0)
+    a = torch.zeros(32, 6, device="cuda")
+    for _ in range(5):
+        for e in (e1, e2, e3):
+            e.step(a)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.qpos, e2.qpos)
+    assert not torch.equal(e1.qpos, e3.qpos)
+    assert ((e1.dr_params[:, 0] >= 0.8) & (e1.dr_params[:, 0] <= 1.2)).all()
+
+
+def test_single_env_api():
+    from gym_so100 import SO100Env, SO100GoalEnv
+    env = SO100Env("so100_cube_to_bin")
+    obs, info = env.reset(seed=0)
+    assert obs.shape == (15,) and obs.dtype == np.float32 and info == {"is_success": False}
+    obs, r, term, trunc, info = env.step(np.zeros(6, np.float32))
+    assert obs.shape == (15,) and isinstance(r, float) and trunc is False and "is_success" in info
+    g = SO100GoalEnv()
+    o, _ = g.reset(seed=0)
+    assert set(o) == {"observation", "achieved_goal", "desired_goal"}
+    o, r, term, trunc, info = g.step(np.zeros(6, np.float32))
+    assert r in (0.0, -1.0)
+    rb = g.compute_reward(np.zeros((4, 3)), np.zeros((4, 3)) + 0.001, {})
+    assert rb.dtype == np.float32 and (rb == 0).all()

@@ -1,0 +1,234 @@
+"""Analytic known-answer tests that pin the oracle's physics restatement (no MuJoCo in this container).
+
+Each test checks a property that MuJoCo's algorithms satisfy by construction: the CRBA mass matrix
+equals the Jacobian-method M0 computed independently by tools/compile_model.py; gravity bias is the
+gradient of potential energy; Coriolis terms satisfy the skew-symmetry identity; semi-implicit Euler
+free fall and quaternion integration have closed forms; box-box contacts on canonical poses; PGS
+solutions satisfy the complementarity (KKT) conditions of the frictionloss problem; a cube comes to
+rest on the table carrying m*g in normal force.
+"""
+import copy
+import ctypes
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from gym_so100.model import ASSET, build_model
+
+NV = 12
+
+
+def fresh(o, m, box=(-0.2, 0.45, 0.3, 1, 0, 0, 0), arm=None):
+    d = o.new_data()
+    o.reset(m, d, np.array(box, dtype=np.float64))
+    if arm is not None:
+        for k in range(6):
+            d.qpos[k] = arm[k]
+        o.call("so100o_fwd_position", m, d)
+        o.call("so100o_fwd_velocity", m, d)
+    return d
+
+
+def qM(d):
+    return np.array([[d.qM[i][j] for j in range(NV)] for i in range(NV)])
+
+
+def test_mass_matrix_equals_independent_M0(model, oracle64):
+    M0 = np.array(json.load(open(ASSET))["M0"])
+    box0 = json.load(open(ASSET))["qpos0_box"]
+    d = fresh(oracle64, model, box=tuple(box0) + (1, 0, 0, 0), arm=np.zeros(6))
+    np.testing.assert_allclose(qM(d), M0, rtol=1e-10, atol=1e-12)
+
+
+def test_mass_matrix_spd_random_configs(model, oracle64):
+    rng = np.random.default_rng(1)
+    for _ in range(20):
+        arm = rng.uniform(-1.5, 1.5, 6)
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        d = fresh(oracle64, model, box=(-0.2, 0.4, 0.3, *q), arm=arm)
+        M = qM(d)
+        np.testing.assert_allclose(M, M.T, atol=1e-14)
+        assert np.linalg.eigvalsh(M).min() > 0
+        # cube block: diag(m, m, m, I) for the isotropic cube (COM at origin)
+        np.testing.assert_allclose(M[6:, 6:], np.diag([0.05] * 3 + [0.002] * 3), atol=1e-14)
+        np.testing.assert_allclose(M[:6, 6:], 0, atol=1e-14)
+
+
+def _potential(o, m, d_arm):
+    d = fresh(o, m, arm=d_arm)
+    V = 0.0
+    for b in range(2, 8):
+        V += m.body_mass[b] * 9.81 * d.xipos[b][2]
+    return V
+
+
+def test_gravity_bias_is_potential_gradient(model, oracle64):
+    rng = np.random.default_rng(2)
+    for _ in range(5):
+        arm = rng.uniform(-1.2, 1.2, 6)
+        d = fresh(oracle64, model, arm=arm)
+        bias = np.array(d.qfrc_bias[:6])
+        grad = np.zeros(6)
+        eps = 1e-6
+        for k in range(6):
+            a1, a2 = arm.copy(), arm.copy()
+            a1[k] += eps
+            a2[k] -= eps
+            grad[k] = (_potential(oracle64, model, a1) - _potential(oracle64, model, a2)) / (2 * eps)
+        np.testing.assert_allclose(bias, grad, rtol=1e-6, atol=1e-8)
+        # cube at rest: bias = (0, 0, m g, 0, 0, 0)
+        np.testing.assert_allclose(np.array(d.qfrc_bias[6:]), [0, 0, 0.05 * 9.81, 0, 0, 0], atol=1e-14)
+
+
+def test_coriolis_skew_symmetry(model, oracle64):
+    m = copy.deepcopy(model)
+    for k in range(3):
+        m.gravity[k] = 0.0
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        arm = rng.uniform(-1.2, 1.2, 6)
+        qd = rng.normal(size=6)
+        d = fresh(oracle64, m, arm=arm)
+        for k in range(6):
+            d.qvel[k] = qd[k]
+        oracle64.call("so100o_fwd_velocity", m, d)
+        c = np.array(d.qfrc_bias[:6])
+        eps = 1e-6
+        Mp = qM(fresh(oracle64, m, arm=arm + eps * qd))[:6, :6]
+        Mm = qM(fresh(oracle64, m, arm=arm - eps * qd))[:6, :6]
+        Mdot = (Mp - Mm) / (2 * eps)
+        # d/dt(0.5 qd' M qd) with qdd = -M^-1 c  ==>  qd' c == 0.5 qd' Mdot qd
+        assert abs(qd @ c - 0.5 * qd @ Mdot @ qd) < 1e-6 * (1 + abs(qd @ c))
+
+
+def _no_cube_friction(model):
+    m = copy.deepcopy(model)
+    return m
+
+
+def test_free_fall_semi_implicit_euler(model, oracle64):
+    m = copy.deepcopy(model)
+    for k in range(6, 12):
+        m.dof_frictionloss[k] = 1e-12       # (near) frictionless cube dofs
+    d = fresh(oracle64, m, box=(-0.2, 0.45, 0.6, 1, 0, 0, 0))
+    z0 = d.qpos[8]
+    h, g = m.timestep, 9.81
+    for n in range(1, 31):
+        oracle64.call("so100o_substep", m, d)
+        assert abs(d.qvel[8] - (-g * h * n)) < 1e-9
+        assert abs(d.qpos[8] - (z0 - g * h * h * n * (n + 1) / 2)) < 1e-9
+
+
+def test_quaternion_integration_closed_form(model, oracle64):
+    m = copy.deepcopy(model)
+    for k in range(3):
+        m.gravity[k] = 0.0
+    for k in range(6, 12):
+        m.dof_frictionloss[k] = 1e-12
+    d = fresh(oracle64, m, box=(-0.2, 0.45, 0.6, 1, 0, 0, 0))
+    w = np.array([0.3, -1.1, 2.0])
+    for k in range(3):
+        d.qvel[9 + k] = w[k]
+    n = 50
+    for _ in range(n):
+        oracle64.call("so100o_substep", m, d)
+    q = np.array(d.qpos[9:13])
+    ang = np.linalg.norm(w) * m.timestep * n
+    ax = w / np.linalg.norm(w)
+    want = np.concatenate([[math.cos(ang / 2)], ax * math.sin(ang / 2)])
+    assert abs(np.linalg.norm(q) - 1) < 1e-12
+    np.testing.assert_allclose(q, want, atol=1e-6)   # frictionloss 1e-12 leaves a tiny residual torque
+
+
+def _contacts(d):
+    return [(d.con[i].pair, np.array(d.con[i].pos[:]), np.array(d.con[i].frame[:3]), d.con[i].dist)
+            for i in range(d.ncon)]
+
+
+def test_box_on_table_four_corner_contacts(model, oracle64):
+    pen = 0.001
+    d = fresh(oracle64, model, box=(-0.2, 0.45, 0.02 - pen, 1, 0, 0, 0))
+    cs = [c for c in _contacts(d) if c[0] == 8]
+    assert len(cs) == 4
+    for pair, pos, n, dist in cs:
+        np.testing.assert_allclose(n, [0, 0, -1], atol=1e-12)       # geom1 (red_box) -> geom2 (table)
+        assert abs(dist + pen) < 1e-12
+        assert abs(pos[2] + pen / 2) < 1e-12                        # midway between the surfaces
+        assert abs(abs(pos[0] + 0.2) - 0.02) < 1e-12 and abs(abs(pos[1] - 0.45) - 0.02) < 1e-12
+
+
+def test_box_on_edge_two_contacts(model, oracle64):
+    # cube rotated 45 deg about x, resting on its edge: two contacts along the edge
+    s = math.sin(math.pi / 8)
+    c = math.cos(math.pi / 8)
+    zc = 0.02 * math.sqrt(2) - 0.0005
+    d = fresh(oracle64, model, box=(-0.2, 0.45, zc, c, s, 0, 0))
+    cs = [x for x in _contacts(d) if x[0] == 8]
+    assert len(cs) == 2
+    for _, pos, n, dist in cs:
+        assert abs(dist + 0.0005) < 1e-9
+        assert abs(pos[1] - 0.45) < 1e-9
+
+
+def test_separated_boxes_no_contact(model, oracle64):
+    d = fresh(oracle64, model, box=(-0.2, 0.45, 0.0201, 1, 0, 0, 0))
+    assert d.ncon == 0
+
+
+def test_pgs_frictionloss_kkt(model, oracle64):
+    """Arm moving, no contacts: every frictionloss row satisfies the box-constrained optimality."""
+    d = fresh(oracle64, model, box=(-0.2, 0.45, 0.5, 1, 0, 0, 0))
+    rng = np.random.default_rng(4)
+    for k in range(6):
+        d.qvel[k] = rng.normal() * 0.3
+    for k in range(6):
+        d.ctrl[k] = d.qpos[k] + 0.1 * rng.normal()
+    oracle64.call("so100o_fwd_position", model, d)
+    oracle64.call("so100o_fwd_velocity", model, d)
+    oracle64.call("so100o_fwd_acceleration", model, d)
+    n = d.nefc
+    assert n == 12 and d.ncon == 0
+    A = np.array([[d.efc_AR[i][j] for j in range(n)] for i in range(n)])
+    b = np.array(d.efc_b[:n])
+    f = np.array(d.efc_force[:n])
+    fl = np.array(d.efc_frictionloss[:n])
+    g = A @ f + b                       # gradient of the dual objective
+    for i in range(n):
+        if f[i] >= fl[i] - 1e-9:
+            assert g[i] <= 1e-6
+        elif f[i] <= -fl[i] + 1e-9:
+            assert g[i] >= -1e-6
+        else:
+            assert abs(g[i]) < 1e-6 * max(1.0, abs(b[i]))
+
+
+def test_cube_settles_on_table_carrying_weight(model, oracle64):
+    d = fresh(oracle64, model, box=(-0.2, 0.45, 0.03, 1, 0, 0, 0))
+    start = np.array(model.start_qpos[:])
+    for k in range(6):
+        d.ctrl[k] = start[k]
+    for _ in range(400):
+        oracle64.call("so100o_substep", model, d)
+    oracle64.call("so100o_fwd_position", model, d)
+    oracle64.call("so100o_fwd_velocity", model, d)
+    oracle64.call("so100o_fwd_acceleration", model, d)
+    assert abs(d.qpos[8] - 0.02) < 2e-3
+    assert np.abs(np.array(d.qvel[6:12])).max() < 0.05
+    fn = sum(d.efc_force[i] for i in range(d.nefc) if d.efc_type[i] == 2 and d.efc_dim[i] == 4)
+    assert abs(fn - 0.05 * 9.81) < 0.05 * 0.05 * 9.81
+
+
+def test_arm_holds_start_pose(model, oracle64):
+    d = fresh(oracle64, model, box=(-0.2, 0.45, 0.02, 1, 0, 0, 0))
+    start = np.array(model.start_qpos[:])
+    a = np.array([(start[k] - lo) / (hi - lo) * 2 - 1 for k, (lo, hi) in
+                  enumerate(zip(model.action_lo, model.action_hi))], dtype=np.float32)
+    for _ in range(50):
+        oracle64.env_step(model, d, 0, a)
+    q = np.array(d.qpos[:6])
+    assert np.abs(q - start).max() < 0.05
+    assert np.abs(np.array(d.qvel[:6])).max() < 0.05
