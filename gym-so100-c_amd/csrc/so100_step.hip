@@ -22,21 +22,45 @@
 namespace so100 {
 
 #define DEV __device__ __forceinline__
+
+// Diagnostic build only (-DSO100_STAMPS): per-wave cycle attribution by phase (s_memtime), written to
+// the debug buffer's tail.  The product build compiles these to nothing.
+#ifdef SO100_STAMPS
+#define STAMP_DECL unsigned long long st_prev_ = 0, st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(slot)                                                                              \
+  do {                                                                                           \
+    unsigned long long t_;                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if ((slot) >= 0) st_acc_[(slot)] += t_ - st_prev_;                                           \
+    st_prev_ = t_;                                                                               \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(slot) do {} while (0)
+#endif
 constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;
 
 // ------------------------------------------------------------------ LDS layout (per env)
-struct __attribute__((aligned(16))) ConSolve {   // per-contact PGS data (192 B)
-  float AR[16];        // 4x4 diagonal block of A + R (normal, tangent1, tangent2, torsion)
-  float Ainv[9];       // inverse of the cone-scaled friction block (QCQP at lambda = 0)
-  float dd[3];         // cone coefficients (mu0, mu0, mu1)
+struct __attribute__((aligned(16))) ConSolve {   // per-contact PGS data (144 B = 9 x ds_read_b128;
+                                                 // the PGS reads it as float4[9], keep the order)
+  // symmetric 4x4 block of A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
+  float ar[10];
+  // eigen-decomposition of the cone-scaled friction block As = D A11 D (D = diag(mu0, mu0, mu1)):
+  // As = Q diag(lam) Q', Q row-major (columns = eigenvectors) — QCQP Newton without 3x3 inverses
+  float q[9];
+  float lam[3];
+  float R0, arinv0;    // normal-row regulariser, 1 / AR00
   float4 aref;
-  float4 R;
-  float4 f;            // current forces
-  float arinv0;        // 1 / AR[0][0]
-  float pad[3];
+  float4 f;            // current forces (normal, t1, t2, torsion)
+  float mu0, mu1;      // cone coefficients (mu0, mu0, mu1)
+  float R1, R3;        // friction-row regularisers (R2 = R1)
 };
+static_assert(sizeof(ConSolve) == 144 && offsetof(ConSolve, aref) == 96 && offsetof(ConSolve, f) == 112 &&
+                  offsetof(ConSolve, mu0) == 128, "ConSolve layout is read as float4[9] in the PGS");
 struct __attribute__((aligned(16))) ConGeom {    // per-contact geometry (collision output)
   float pos[4];
   float frame[12];     // normal (geom1 -> geom2), tangent1, tangent2
@@ -55,11 +79,13 @@ struct __attribute__((aligned(16))) SerialScratch {   // per-body arrays of the 
 struct __attribute__((aligned(16))) EnvShared {
   float qpos[16];
   float qvel[16];
-  float warm[16];
   float qacc_smooth[16];
-  float vec[16];
+  union {
+    float vec[16];
+    int cnt[16];                 // S3 compaction counts (vec is free during collision)
+  };
   float ctrl[8];
-  float minv[6][8];
+  float minv[6][6];
   float inv_mcube[8];
   float anchor[6][4];
   float axis[6][4];
@@ -69,7 +95,6 @@ struct __attribute__((aligned(16))) EnvShared {
   float jaw_mat[2][12];
   float site_cube[4];
   float site_ee[4];
-  int cnt[16];
   int ncon;
   int nlim;
   int misc[2];
@@ -964,50 +989,79 @@ DEV void inv3(float Pi[3][3], const float P[3][3]) {
     for (int j = 0; j < 3; j++) Pi[i][j] *= id;
 }
 
-// MuJoCo mju_QCQP3 restated, with the lambda = 0 inverse precomputed once per substep (Ainv): the
-// sticking case (inside the cone) costs one 3x3 mat-vec; sliding contacts continue Newton on lambda.
-DEV void qcqp3_warm(float* x, const float* Ainv, const float A0[3][3], const float* b0, const float* dd, float r) {
-  float b[3], y[3];
+// Symmetric 3x3 eigen-decomposition by cyclic Jacobi (5 sweeps: quadratic convergence reaches fp32
+// round-off for 3x3): A = Q diag(lam) Q', columns of Q are the eigenvectors.
+DEV void eig3_sym(const float A0[3][3], float lam[3], float Q[3][3]) {
+  float a[3][3];
 #pragma unroll
-  for (int i = 0; i < 3; i++) b[i] = b0[i] * dd[i];
+  for (int i = 0; i < 3; i++)
 #pragma unroll
-  for (int i = 0; i < 3; i++) y[i] = -(Ainv[3 * i] * b[0] + Ainv[3 * i + 1] * b[1] + Ainv[3 * i + 2] * b[2]);
-  float val = y[0] * y[0] + y[1] * y[1] + y[2] * y[2] - r * r;
-  if (val >= 1e-10f) {
-    float deriv = 0.f;
+    for (int j = 0; j < 3; j++) { a[i][j] = A0[i][j]; Q[i][j] = (i == j) ? 1.f : 0.f; }
 #pragma unroll
-    for (int i = 0; i < 3; i++) deriv += y[i] * (Ainv[3 * i] * y[0] + Ainv[3 * i + 1] * y[1] + Ainv[3 * i + 2] * y[2]);
-    deriv *= -2.f;
-    float delta = -val / deriv;
-    if (delta >= 1e-10f) {
-      float A[3][3];
+  for (int sweep = 0; sweep < 5; sweep++) {
 #pragma unroll
-      for (int i = 0; i < 3; i++)
+    for (int pq = 0; pq < 3; pq++) {
+      const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
+      const float apq = a[p][q];
+      if (fabsf(apq) > 1e-30f) {
+        const float theta = (a[q][q] - a[p][p]) / (2.f * apq);
+        const float t = copysignf(1.f, theta) / (fabsf(theta) + sqrtf(theta * theta + 1.f));
+        const float c = 1.f / sqrtf(t * t + 1.f), sn = t * c;
 #pragma unroll
-        for (int j = 0; j < 3; j++) A[i][j] = A0[i][j] * dd[i] * dd[j];
-      float la = delta;
-      for (int it = 1; it < 20; it++) {
-        float P[3][3], Pi[3][3];
+        for (int k = 0; k < 3; k++) {           // columns p, q
+          const float akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - sn * akq;
+          a[k][q] = sn * akp + c * akq;
+        }
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+        for (int k = 0; k < 3; k++) {           // rows p, q
+          const float apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - sn * aqk;
+          a[q][k] = sn * apk + c * aqk;
+        }
 #pragma unroll
-          for (int j = 0; j < 3; j++) P[i][j] = A[i][j] + (i == j ? la : 0.f);
-        inv3(Pi, P);
-#pragma unroll
-        for (int i = 0; i < 3; i++) y[i] = -(Pi[i][0] * b[0] + Pi[i][1] * b[1] + Pi[i][2] * b[2]);
-        val = y[0] * y[0] + y[1] * y[1] + y[2] * y[2] - r * r;
-        if (val < 1e-10f) break;
-        deriv = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; i++) deriv += y[i] * (Pi[i][0] * y[0] + Pi[i][1] * y[1] + Pi[i][2] * y[2]);
-        deriv *= -2.f;
-        delta = -val / deriv;
-        if (delta < 1e-10f) break;
-        la += delta;
+        for (int k = 0; k < 3; k++) {
+          const float qkp = Q[k][p], qkq = Q[k][q];
+          Q[k][p] = c * qkp - sn * qkq;
+          Q[k][q] = sn * qkp + c * qkq;
+        }
       }
     }
   }
-  x[0] = y[0] * dd[0]; x[1] = y[1] * dd[1]; x[2] = y[2] * dd[2];
+  lam[0] = a[0][0]; lam[1] = a[1][1]; lam[2] = a[2][2];
+}
+
+// MuJoCo mju_QCQP3 restated: min 0.5 x'Ax + x'b s.t. sum (x_i/d_i)^2 <= r^2, Newton on the multiplier
+// la from la = 0.  In the eigenbasis of As = D A D (precomputed per substep) every iterate
+// y(la) = -(As + la I)^-1 D b is c_i / (lam_i + la) with c = -Q'Db, so an iteration is three
+// reciprocals instead of a 3x3 inverse; the iterates are MuJoCo's (same val/deriv/delta tests).
+DEV void qcqp3_eig(float* x, const float* Q, const float* lam, const float* b0, float mu0, float mu1, float r) {
+  const float dd[3] = {mu0, mu0, mu1};
+  float bs[3], c[3], w[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) bs[i] = b0[i] * dd[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) c[i] = -(Q[i] * bs[0] + Q[3 + i] * bs[1] + Q[6 + i] * bs[2]);   // -Q' b
+#pragma unroll
+  for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i]); w[i] = c[i] * d[i]; }
+  float val = w[0] * w[0] + w[1] * w[1] + w[2] * w[2] - r * r;
+  if (val >= 1e-10f) {
+    float la = 0.f;
+    for (int it = 0; it < 20; it++) {
+      // deriv = -2 y'(As + la I)^-1 y = -2 sum w_i^2 d_i
+      const float deriv = -2.f * (w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2]);
+      const float delta = -val * __builtin_amdgcn_rcpf(deriv);
+      if (delta < 1e-10f) break;
+      la += delta;
+#pragma unroll
+      for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
+      val = w[0] * w[0] + w[1] * w[1] + w[2] * w[2] - r * r;
+      if (val < 1e-10f) break;
+    }
+  }
+  // y = Q w, x = D y
+#pragma unroll
+  for (int i = 0; i < 3; i++) x[i] = (Q[3 * i] * w[0] + Q[3 * i + 1] * w[1] + Q[3 * i + 2] * w[2]) * dd[i];
 }
 
 // ------------------------------------------------------------------ the step kernel
@@ -1057,7 +1111,7 @@ DEV void write_obs(const DevModel* __restrict__ m, const EnvShared& sh, int lane
   if (lane < SO100_NOBS) dst[lane] = v;
 }
 
-__global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
+__global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) {
   __shared__ EnvShared shm[kEnvsPerBlock];
   const DevModel* __restrict__ m = args.m;
   const int tid = threadIdx.x;
@@ -1090,17 +1144,20 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
   }
 
   const float h = m->timestep;
+  STAMP_DECL
+  STAMP(-1);
   float dbg_iter = 0.f, dbg_impr = 0.f;
   int dbg_nefc = 0;
 
   for (int sub = 0; sub < m->nsubstep; sub++) {
     // ---------------- S1: stage state in LDS
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
-    if (lane < SO100_NV) { sh.qvel[lane] = qvel_r; sh.warm[lane] = warm_r; }
+    if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
     __syncthreads();
     // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
     if (lane == 0) serial_stage(m, sh, true, mscale);
     __syncthreads();
+    STAMP(0);
     // ---------------- S3: collision, one pair per lane, compaction in pair order
     PairContacts pc;
     pc.n = 0;
@@ -1130,6 +1187,7 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
 
+    STAMP(1);
     // ---------------- S4/S5: contact Jacobian rows and M^-1 J' in registers (lane = dof, contacts unrolled)
     float minv_row[6];
 #pragma unroll
@@ -1242,21 +1300,23 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
               for (int k = 1; k < 4; k++) f[k] = -f[0] / T * U[k] * mus[k - 1];
             }
           }
-          // QCQP at lambda = 0: inverse of the friction block scaled by the cone coefficients
-          float As[3][3], Ai[3][3];
+          // QCQP data: eigen-decomposition of the cone-scaled friction block (constant over the sweeps)
+          float As[3][3], Qe[3][3], lam[3];
 #pragma unroll
           for (int a = 0; a < 3; a++)
 #pragma unroll
             for (int b2 = 0; b2 < 3; b2++) As[a][b2] = ARb[1 + a][1 + b2] * mus[a] * mus[b2];
-          inv3(Ai, As);
+          eig3_sym(As, lam, Qe);
           ConSolve& cs = sh.con[c].s;
+          cs.ar[0] = ARb[0][0]; cs.ar[1] = ARb[0][1]; cs.ar[2] = ARb[0][2]; cs.ar[3] = ARb[0][3];
+          cs.ar[4] = ARb[1][1]; cs.ar[5] = ARb[1][2]; cs.ar[6] = ARb[1][3];
+          cs.ar[7] = ARb[2][2]; cs.ar[8] = ARb[2][3]; cs.ar[9] = ARb[3][3];
 #pragma unroll
-          for (int k = 0; k < 16; k++) cs.AR[k] = ARb[k >> 2][k & 3];
-#pragma unroll
-          for (int k = 0; k < 9; k++) cs.Ainv[k] = Ai[k / 3][k % 3];
-          cs.dd[0] = mus[0]; cs.dd[1] = mus[1]; cs.dd[2] = mus[2];
+          for (int k = 0; k < 9; k++) cs.q[k] = Qe[k / 3][k % 3];
+          cs.lam[0] = lam[0]; cs.lam[1] = lam[1]; cs.lam[2] = lam[2];
+          cs.mu0 = mu0; cs.mu1 = mu1;
           cs.aref = make_float4(aref[0], aref[1], aref[2], aref[3]);
-          cs.R = make_float4(R[0], R[1], R[2], R[3]);
+          cs.R0 = R[0]; cs.R1 = R[1]; cs.R3 = R[3];
           cs.f = make_float4(f[0], f[1], f[2], f[3]);
           cs.arinv0 = 1.f / ARb[0][0];
           if (lane == 0) {
@@ -1290,25 +1350,26 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     if (lane >= SO100_NV) qacc_c = 0.f;
     __syncthreads();
 
+    STAMP(2);
     // ---------------- S8: projected Gauss-Seidel (MuJoCo mj_solPGS order: friction | limits | contacts)
     bool done = !valid;
     int iters = 0;
     float last_impr = 0.f;
     for (int it = 0; it < m->iterations; it++) {
       if (__ballot(!done) == 0ull) break;
+      // keep the per-contact LDS loads inside the sweep (no LICM of 16 contacts' blocks into VGPRs)
+      asm volatile("" ::: "memory");
       float impr = 0.f;
       // arm frictionloss rows: sequential, coupled through M^-1 (row broadcast by DPP)
 #pragma unroll
       for (int j = 0; j < 6; j++) {
-        float delta = 0.f;
-        if (lane == j && !done) {
-          const float res = qacc_c - fr_aref + fr_R * fr_f;
-          const float old = fr_f;
-          const float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
-          delta = fn - old;
-          fr_f = fn;
-          impr -= delta * (res + 0.5f * fr_AR * delta);
-        }
+        // every lane evaluates the row update on its own dof, only lane j keeps it (no exec branching)
+        const bool mine = (lane == j) && !done;
+        const float res = qacc_c - fr_aref + fr_R * fr_f;
+        const float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
+        const float delta = mine ? fn - fr_f : 0.f;
+        fr_f += delta;
+        impr -= delta * (res + 0.5f * fr_AR * delta);
         qacc_c += minv_row[j] * bcast_row(delta, j);
       }
       // cube frictionloss rows: decoupled (diagonal M), all six in parallel
@@ -1339,60 +1400,65 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
           qacc_c += minv_row[j] * bcast_row(delta, j);
         }
       }
+      STAMP(3);
       // contact blocks (elliptic, condim 4): normal update, then friction QCQP on the cone
 #pragma unroll
       for (int c = 0; c < kMaxCon; c++) {
         if (c < ncon_max) {
-          // keep the per-contact LDS loads inside the sweep (no LICM of 16 contacts' blocks into VGPRs)
-          asm volatile("" ::: "memory");
-          const ConSolve& cs = sh.con[c].s;
+          // the whole 144-B block as 9 x ds_read_b128, issued before the row reductions so the LDS
+          // latency overlaps them (unconditional: inactive envs read their own unused slot)
+          const float4* cv = reinterpret_cast<const float4*>(&sh.con[c].s);
+          const float4 v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3], v4 = cv[4], v5 = cv[5];
+          const float4 v6 = cv[6], v7 = cv[7], v8 = cv[8];
           const float j0 = rowsum16(Jr[c].x * qacc_c), j1 = rowsum16(Jr[c].y * qacc_c);
           const float j2 = rowsum16(Jr[c].z * qacc_c), j3 = rowsum16(Jr[c].w * qacc_c);
+          // unpack (layout of ConSolve)
+          const float a00 = v0.x, a01 = v0.y, a02 = v0.z, a03 = v0.w, a11 = v1.x, a12 = v1.y, a13 = v1.z;
+          const float a22 = v1.w, a23 = v2.x, a33 = v2.y;
+          const float Qe[9] = {v2.z, v2.w, v3.x, v3.y, v3.z, v3.w, v4.x, v4.y, v4.z};
+          const float lam[3] = {v4.w, v5.x, v5.y};
+          const float R0 = v5.z, arinv0 = v5.w, mu0 = v8.x, mu1 = v8.y, R1 = v8.z, R3 = v8.w;
+          const float4 ar = v6, f4 = v7;
           float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
           if (c < ncon && !done) {
-            const float4 ar = cs.aref, R4 = cs.R, f4 = cs.f;
-            const float res[4] = {j0 - ar.x + R4.x * f4.x, j1 - ar.y + R4.y * f4.y, j2 - ar.z + R4.z * f4.z,
-                                  j3 - ar.w + R4.w * f4.w};
+            const float res[4] = {j0 - ar.x + R0 * f4.x, j1 - ar.y + R1 * f4.y, j2 - ar.z + R1 * f4.z,
+                                  j3 - ar.w + R3 * f4.w};
             const float old[4] = {f4.x, f4.y, f4.z, f4.w};
             float f[4];
-            f[0] = old[0] - res[0] * cs.arinv0;
+            f[0] = old[0] - res[0] * arinv0;
             if (f[0] < kMinVal) {
               f[0] = f[1] = f[2] = f[3] = 0.f;
             } else {
-              float Af[3][3], bf[3];
-#pragma unroll
-              for (int a = 0; a < 3; a++) {
-                bf[a] = res[1 + a] + cs.AR[4 * (1 + a)] * (f[0] - old[0]);
-#pragma unroll
-                for (int b2 = 0; b2 < 3; b2++) {
-                  Af[a][b2] = cs.AR[4 * (1 + a) + 1 + b2];
-                  bf[a] -= Af[a][b2] * old[1 + b2];
-                }
-              }
+              const float dn = f[0] - old[0];
+              float bf[3];
+              bf[0] = res[1] + a01 * dn - (a11 * old[1] + a12 * old[2] + a13 * old[3]);
+              bf[1] = res[2] + a02 * dn - (a12 * old[1] + a22 * old[2] + a23 * old[3]);
+              bf[2] = res[3] + a03 * dn - (a13 * old[1] + a23 * old[2] + a33 * old[3]);
               float x[3];
-              qcqp3_warm(x, cs.Ainv, Af, bf, cs.dd, f[0]);
+              qcqp3_eig(x, Qe, lam, bf, mu0, mu1, f[0]);
               f[1] = x[0]; f[2] = x[1]; f[3] = x[2];
             }
             const float dl[4] = {f[0] - old[0], f[1] - old[1], f[2] - old[2], f[3] - old[3]};
             if (lane == 0) {
-#pragma unroll
-              for (int r = 0; r < 4; r++) {
-                const float q = cs.AR[4 * r] * dl[0] + cs.AR[4 * r + 1] * dl[1] + cs.AR[4 * r + 2] * dl[2] +
-                                cs.AR[4 * r + 3] * dl[3];
-                impr -= dl[r] * (res[r] + 0.5f * q);
-              }
+              const float q0 = a00 * dl[0] + a01 * dl[1] + a02 * dl[2] + a03 * dl[3];
+              const float q1 = a01 * dl[0] + a11 * dl[1] + a12 * dl[2] + a13 * dl[3];
+              const float q2 = a02 * dl[0] + a12 * dl[1] + a22 * dl[2] + a23 * dl[3];
+              const float q3 = a03 * dl[0] + a13 * dl[1] + a23 * dl[2] + a33 * dl[3];
+              impr -= dl[0] * (res[0] + 0.5f * q0) + dl[1] * (res[1] + 0.5f * q1) + dl[2] * (res[2] + 0.5f * q2) +
+                      dl[3] * (res[3] + 0.5f * q3);
             }
-            sh.con[c].s.f = make_float4(f[0], f[1], f[2], f[3]);
+            reinterpret_cast<float4*>(&sh.con[c].s)[7] = make_float4(f[0], f[1], f[2], f[3]);
             d4 = make_float4(dl[0], dl[1], dl[2], dl[3]);
           }
           // qacc += M^-1 J' d: g = J_dof . d per lane, then the arm's M^-1 row via row broadcasts
-          const float g = Jr[c].x * d4.x + Jr[c].y * d4.y + Jr[c].z * d4.z + Jr[c].w * d4.w;
-          float upd = invmc * g;
-#pragma unroll
-          for (int j = 0; j < 6; j++) upd += minv_row[j] * bcast_row(g, j);
-          qacc_c += upd;
+          const float g = (Jr[c].x * d4.x + Jr[c].y * d4.y) + (Jr[c].z * d4.z + Jr[c].w * d4.w);
+          const float u01 = minv_row[0] * bcast_row(g, 0) + minv_row[1] * bcast_row(g, 1);
+          const float u23 = minv_row[2] * bcast_row(g, 2) + minv_row[3] * bcast_row(g, 3);
+          const float u45 = minv_row[4] * bcast_row(g, 4) + minv_row[5] * bcast_row(g, 5);
+          qacc_c += (invmc * g + u01) + (u23 + u45);
         }
       }
+      STAMP(4);
       const float improvement = rowsum16(impr) * m->pgs_scale;
       if (!done) {
         iters = it + 1;
@@ -1400,6 +1466,7 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
         if (improvement < m->tolerance) done = true;
       }
     }
+    STAMP(3);
     dbg_iter = (float)iters;
     dbg_impr = last_impr;
     dbg_nefc = 12 + __popcll(lim_mask & (0xFFFFull << (grp * 16))) + 4 * ncon;
@@ -1440,6 +1507,7 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     __syncthreads();
   }
 
+  STAMP(5);
   // ---------------- final position stage (mj_step1): sites + contact set for reward / obs
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
@@ -1540,6 +1608,14 @@ __global__ void __launch_bounds__(kThreads) so100_step_kernel(StepArgs args) {
     }
   }
 
+  STAMP(6);
+#ifdef SO100_STAMPS
+  if (B.debug && valid && lane == 0) {
+    float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
+#pragma unroll
+    for (int k = 0; k < 7; k++) dbg[88 + k] = (float)st_acc_[k];
+  }
+#endif
   // ---------------- store state
   if (valid) {
     if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libso100_hip.so")
+LIB_PATH = os.environ.get("SO100_LIB") or os.path.join(HERE, "_lib", "libso100_hip.so")
 
 SO100_FLAG_AUTORESET = 1
 SO100_FLAG_DR = 2
