@@ -104,6 +104,8 @@ struct __attribute__((aligned(16))) EnvShared {
     ConSlot con[kMaxCon];        // geometry (collision -> Jacobian), then solver data (setup -> PGS)
     SerialScratch ser;           // serial stage scratch (dead before collision writes contacts)
   };
+  // stride = 13.25 x 256 B: the 4 envs of a wave hit different LDS bank windows for the same field
+  float bank_pad[16];
 };
 
 // ------------------------------------------------------------------ small math (same formulas as oracle)
@@ -569,76 +571,100 @@ struct PairContacts {
   float dist[SO100_MAXCONPAIR];
 };
 
-DEV int clip_rect_quad(const float h0, const float h1, const float* quad, float* out) {
-  float bufa[16], bufb[16];
-  float* q = bufa;
-  float* r = bufb;
-  int nq = 4, nr = 0;
-  for (int i = 0; i < 8; i++) q[i] = quad[i];
-  const float h[2] = {h0, h1};
-  for (int dir = 0; dir < 2; dir++) {
-    for (int sign = -1; sign <= 1; sign += 2) {
-      nr = 0;
-      for (int i = 0; i < nq && nr < 8; i++) {
-        const float* a = q + 2 * i;
-        const float* b = q + 2 * ((i + 1) % nq);
-        bool ina = (float)sign * a[dir] < h[dir];
-        bool inb = (float)sign * b[dir] < h[dir];
-        if (ina) { r[2 * nr] = a[0]; r[2 * nr + 1] = a[1]; nr++; }
-        if (ina != inb && nr < 8) {
-          float lim = (float)sign * h[dir];
-          r[2 * nr + 1 - dir] = a[1 - dir] + (b[1 - dir] - a[1 - dir]) / (b[dir] - a[dir]) * (lim - a[dir]);
-          r[2 * nr + dir] = lim;
-          nr++;
-        }
+// Register-resident polygons: fixed 8 slots written by select chains (static indices only), so the
+// clipping never touches scratch memory.  Same Sutherland-Hodgman order and 8-vertex cap as the oracle.
+struct Poly8 {
+  float x[8], y[8];
+  int n;
+};
+DEV void poly_push(Poly8& p, float x, float y) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const bool w = (k == p.n);
+    p.x[k] = w ? x : p.x[k];
+    p.y[k] = w ? y : p.y[k];
+  }
+  p.n = p.n + 1;
+}
+// clip polygon q by the half-plane sign * coord[dir] < h (rectangle side), result in r
+DEV void clip_stage(const Poly8& q, Poly8& r, int dir, float sign, float h) {
+  r.n = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (i < q.n && r.n < 8) {
+      const float ax = q.x[i], ay = q.y[i];
+      const bool last = (i + 1 >= q.n);
+      const float bx = last ? q.x[0] : q.x[(i + 1) & 7], by = last ? q.y[0] : q.y[(i + 1) & 7];
+      const float ad = dir ? ay : ax, bd = dir ? by : bx;
+      const bool ina = sign * ad < h, inb = sign * bd < h;
+      if (ina) poly_push(r, ax, ay);
+      if (ina != inb && r.n < 8) {
+        const float lim = sign * h;
+        const float ao = dir ? ax : ay, bo = dir ? bx : by;
+        const float o = ao + (bo - ao) / (bd - ad) * (lim - ad);
+        if (dir) poly_push(r, o, lim); else poly_push(r, lim, o);
       }
-      float* t = q; q = r; r = t;
-      nq = nr;
     }
   }
-  for (int i = 0; i < 2 * nq; i++) out[i] = q[i];
-  return nq;
 }
 
-DEV void cull_points(int n, const float* p, int mm, int i0, int* iret) {
+// deepest point first, then the points closest in angle to the spread targets (ODE cullPoints order)
+DEV void cull_points8(const Poly8& p, int mm, int i0, int* iret) {
+  const int n = p.n;
   float cx, cy;
-  if (n == 1) { cx = p[0]; cy = p[1]; }
-  else if (n == 2) { cx = 0.5f * (p[0] + p[2]); cy = 0.5f * (p[1] + p[3]); }
+  if (n == 1) { cx = p.x[0]; cy = p.y[0]; }
+  else if (n == 2) { cx = 0.5f * (p.x[0] + p.x[1]); cy = 0.5f * (p.y[0] + p.y[1]); }
   else {
-    float a = 0.f, qq;
+    float a = 0.f;
     cx = 0.f; cy = 0.f;
-    for (int i = 0; i < n; i++) {
-      int j = (i + 1) % n;
-      qq = p[2 * i] * p[2 * j + 1] - p[2 * j] * p[2 * i + 1];
-      a += qq;
-      cx += qq * (p[2 * i] + p[2 * j]);
-      cy += qq * (p[2 * i + 1] + p[2 * j + 1]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (i < n) {
+        const bool last = (i + 1 >= n);
+        const float xj = last ? p.x[0] : p.x[(i + 1) & 7], yj = last ? p.y[0] : p.y[(i + 1) & 7];
+        const float qq = p.x[i] * yj - xj * p.y[i];
+        a += qq;
+        cx += qq * (p.x[i] + xj);
+        cy += qq * (p.y[i] + yj);
+      }
     }
     if (fabsf(a) > 1e-12f) { a = 1.0f / (3.0f * a); cx *= a; cy *= a; }
     else {
       cx = 0.f; cy = 0.f;
-      for (int i = 0; i < n; i++) { cx += p[2 * i]; cy += p[2 * i + 1]; }
+#pragma unroll
+      for (int i = 0; i < 8; i++) if (i < n) { cx += p.x[i]; cy += p.y[i]; }
       cx /= (float)n; cy /= (float)n;
     }
   }
   float A[8];
-  bool avail[8];
-  for (int i = 0; i < n; i++) { A[i] = atan2f(p[2 * i + 1] - cy, p[2 * i] - cx); avail[i] = true; }
-  avail[i0] = false;
+  uint32_t avail = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    A[i] = (i < n) ? atan2f(p.y[i] - cy, p.x[i] - cx) : 0.f;
+    if (i < n) avail |= 1u << i;
+  }
+  avail &= ~(1u << i0);
   iret[0] = i0;
+  float Ai0 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; i++) Ai0 = (i == i0) ? A[i] : Ai0;
   const float PI = 3.14159265358979323846f;
-  for (int j = 1; j < mm; j++) {
-    float a = (float)j * (2.f * PI / (float)mm) + A[i0];
+#pragma unroll
+  for (int j = 1; j < SO100_MAXCONPAIR; j++) {
+    float a = (float)j * (2.f * PI / (float)mm) + Ai0;
     if (a > PI) a -= 2.f * PI;
     float best = 1e9f;
-    iret[j] = i0;
-    for (int i = 0; i < n; i++) {
-      if (!avail[i]) continue;
-      float df = fabsf(A[i] - a);
-      if (df > PI) df = 2.f * PI - df;
-      if (df < best) { best = df; iret[j] = i; }
+    int pick = i0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if ((avail >> i) & 1u) {
+        float df = fabsf(A[i] - a);
+        if (df > PI) df = 2.f * PI - df;
+        if (df < best) { best = df; pick = i; }
+      }
     }
-    avail[iret[j]] = false;
+    iret[j] = pick;
+    avail &= ~(1u << pick);
   }
 }
 
@@ -754,45 +780,75 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   float cc1 = dot3(center, u1), cc2 = dot3(center, u2);
   float m11 = dot3(u1, v1), m12 = dot3(u1, v2), m21 = dot3(u2, v1), m22 = dot3(u2, v2);
   float k1 = m11 * SI[a1], k2 = m21 * SI[a1], k3 = m12 * SI[a2], k4 = m22 * SI[a2];
-  float quad[8] = {cc1 - k1 - k3, cc2 - k2 - k4, cc1 - k1 + k3, cc2 - k2 + k4,
-                   cc1 + k1 + k3, cc2 + k2 + k4, cc1 + k1 - k3, cc2 + k2 - k4};
-  float pts[16];
-  int n = clip_rect_quad(SR[c1], SR[c2], quad, pts);
+  Poly8 P, Pq;
+  P.n = 4;
+  P.x[0] = cc1 - k1 - k3; P.y[0] = cc2 - k2 - k4;
+  P.x[1] = cc1 - k1 + k3; P.y[1] = cc2 - k2 + k4;
+  P.x[2] = cc1 + k1 + k3; P.y[2] = cc2 + k2 + k4;
+  P.x[3] = cc1 + k1 - k3; P.y[3] = cc2 + k2 - k4;
+#pragma unroll
+  for (int k = 4; k < 8; k++) { P.x[k] = 0.f; P.y[k] = 0.f; }
+  clip_stage(P, Pq, 0, -1.f, SR[c1]);
+  clip_stage(Pq, P, 0, 1.f, SR[c1]);
+  clip_stage(P, Pq, 1, -1.f, SR[c2]);
+  clip_stage(Pq, P, 1, 1.f, SR[c2]);
+  const int n = P.n;
   if (n < 1) return;
   float det = m11 * m22 - m12 * m21;
   if (fabsf(det) < 1e-12f) return;
   det = 1.f / det;
-  float i11 = m22 * det, i12 = -m12 * det, i21 = -m21 * det, i22 = m11 * det;
-  float P3[8][3], dep[8], P2[16];
-  int cnum = 0;
-  for (int k = 0; k < n; k++) {
-    float x = pts[2 * k] - cc1, y = pts[2 * k + 1] - cc2;
-    float s1 = i11 * x + i12 * y, s2 = i21 * x + i22 * y;
-    float pt[3];
-    for (int t = 0; t < 3; t++) pt[t] = center[t] + s1 * v1[t] + s2 * v2[t];
-    float dp = SR[codeN] - dot3(nref, pt);
-    if (dp > -margin) {
-      for (int t = 0; t < 3; t++) P3[cnum][t] = pt[t] + pR[t];
-      dep[cnum] = dp;
-      P2[2 * cnum] = pts[2 * k];
-      P2[2 * cnum + 1] = pts[2 * k + 1];
-      cnum++;
+  const float i11 = m22 * det, i12 = -m12 * det, i21 = -m21 * det, i22 = m11 * det;
+  // keep the penetrating points (compacted in order; 2D coords in K, depth in D)
+  Poly8 K;
+  K.n = 0;
+  float D[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { K.x[k] = 0.f; K.y[k] = 0.f; D[k] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k < n) {
+      const float x = P.x[k] - cc1, y = P.y[k] - cc2;
+      const float s1 = i11 * x + i12 * y, s2 = i21 * x + i22 * y;
+      float pt[3];
+      for (int t = 0; t < 3; t++) pt[t] = center[t] + s1 * v1[t] + s2 * v2[t];
+      const float dp = SR[codeN] - dot3(nref, pt);
+      if (dp > -margin) {
+#pragma unroll
+        for (int q2 = 0; q2 < 8; q2++) D[q2] = (q2 == K.n) ? dp : D[q2];
+        poly_push(K, P.x[k], P.y[k]);
+      }
     }
   }
+  const int cnum = K.n;
   if (cnum < 1) return;
-  int idx[8], nout = cnum;
+  int idx[SO100_MAXCONPAIR] = {0, 1, 2, 3};
+  int nout = cnum;
   if (cnum > SO100_MAXCONPAIR) {
     int i0 = 0;
-    for (int k = 1; k < cnum; k++) if (dep[k] > dep[i0]) i0 = k;
-    cull_points(cnum, P2, SO100_MAXCONPAIR, i0, idx);
+    float dmax = D[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) if (k < cnum && D[k] > dmax) { dmax = D[k]; i0 = k; }
+    cull_points8(K, SO100_MAXCONPAIR, i0, idx);
     nout = SO100_MAXCONPAIR;
-  } else {
-    for (int k = 0; k < cnum; k++) idx[k] = k;
   }
-  for (int c = 0; c < nout; c++) {
-    int k = idx[c];
-    for (int t = 0; t < 3; t++) out.pos[c][t] = P3[k][t] + 0.5f * dep[k] * nref[t];
-    out.dist[c] = -dep[k];
+#pragma unroll
+  for (int c = 0; c < SO100_MAXCONPAIR; c++) {
+    if (c < nout) {
+      float x = 0.f, y = 0.f, dp = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const bool w = (k == idx[c]);
+        x = w ? K.x[k] : x; y = w ? K.y[k] : y; dp = w ? D[k] : dp;
+      }
+      const float xr = x - cc1, yr = y - cc2;
+      const float s1 = i11 * xr + i12 * yr, s2 = i21 * xr + i22 * yr;
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        const float pt = center[t] + s1 * v1[t] + s2 * v2[t];
+        out.pos[c][t] = pt + pR[t] + 0.5f * dp * nref[t];
+      }
+      out.dist[c] = -dp;
+    }
   }
   out.n = nout;
 }
