@@ -14,7 +14,10 @@
 #include "so100_device.h"
 
 namespace so100 {
-hipError_t launch_step(const DevModel*, const so100_buffers&, int, int, int, int, uint64_t, int, hipStream_t);
+hipError_t launch_step(const DevModel*, int, const Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
+                       hipStream_t);
+hipError_t alloc_workspace(int, Workspace*);
+hipError_t free_workspace(Workspace*);
 hipError_t launch_reset(const DevModel*, const so100_buffers&, int, int, uint64_t, int, const uint8_t*, const uint32_t*,
                         hipStream_t);
 hipError_t launch_reward(const DevModel*, int, int, const float*, const float*, const uint32_t*, float*, hipStream_t);
@@ -24,11 +27,14 @@ hipError_t launch_goal_reward(const DevModel*, int, const float*, const float*, 
 }  // namespace so100
 
 using so100::DevModel;
+using so100::Workspace;
 
 struct so100_env {
   int device;
   int n;
   DevModel* d_model;
+  int nsubstep;
+  Workspace ws;                 // substep hand-off record between the stage and solver kernels
   int task;
   int max_steps;
   uint64_t base_seed;
@@ -238,7 +244,10 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (e != hipSuccess) { fail_hip("so100_create: hipMalloc", e); return nullptr; }
   e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
-  so100_env* env = new so100_env{device, n_envs, dm, SO100_TASK_CUBE_TO_BIN, 700, 0, 0};
+  Workspace ws;
+  e = so100::alloc_workspace(n_envs, &ws);
+  if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: workspace hipMalloc", e); return nullptr; }
+  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, ws, SO100_TASK_CUBE_TO_BIN, 700, 0, 0};
   return env;
 }
 
@@ -246,6 +255,8 @@ int so100_destroy(so100_env* env) {
   if (!env) return 0;
   DeviceGuard g(env->device);
   hipError_t e = hipFree(env->d_model);
+  hipError_t e2 = so100::free_workspace(&env->ws);
+  if (e == hipSuccess) e = e2;
   delete env;
   return e == hipSuccess ? 0 : fail_hip("so100_destroy", e);
 }
@@ -287,7 +298,7 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
   if ((flags & SO100_FLAG_DR) && !b->dr_params) return fail("so100_step: FLAG_DR needs dr_params");
   if ((flags & SO100_FLAG_AUTORESET) && !b->episode) return fail("so100_step: FLAG_AUTORESET needs episode");
   DeviceGuard g(env->device);
-  hipError_t e = so100::launch_step(env->d_model, *b, env->n, env->task, flags, env->max_steps, env->base_seed, env->env_offset,
+  hipError_t e = so100::launch_step(env->d_model, env->nsubstep, env->ws, *b, env->n, env->task, flags, env->max_steps, env->base_seed, env->env_offset,
                                     (hipStream_t)stream);
   return e == hipSuccess ? 0 : fail_hip("so100_step", e);
 }

@@ -1,0 +1,125 @@
+// so100_common.h — device-side pieces shared by the stage and solver kernels (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "so100_device.h"
+
+namespace so100 {
+#define DEV __device__ __forceinline__
+
+// Diagnostic build only (-DSO100_STAMPS): per-wave cycle attribution by phase (s_memtime), written to
+// the debug buffer's tail.  The product build compiles these to nothing.
+#ifdef SO100_STAMPS
+#define STAMP_DECL unsigned long long st_prev_ = 0, st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(slot)                                                                              \
+  do {                                                                                           \
+    unsigned long long t_;                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if ((slot) >= 0) st_acc_[(slot)] += t_ - st_prev_;                                           \
+    st_prev_ = t_;                                                                               \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(slot) do {} while (0)
+#endif
+constexpr float kMinVal = 1e-15f;
+constexpr float kMinImp = 0.0001f;
+constexpr float kMaxImp = 0.9999f;
+
+// ------------------------------------------------------------------ LDS layout (per env)
+struct __attribute__((aligned(16))) ConSolve {   // per-contact PGS data (144 B = 9 x ds_read_b128;
+                                                 // the PGS reads it as float4[9], keep the order)
+  // symmetric 4x4 block of A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
+  float ar[10];
+  // eigen-decomposition of the cone-scaled friction block As = D A11 D (D = diag(mu0, mu0, mu1)):
+  // As = Q diag(lam) Q', Q row-major (columns = eigenvectors) — QCQP Newton without 3x3 inverses
+  float q[9];
+  float lam[3];
+  float R0, arinv0;    // normal-row regulariser, 1 / AR00
+  float4 aref;
+  float4 f;            // current forces (normal, t1, t2, torsion)
+  float mu0, mu1;      // cone coefficients (mu0, mu0, mu1)
+  float R1, R3;        // friction-row regularisers (R2 = R1)
+};
+static_assert(sizeof(ConSolve) == 144 && offsetof(ConSolve, aref) == 96 && offsetof(ConSolve, f) == 112 &&
+                  offsetof(ConSolve, mu0) == 128, "ConSolve layout is read as float4[9] in the PGS");
+// ------------------------------------------------------------------ cross-lane (16-lane row) primitives
+template <int CTRL>
+DEV float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// sum over the 16 lanes of this DPP row; result in every lane of the row
+DEV float rowsum16(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return v;
+}
+DEV float bcast16(float v, int src) { return __shfl(v, src, kLanes); }
+DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
+
+// MuJoCo mju_QCQP3 restated (engine_util_solve.c): min 0.5 x'Ax + x'b s.t. sum (x_i/d_i)^2 <= r^2.
+// The minimiser is y(la) = -(As + la I)^-1 D b for the multiplier la >= 0 that puts y on the sphere
+// |y| = r (As = D A D, D = diag(mu0, mu0, mu1)).  In the eigenbasis of As (precomputed per substep)
+// y_i(la) = c_i / (lam_i + la) with c = -Q' D b, so an iterate costs three reciprocals.
+// Root finding: MuJoCo runs Newton on |y|^2 - r^2 from la = 0, which on this 1/la^2-shaped function
+// advances la by at most x1.5 per step while far from the root (3.5-7 steps per contact-sweep on
+// sliding grasp contacts).  We solve the same equation with Newton on 1/|y(la)| - 1/r (the trust-region
+// secular equation: near-linear and concave in la, exact for one active term), started from the lower
+// bound la0 = max(0, |c|/r - max lam) <= la*: from the left it converges monotonically to the same root,
+// with MuJoCo's exit tests (val < 1e-10, delta < 1e-10) plus an fp32 step test.  1-2 steps typical.
+// Returns the number of Newton steps taken (diagnostics).
+DEV int qcqp3_eig(float* x, const float* Q, const float* lam, const float* b0, float mu0, float mu1, float r,
+                  bool live = true) {
+  int nit = 0;
+  const float dd[3] = {mu0, mu0, mu1};
+  float bs[3], c[3], w[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) bs[i] = b0[i] * dd[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) c[i] = -(Q[i] * bs[0] + Q[3 + i] * bs[1] + Q[6 + i] * bs[2]);   // -Q' b
+#pragma unroll
+  for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i]); w[i] = c[i] * d[i]; }
+  float s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (live && s - r * r >= 1e-10f) {
+    const float rinv = __builtin_amdgcn_rcpf(r);
+    const float cn = sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    float la = fmaxf(0.f, cn * rinv - fmaxf(lam[0], fmaxf(lam[1], lam[2])));
+#pragma unroll
+    for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
+    s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    for (int it = 0; it < 20; it++) {
+      if (s - r * r < 1e-10f) break;
+      nit++;
+      // d|y|^2/dla = -2 sum w_i^2 d_i;  Newton on g = 1/|y|: delta = (1/r - g) / g' = s (|y|/r - 1) / t
+      const float t = w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2];
+      const float delta = s * (sqrtf(s) * rinv - 1.f) * __builtin_amdgcn_rcpf(t);
+      if (delta < 1e-10f || delta <= 4e-7f * la) break;
+      la += delta;
+#pragma unroll
+      for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
+      s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    }
+  }
+  // y = Q w, x = D y
+#pragma unroll
+  for (int i = 0; i < 3; i++) x[i] = (Q[3 * i] * w[0] + Q[3 * i + 1] * w[1] + Q[3 * i + 2] * w[2]) * dd[i];
+  return nit;
+}
+
+// ------------------------------------------------------------------ 4-lane (quad) primitives
+DEV float quad_swap1(float v) { return dpp<0xB1>(v); }   // quad_perm [1,0,3,2]
+DEV float quad_swap2(float v) { return dpp<0x4E>(v); }   // quad_perm [2,3,0,1]
+// sum over the 4 lanes of a quad; every lane gets the bitwise-same value (fp add is commutative)
+DEV float quadsum(float v) {
+  v += quad_swap1(v);
+  v += quad_swap2(v);
+  return v;
+}
+template <int L>
+DEV float quad_bcast(float v) { return dpp<L | (L << 2) | (L << 4) | (L << 6)>(v); }
+
+}  // namespace so100

@@ -83,4 +83,31 @@ struct DevModel {
   float goal_bin_lo[3], goal_bin_hi[3];   // env.py:245-249
 };
 
+// ------------------------------------------------------------------ substep workspace (HBM)
+// The substep is split in two kernels: the stage kernel (16 lanes per env) assembles
+// the constraint rows, the PGS kernel (4 lanes per env, 3 dofs per lane) solves them.  The hand-off
+// is a per-env record in HBM, laid out for the solver's lanes:
+//   hdr[env][q][kHdrLane]  lane q owns dofs 3q..3q+2 (q = 0,1: arm, q = 2,3: cube)
+//   con[env][c][kConRec]   ConSolve (36 floats) then J[dof][row] (12 x 4 floats)
+constexpr int kHdrLane = 40;
+constexpr int kHdrEnv = 4 * kHdrLane;
+constexpr int kConRec = 36 + 48;
+enum HdrField : int {
+  H_QACC = 0,       // qacc at the solver start (qacc_smooth, plus M^-1 J' f of the kept warmstart)
+  H_FRAREF = 3,     // frictionloss rows: aref = -B vel
+  H_FRF = 6,        //   warmstart force
+  H_LIMS = 9,       // joint-limit rows (arm lanes): side +-1, 0 = inactive
+  H_LIMAREF = 12,
+  H_LIMR = 15,
+  H_LIMF = 18,
+  H_MROW = 21,      // 3 x 6: M^-1 rows of this lane's dofs, own 3 columns then the partner lane's 3
+                    // (cube lanes: the diagonal inverse mass, partner columns 0)
+  H_NCON = 39,      // contact count (int bits)
+};
+static_assert(H_NCON + 1 == kHdrLane && kHdrLane % 4 == 0 && kConRec % 4 == 0, "workspace record layout");
+struct Workspace {
+  float* hdr;
+  float* con;
+};
+
 }  // namespace so100

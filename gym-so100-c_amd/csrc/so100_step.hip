@@ -18,49 +18,10 @@
 #include <stdint.h>
 #include "so100_device.h"
 #include "so100.h"
+#include "so100_common.h"
 
 namespace so100 {
 
-#define DEV __device__ __forceinline__
-
-// Diagnostic build only (-DSO100_STAMPS): per-wave cycle attribution by phase (s_memtime), written to
-// the debug buffer's tail.  The product build compiles these to nothing.
-#ifdef SO100_STAMPS
-#define STAMP_DECL unsigned long long st_prev_ = 0, st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define STAMP(slot)                                                                              \
-  do {                                                                                           \
-    unsigned long long t_;                                                                       \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    if ((slot) >= 0) st_acc_[(slot)] += t_ - st_prev_;                                           \
-    st_prev_ = t_;                                                                               \
-  } while (0)
-#else
-#define STAMP_DECL
-#define STAMP(slot) do {} while (0)
-#endif
-constexpr float kMinVal = 1e-15f;
-constexpr float kMinImp = 0.0001f;
-constexpr float kMaxImp = 0.9999f;
-
-// ------------------------------------------------------------------ LDS layout (per env)
-struct __attribute__((aligned(16))) ConSolve {   // per-contact PGS data (144 B = 9 x ds_read_b128;
-                                                 // the PGS reads it as float4[9], keep the order)
-  // symmetric 4x4 block of A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
-  float ar[10];
-  // eigen-decomposition of the cone-scaled friction block As = D A11 D (D = diag(mu0, mu0, mu1)):
-  // As = Q diag(lam) Q', Q row-major (columns = eigenvectors) — QCQP Newton without 3x3 inverses
-  float q[9];
-  float lam[3];
-  float R0, arinv0;    // normal-row regulariser, 1 / AR00
-  float4 aref;
-  float4 f;            // current forces (normal, t1, t2, torsion)
-  float mu0, mu1;      // cone coefficients (mu0, mu0, mu1)
-  float R1, R3;        // friction-row regularisers (R2 = R1)
-};
-static_assert(sizeof(ConSolve) == 144 && offsetof(ConSolve, aref) == 96 && offsetof(ConSolve, f) == 112 &&
-                  offsetof(ConSolve, mu0) == 128, "ConSolve layout is read as float4[9] in the PGS");
 struct __attribute__((aligned(16))) ConGeom {    // per-contact geometry (collision output)
   float pos[4];
   float frame[12];     // normal (geom1 -> geom2), tangent1, tangent2
@@ -175,22 +136,6 @@ DEV void mul_inert(float* r, const float* in, const float* v) {
 #pragma unroll
   for (int k = 0; k < 3; k++) { r[k] = Iw[k] + mdv[k]; r[3 + k] = in[12] * v[3 + k] - mdw[k]; }
 }
-
-// ------------------------------------------------------------------ cross-lane (16-lane row) primitives
-template <int CTRL>
-DEV float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
-// sum over the 16 lanes of this DPP row; result in every lane of the row
-DEV float rowsum16(float v) {
-  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp<0x141>(v);  // row_half_mirror
-  v += dpp<0x140>(v);  // row_mirror
-  return v;
-}
-DEV float bcast16(float v, int src) { return __shfl(v, src, kLanes); }
-DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 
 // ------------------------------------------------------------------ impedance / reference (MuJoCo restated)
 DEV float getimpedance(const float* solimp, float pos, float margin) {
@@ -1087,49 +1032,18 @@ DEV void eig3_sym(const float A0[3][3], float lam[3], float Q[3][3]) {
   lam[0] = a[0][0]; lam[1] = a[1][1]; lam[2] = a[2][2];
 }
 
-// MuJoCo mju_QCQP3 restated: min 0.5 x'Ax + x'b s.t. sum (x_i/d_i)^2 <= r^2, Newton on the multiplier
-// la from la = 0.  In the eigenbasis of As = D A D (precomputed per substep) every iterate
-// y(la) = -(As + la I)^-1 D b is c_i / (lam_i + la) with c = -Q'Db, so an iteration is three
-// reciprocals instead of a 3x3 inverse; the iterates are MuJoCo's (same val/deriv/delta tests).
-DEV void qcqp3_eig(float* x, const float* Q, const float* lam, const float* b0, float mu0, float mu1, float r) {
-  const float dd[3] = {mu0, mu0, mu1};
-  float bs[3], c[3], w[3], d[3];
-#pragma unroll
-  for (int i = 0; i < 3; i++) bs[i] = b0[i] * dd[i];
-#pragma unroll
-  for (int i = 0; i < 3; i++) c[i] = -(Q[i] * bs[0] + Q[3 + i] * bs[1] + Q[6 + i] * bs[2]);   // -Q' b
-#pragma unroll
-  for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i]); w[i] = c[i] * d[i]; }
-  float val = w[0] * w[0] + w[1] * w[1] + w[2] * w[2] - r * r;
-  if (val >= 1e-10f) {
-    float la = 0.f;
-    for (int it = 0; it < 20; it++) {
-      // deriv = -2 y'(As + la I)^-1 y = -2 sum w_i^2 d_i
-      const float deriv = -2.f * (w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2]);
-      const float delta = -val * __builtin_amdgcn_rcpf(deriv);
-      if (delta < 1e-10f) break;
-      la += delta;
-#pragma unroll
-      for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
-      val = w[0] * w[0] + w[1] * w[1] + w[2] * w[2] - r * r;
-      if (val < 1e-10f) break;
-    }
-  }
-  // y = Q w, x = D y
-#pragma unroll
-  for (int i = 0; i < 3; i++) x[i] = (Q[3 * i] * w[0] + Q[3 * i + 1] * w[1] + Q[3 * i + 2] * w[2]) * dd[i];
-}
-
 // ------------------------------------------------------------------ the step kernel
-struct StepArgs {
+struct StageArgs {
   const DevModel* m;
   so100_buffers b;
+  Workspace w;
   int n;
   int task;
   int flags;
   int max_steps;
   uint64_t base_seed;
   int env_offset;
+  int sub;             // substep index (kMode 2: nsubstep)
 };
 
 DEV int wave_max_i(int v) {
@@ -1167,7 +1081,37 @@ DEV void write_obs(const DevModel* __restrict__ m, const EnvShared& sh, int lane
   if (lane < SO100_NOBS) dst[lane] = v;
 }
 
-__global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) {
+// Euler (mj_Euler) of the previous substep on the state held in registers: qvel += h qacc, then qpos
+// with the new qvel; the cube quaternion by the exponential map (lanes 9..12, staged through LDS).
+DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_r, float& qvel_r) {
+  if (lane < SO100_NV) qvel_r += h * qacc;
+  if (lane < 9) qpos_r += h * qvel_r;
+  if (lane >= 9 && lane < 12) sh.vec[lane] = qvel_r;
+  if (lane >= 9 && lane < 13) sh.qpos[lane] = qpos_r;
+  __syncthreads();
+  if (lane >= 9 && lane < 13) {
+    float q[4] = {sh.qpos[9], sh.qpos[10], sh.qpos[11], sh.qpos[12]};
+    float w[3] = {sh.vec[9], sh.vec[10], sh.vec[11]};
+    float nw = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    if (nw > kMinVal) {
+      float s, c;
+      sincosf(0.5f * h * nw, &s, &c);
+      float qr[4] = {c, w[0] / nw * s, w[1] / nw * s, w[2] / nw * s};
+      quat_mul(q, q, qr);
+    }
+    quat_normalize(q);
+    qpos_r = q[lane - 9];
+  }
+  __syncthreads();
+}
+
+// Substep stage kernel (one wave = 4 envs x 16 lanes).
+//   kMode 0: substep 0 — position/velocity stages and constraint assembly on the stored state;
+//   kMode 1: Euler with the previous substep's solver output, then the same assembly;
+//   kMode 2: Euler, then the mj_step1 position stage and the task epilogue (reward, obs, autoreset).
+// Assembly writes the solver's per-env record (Workspace) that so100_pgs_kernel consumes.
+template <int kMode>
+__global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args) {
   __shared__ EnvShared shm[kEnvsPerBlock];
   const DevModel* __restrict__ m = args.m;
   const int tid = threadIdx.x;
@@ -1179,7 +1123,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
   EnvShared& sh = shm[grp];
   const so100_buffers& B = args.b;
 
-  // ---------------- prologue: state + action -> registers
+  // ---------------- prologue: state -> registers
   float qpos_r = (lane < SO100_NQ) ? B.qpos[(size_t)e * SO100_NQ + lane] : 0.f;
   float qvel_r = (lane < SO100_NV) ? B.qvel[(size_t)e * SO100_NV + lane] : 0.f;
   float warm_r = (lane < SO100_NV) ? B.qacc_warmstart[(size_t)e * SO100_NV + lane] : 0.f;
@@ -1191,21 +1135,19 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
   }
   const int elapsed0 = B.elapsed ? B.elapsed[e] : 0;
   const uint32_t episode0 = B.episode ? B.episode[e] : 0u;
-  if (lane < 6) {
-    float a = B.action[(size_t)e * 6 + lane];
-    if (sigma > 0.f)
-      a += sigma * hash_normal(splitmix64(args.base_seed ^ ((uint64_t)(e + args.env_offset) << 40) ^ ((uint64_t)episode0 << 20) ^
-                                          (uint64_t)(elapsed0 * 8 + lane)));
-    sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
-  }
-
   const float h = m->timestep;
-  STAMP_DECL
-  STAMP(-1);
-  float dbg_iter = 0.f, dbg_impr = 0.f;
-  int dbg_nefc = 0;
 
-  for (int sub = 0; sub < m->nsubstep; sub++) {
+  if (kMode != 0) euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
+
+  if (kMode != 2) {
+    // control (the same every substep of the env step: elapsed/episode only change in the epilogue)
+    if (lane < 6) {
+      float a = B.action[(size_t)e * 6 + lane];
+      if (sigma > 0.f)
+        a += sigma * hash_normal(splitmix64(args.base_seed ^ ((uint64_t)(e + args.env_offset) << 40) ^
+                                            ((uint64_t)episode0 << 20) ^ (uint64_t)(elapsed0 * 8 + lane)));
+      sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
+    }
     // ---------------- S1: stage state in LDS
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
     if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
@@ -1213,7 +1155,6 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
     // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
     if (lane == 0) serial_stage(m, sh, true, mscale);
     __syncthreads();
-    STAMP(0);
     // ---------------- S3: collision, one pair per lane, compaction in pair order
     PairContacts pc;
     pc.n = 0;
@@ -1242,30 +1183,18 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
     __syncthreads();
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
+    float* const crec = args.w.con + (size_t)e * kMaxCon * kConRec;
 
-    STAMP(1);
-    // ---------------- S4/S5: contact Jacobian rows and M^-1 J' in registers (lane = dof, contacts unrolled)
+    // ---------------- S4/S5: M^-1 rows, frictionloss and joint-limit rows (lane = dof)
     float minv_row[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) minv_row[j] = (lane < 6) ? sh.minv[lane][j] : 0.f;
     const float invmc = (lane >= 6 && lane < 12) ? sh.inv_mcube[lane - 6] : 0.f;
-    float4 Jr[kMaxCon];
-#pragma unroll
-    for (int c = 0; c < kMaxCon; c++) {
-      Jr[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (c < ncon_max && c < ncon && lane < SO100_NV) Jr[c] = contact_jac(m, sh, c, lane);
-    }
     const float qs_r = (lane < SO100_NV) ? sh.qacc_smooth[lane] : 0.f;
-    // frictionloss row of dof `lane` (pos 0: aref = -B vel, R constant)
     const bool has_fr = lane < SO100_NV;
     const float fr_R = has_fr ? m->fr_R[lane] : 1.f;
     const float fr_fl = has_fr ? m->fr_floss[lane] : 0.f;
     const float fr_aref = -m->fr_B * qvel_r;
-    float mdiag = invmc;
-#pragma unroll
-    for (int j = 0; j < 6; j++) mdiag = (lane == j) ? minv_row[j] : mdiag;
-    const float fr_AR = mdiag + fr_R;
-    const float fr_ARinv = 1.f / fr_AR;
     float fr_f;
     {
       const float jar = warm_r - fr_aref;
@@ -1274,9 +1203,11 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
       else fr_f = -jar / fr_R;
       if (!has_fr) fr_f = 0.f;
     }
-    // joint-limit row of hinge `lane`
+    float mdiag = invmc;
+#pragma unroll
+    for (int j = 0; j < 6; j++) mdiag = (lane == j) ? minv_row[j] : mdiag;
     bool lim_on = false;
-    float lim_s = 0.f, lim_aref = 0.f, lim_R = 1.f, lim_AR = 1.f, lim_f = 0.f;
+    float lim_s = 0.f, lim_aref = 0.f, lim_R = 1.f, lim_f = 0.f;
     if (lane < 6) {
       const float dlo = qpos_r - m->jnt_lo[lane], dhi = m->jnt_hi[lane] - qpos_r;
       float dist = 0.f;
@@ -1286,7 +1217,6 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
         const float imp = getimpedance(m->lim_solimp, dist, 0.f);
         lim_R = fmaxf(kMinVal, (1.f - imp) / imp * m->lim_invw[lane]);
         lim_aref = -m->lim_B * (lim_s * qvel_r) - m->lim_K * imp * dist;
-        lim_AR = mdiag + lim_R;
         const float jar = lim_s * warm_r - lim_aref;
         lim_f = jar < 0.f ? -jar / lim_R : 0.f;
       }
@@ -1297,11 +1227,15 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
     if (has_fr) cost_part += 0.5f * fr_R * fr_f * fr_f + fr_f * (qs_r - fr_aref);
     if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
 
-    // ---------------- S6: per-contact constraint setup (DPP row reductions; scalar part per env)
+    // ---------------- S6: per-contact Jacobian rows (-> HBM) and constraint setup (DPP row reductions)
 #pragma unroll
     for (int c = 0; c < kMaxCon; c++) {
       if (c < ncon_max) {
-        const float4 J = Jr[c];
+        float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c < ncon && lane < SO100_NV) {
+          J = contact_jac(m, sh, c, lane);
+          reinterpret_cast<float4*>(crec + c * kConRec + 36)[lane] = J;
+        }
         const float4 M = minv_times(J, minv_row, invmc, lane);   // M^-1 J' column of this dof
         const float jv[4] = {J.x, J.y, J.z, J.w}, mv[4] = {M.x, M.y, M.z, M.w};
         float ARb[4][4], vel[4], acc[4], ws[4];
@@ -1403,167 +1337,55 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
     } else {
       qacc_c += dq;
     }
-    if (lane >= SO100_NV) qacc_c = 0.f;
     __syncthreads();
 
-    STAMP(2);
-    // ---------------- S8: projected Gauss-Seidel (MuJoCo mj_solPGS order: friction | limits | contacts)
-    bool done = !valid;
-    int iters = 0;
-    float last_impr = 0.f;
-    for (int it = 0; it < m->iterations; it++) {
-      if (__ballot(!done) == 0ull) break;
-      // keep the per-contact LDS loads inside the sweep (no LICM of 16 contacts' blocks into VGPRs)
-      asm volatile("" ::: "memory");
-      float impr = 0.f;
-      // arm frictionloss rows: sequential, coupled through M^-1 (row broadcast by DPP)
+    // ---------------- solver record -> HBM (consumed by so100_pgs_kernel)
+    if (valid) {
+      if (lane < SO100_NV) {
+        const int q = lane / 3, k = lane - 3 * (lane / 3);
+        float* hd = args.w.hdr + (size_t)e * kHdrEnv + q * kHdrLane;
+        hd[H_QACC + k] = qacc_c;
+        hd[H_FRAREF + k] = fr_aref;
+        hd[H_FRF + k] = fr_f;
+        hd[H_LIMS + k] = lim_on ? lim_s : 0.f;
+        hd[H_LIMAREF + k] = lim_aref;
+        hd[H_LIMR + k] = lim_R;
+        hd[H_LIMF + k] = lim_f;
+        float* mr = hd + H_MROW + 6 * k;
+        if (lane < 6) {
+          const int own = 3 * q, par = 3 - own;
 #pragma unroll
-      for (int j = 0; j < 6; j++) {
-        // every lane evaluates the row update on its own dof, only lane j keeps it (no exec branching)
-        const bool mine = (lane == j) && !done;
-        const float res = qacc_c - fr_aref + fr_R * fr_f;
-        const float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
-        const float delta = mine ? fn - fr_f : 0.f;
-        fr_f += delta;
-        impr -= delta * (res + 0.5f * fr_AR * delta);
-        qacc_c += minv_row[j] * bcast_row(delta, j);
-      }
-      // cube frictionloss rows: decoupled (diagonal M), all six in parallel
-      if (lane >= 6 && lane < 12 && !done) {
-        const float res = qacc_c - fr_aref + fr_R * fr_f;
-        const float old = fr_f;
-        const float fn = fminf(fmaxf(fr_f - res * fr_ARinv, -fr_fl), fr_fl);
-        const float delta = fn - old;
-        fr_f = fn;
-        impr -= delta * (res + 0.5f * fr_AR * delta);
-        qacc_c += invmc * delta;
-      }
-      // joint-limit rows (hinge order)
-      if (lim_mask) {
+          for (int i = 0; i < 3; i++) { mr[i] = sh.minv[lane][own + i]; mr[3 + i] = sh.minv[lane][par + i]; }
+        } else {
 #pragma unroll
-        for (int j = 0; j < 6; j++) {
-          if (!((lim_mask >> j) & 0x0001000100010001ull)) continue;
-          float delta = 0.f;
-          if (lane == j && lim_on && !done) {
-            const float res = lim_s * qacc_c - lim_aref + lim_R * lim_f;
-            const float old = lim_f;
-            const float fn = fmaxf(lim_f - res / lim_AR, 0.f);
-            delta = fn - old;
-            lim_f = fn;
-            impr -= delta * (res + 0.5f * lim_AR * delta);
-            delta *= lim_s;
-          }
-          qacc_c += minv_row[j] * bcast_row(delta, j);
+          for (int i = 0; i < 6; i++) mr[i] = (i == k) ? invmc : 0.f;
+        }
+        if (k == 0) hd[H_NCON] = __int_as_float(ncon);
+      }
+
+      for (int c = 0; c < ncon; c++)
+        if (lane < 9) reinterpret_cast<float4*>(crec + c * kConRec)[lane] = reinterpret_cast<const float4*>(&sh.con[c].s)[lane];
+      if (kMode == 1) {
+        if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
+        if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
+      }
+      // debug: contact set of the last substep (forces / iterations come from the solver kernel)
+      if (B.debug && args.sub == m->nsubstep - 1) {
+        float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
+        if (lane < kMaxCon) {
+          dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
+          dbg[48 + lane] = lane < ncon ? (float)sh.con_pair[lane] : -1.f;
+        }
+        if (lane < SO100_NV) dbg[64 + lane] = qs_r;
+        if (lane == 0) {
+          dbg[0] = (float)ncon;
+          dbg[3] = (float)(12 + __popcll(lim_mask & (0xFFFFull << (grp * 16))) + 4 * ncon);
         }
       }
-      STAMP(3);
-      // contact blocks (elliptic, condim 4): normal update, then friction QCQP on the cone
-#pragma unroll
-      for (int c = 0; c < kMaxCon; c++) {
-        if (c < ncon_max) {
-          // the whole 144-B block as 9 x ds_read_b128, issued before the row reductions so the LDS
-          // latency overlaps them (unconditional: inactive envs read their own unused slot)
-          const float4* cv = reinterpret_cast<const float4*>(&sh.con[c].s);
-          const float4 v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3], v4 = cv[4], v5 = cv[5];
-          const float4 v6 = cv[6], v7 = cv[7], v8 = cv[8];
-          const float j0 = rowsum16(Jr[c].x * qacc_c), j1 = rowsum16(Jr[c].y * qacc_c);
-          const float j2 = rowsum16(Jr[c].z * qacc_c), j3 = rowsum16(Jr[c].w * qacc_c);
-          // unpack (layout of ConSolve)
-          const float a00 = v0.x, a01 = v0.y, a02 = v0.z, a03 = v0.w, a11 = v1.x, a12 = v1.y, a13 = v1.z;
-          const float a22 = v1.w, a23 = v2.x, a33 = v2.y;
-          const float Qe[9] = {v2.z, v2.w, v3.x, v3.y, v3.z, v3.w, v4.x, v4.y, v4.z};
-          const float lam[3] = {v4.w, v5.x, v5.y};
-          const float R0 = v5.z, arinv0 = v5.w, mu0 = v8.x, mu1 = v8.y, R1 = v8.z, R3 = v8.w;
-          const float4 ar = v6, f4 = v7;
-          float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (c < ncon && !done) {
-            const float res[4] = {j0 - ar.x + R0 * f4.x, j1 - ar.y + R1 * f4.y, j2 - ar.z + R1 * f4.z,
-                                  j3 - ar.w + R3 * f4.w};
-            const float old[4] = {f4.x, f4.y, f4.z, f4.w};
-            float f[4];
-            f[0] = old[0] - res[0] * arinv0;
-            if (f[0] < kMinVal) {
-              f[0] = f[1] = f[2] = f[3] = 0.f;
-            } else {
-              const float dn = f[0] - old[0];
-              float bf[3];
-              bf[0] = res[1] + a01 * dn - (a11 * old[1] + a12 * old[2] + a13 * old[3]);
-              bf[1] = res[2] + a02 * dn - (a12 * old[1] + a22 * old[2] + a23 * old[3]);
-              bf[2] = res[3] + a03 * dn - (a13 * old[1] + a23 * old[2] + a33 * old[3]);
-              float x[3];
-              qcqp3_eig(x, Qe, lam, bf, mu0, mu1, f[0]);
-              f[1] = x[0]; f[2] = x[1]; f[3] = x[2];
-            }
-            const float dl[4] = {f[0] - old[0], f[1] - old[1], f[2] - old[2], f[3] - old[3]};
-            if (lane == 0) {
-              const float q0 = a00 * dl[0] + a01 * dl[1] + a02 * dl[2] + a03 * dl[3];
-              const float q1 = a01 * dl[0] + a11 * dl[1] + a12 * dl[2] + a13 * dl[3];
-              const float q2 = a02 * dl[0] + a12 * dl[1] + a22 * dl[2] + a23 * dl[3];
-              const float q3 = a03 * dl[0] + a13 * dl[1] + a23 * dl[2] + a33 * dl[3];
-              impr -= dl[0] * (res[0] + 0.5f * q0) + dl[1] * (res[1] + 0.5f * q1) + dl[2] * (res[2] + 0.5f * q2) +
-                      dl[3] * (res[3] + 0.5f * q3);
-            }
-            reinterpret_cast<float4*>(&sh.con[c].s)[7] = make_float4(f[0], f[1], f[2], f[3]);
-            d4 = make_float4(dl[0], dl[1], dl[2], dl[3]);
-          }
-          // qacc += M^-1 J' d: g = J_dof . d per lane, then the arm's M^-1 row via row broadcasts
-          const float g = (Jr[c].x * d4.x + Jr[c].y * d4.y) + (Jr[c].z * d4.z + Jr[c].w * d4.w);
-          const float u01 = minv_row[0] * bcast_row(g, 0) + minv_row[1] * bcast_row(g, 1);
-          const float u23 = minv_row[2] * bcast_row(g, 2) + minv_row[3] * bcast_row(g, 3);
-          const float u45 = minv_row[4] * bcast_row(g, 4) + minv_row[5] * bcast_row(g, 5);
-          qacc_c += (invmc * g + u01) + (u23 + u45);
-        }
-      }
-      STAMP(4);
-      const float improvement = rowsum16(impr) * m->pgs_scale;
-      if (!done) {
-        iters = it + 1;
-        last_impr = improvement;
-        if (improvement < m->tolerance) done = true;
-      }
     }
-    STAMP(3);
-    dbg_iter = (float)iters;
-    dbg_impr = last_impr;
-    dbg_nefc = 12 + __popcll(lim_mask & (0xFFFFull << (grp * 16))) + 4 * ncon;
-
-    // debug: contact normal forces of the last substep
-    if (B.debug && valid && sub == m->nsubstep - 1) {
-      float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
-      if (lane < kMaxCon) {
-        dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
-        dbg[32 + lane] = lane < ncon ? sh.con[lane].s.f.x : 0.f;
-        dbg[48 + lane] = lane < ncon ? (float)sh.con_pair[lane] : -1.f;
-      }
-      if (lane < SO100_NV) { dbg[4 + lane] = qacc_c; dbg[64 + lane] = qs_r; dbg[76 + lane] = fr_f; }
-      if (lane == 0) { dbg[0] = (float)ncon; dbg[1] = dbg_iter; dbg[2] = dbg_impr; dbg[3] = (float)dbg_nefc; }
-    }
-
-    // ---------------- S9: semi-implicit Euler (mj_Euler): qvel += h qacc; qpos with the new qvel
-    if (lane < SO100_NV) qvel_r += h * qacc_c;
-    warm_r = (lane < SO100_NV) ? qacc_c : 0.f;
-    if (lane < 9) qpos_r += h * qvel_r;
-    __syncthreads();
-    if (lane >= 9 && lane < 12) sh.vec[lane] = qvel_r;
-    if (lane >= 9 && lane < 13) sh.qpos[lane] = qpos_r;
-    __syncthreads();
-    if (lane >= 9 && lane < 13) {
-      float q[4] = {sh.qpos[9], sh.qpos[10], sh.qpos[11], sh.qpos[12]};
-      float w[3] = {sh.vec[9], sh.vec[10], sh.vec[11]};
-      float nw = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-      if (nw > kMinVal) {
-        float s, c;
-        sincosf(0.5f * h * nw, &s, &c);
-        float qr[4] = {c, w[0] / nw * s, w[1] / nw * s, w[2] / nw * s};
-        quat_mul(q, q, qr);
-      }
-      quat_normalize(q);
-      qpos_r = q[lane - 9];
-    }
-    __syncthreads();
+    return;
   }
 
-  STAMP(5);
   // ---------------- final position stage (mj_step1): sites + contact set for reward / obs
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
@@ -1664,14 +1486,6 @@ __global__ void __launch_bounds__(kThreads, 3) so100_step_kernel(StepArgs args) 
     }
   }
 
-  STAMP(6);
-#ifdef SO100_STAMPS
-  if (B.debug && valid && lane == 0) {
-    float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
-#pragma unroll
-    for (int k = 0; k < 7; k++) dbg[88 + k] = (float)st_acc_[k];
-  }
-#endif
   // ---------------- store state
   if (valid) {
     if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
@@ -1783,12 +1597,48 @@ __global__ void so100_goal_reward_kernel(const DevModel* m, int n, const float* 
 }
 
 // ------------------------------------------------------------------ launchers (called by so100_capi.cpp)
-hipError_t launch_step(const DevModel* m, const so100_buffers& b, int n, int task, int flags, int max_steps,
-                       uint64_t base_seed, int env_offset, hipStream_t s) {
-  StepArgs a{m, b, n, task, flags, max_steps, base_seed, env_offset};
-  dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
-  hipLaunchKernelGGL(so100_step_kernel, grid, dim3(kThreads), 0, s, a);
-  return hipGetLastError();
+hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
+                      hipStream_t s);
+
+
+// One env step = nsubstep x (stage, solve) + the final stage: 2 * nsubstep + 1 launches on one stream.
+hipError_t launch_step(const DevModel* m, int nsubstep, const Workspace& w, const so100_buffers& b, int n, int task,
+                       int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s) {
+  StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0};
+  const dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
+  for (int sub = 0; sub <= nsubstep; sub++) {
+    a.sub = sub;
+    if (sub == 0) hipLaunchKernelGGL(so100_stage_kernel<0>, grid, dim3(kThreads), 0, s, a);
+    else if (sub < nsubstep) hipLaunchKernelGGL(so100_stage_kernel<1>, grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(so100_stage_kernel<2>, grid, dim3(kThreads), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (sub < nsubstep) {
+      e = launch_pgs(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, s);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+hipError_t free_workspace(Workspace* w);
+hipError_t alloc_workspace(int n, Workspace* w) {
+  w->hdr = nullptr;
+  w->con = nullptr;
+  hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kMaxCon * kConRec * sizeof(float));
+  if (e != hipSuccess) (void)free_workspace(w);
+  return e;
+}
+hipError_t free_workspace(Workspace* w) {
+  hipError_t r = hipSuccess;
+  for (void* p : {(void*)w->hdr, (void*)w->con}) {
+    if (!p) continue;
+    hipError_t e = hipFree(p);
+    if (r == hipSuccess) r = e;
+  }
+  w->hdr = w->con = nullptr;
+  return r;
 }
 hipError_t launch_reset(const DevModel* m, const so100_buffers& b, int n, int task, uint64_t base_seed,
                         int env_offset, const uint8_t* mask, const uint32_t* seeds, hipStream_t s) {

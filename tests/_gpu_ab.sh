@@ -1,11 +1,20 @@
+# A/B of library variants (gym_so100/_lib_var/libso100_hip_<name>.so) against the in-tree build on ONE box:
+# bench (default steps) twice each, then a kernel trace of each in the bench's steady state.
+# usage: bash tests/_gpu_ab.sh name1 name2 ...   (writes gpurun_out/ab/*)
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -rA > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-if [ $rc -gt 1 ]; then exit $rc; fi
+O=gpurun_out/ab
+rm -rf $O; mkdir -p $O
+V=gym-so100-c_amd/gym_so100/_lib_var
 for i in 1 2; do
-timeout -k 10 200 python bench.py --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/ab_base_$i.log 2>&1 || exit $?
-SO100_LIB=gym-so100-c_amd/gym_so100/_lib_var/libso100_hip_noslp.so timeout -k 10 200 python bench.py --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/ab_noslp_$i.log 2>&1 || exit $?
+  timeout -k 10 200 python bench.py --no-cpu-baseline > $O/base_$i.log 2>&1 || exit $?
+  for n in "$@"; do
+    SO100_LIB=$V/libso100_hip_$n.so timeout -k 10 200 python bench.py --no-cpu-baseline > $O/${n}_$i.log 2>&1 || exit $?
+  done
 done
-SO100_LIB=gym-so100-c_amd/gym_so100/_lib_var/libso100_hip_stamps.so timeout -k 10 300 python tests/_stamps_report.py > gpurun_out/stamps.log 2>&1 || exit $?
-for f in gpurun_out/ab_*.log; do echo $f $(grep -o '"value": [0-9.]*' $f); done
+T="python bench.py --steps 20 --warmup 60 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o base --output-format csv -- $T > $O/trace_base.log 2>&1 || exit $?
+for n in "$@"; do
+  SO100_LIB=$V/libso100_hip_$n.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o $n --output-format csv -- $T > $O/trace_$n.log 2>&1 || exit $?
+done
+for f in $O/*_[12].log; do echo $f $(grep -o '"value": [0-9.]*' $f); done
+echo ABDONE

@@ -1,5 +1,6 @@
-"""Diagnostic: per-phase cycle attribution of the step kernel (stamps build via SO100_LIB)."""
-import os, sys, json
+"""Diagnostic: per-phase cycle attribution of the PGS kernel (last substep), grouped by the wave's max
+contact count, and QCQP Newton steps per env (stamps build via SO100_LIB)."""
+import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
@@ -9,26 +10,31 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 env = SO100VecEnv(n, device="cuda:0", debug=True)
 env.reset(seed=1000)
 g = torch.Generator(device="cuda").manual_seed(0)
-for i in range(30):
+for i in range(60):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
 torch.cuda.synchronize()
-acc = np.zeros(7)
-ncon, iters = [], []
-for i in range(5):
+D = []
+for i in range(3):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
-    d = env.debug.cpu().numpy()
-    acc += d[::4, 88:95].mean(0)
-    ncon.append(d[:, 0]); iters.append(d[:, 1])
-acc /= 5
-names = ["S1-S2 serial", "S3 collision", "S4-S7 setup", "PGS friction+limits", "PGS contacts", "S9 euler/debug", "final+epilogue"]
-tot = acc.sum()
-out = {k: float(v) for k, v in zip(names, acc)}
-print(json.dumps(out, indent=1))
-for k, v in zip(names, acc):
-    print(f"{k:22s} {v/1e6:8.3f} Mcyc  {100*v/tot:5.1f}%")
-nc = np.concatenate(ncon); it = np.concatenate(iters)
-print("ncon last substep: mean %.2f, hist %s" % (nc.mean(), np.bincount(nc.astype(int), minlength=17)[:17].tolist()))
-print("PGS iterations last substep: mean %.1f, frac==100 %.3f" % (it.mean(), (it == 100).mean()))
-nm = nc.reshape(-1, 4).max(1)
-print("wave-max ncon mean %.2f" % nm.mean())
+    D.append(env.debug.cpu().numpy())
+d = np.concatenate(D)
+ncon = d[:, 0].astype(int)
+wmax = np.repeat(ncon.reshape(-1, 16).max(1), 16)
+st = d[:, 88:93]
+newton = d[:, 93]
+names = ["record load", "friction+limits", "contacts (resident)", "contacts (overflow)", "tail"]
+print("all waves: " + ", ".join(f"{k} {v / 1e3:.1f}K" for k, v in zip(names, st[::16].mean(0))))
+for k in range(0, 17):
+    m = wmax == k
+    if m.sum() == 0:
+        continue
+    w = st[m][::16].mean(0)
+    per_contact = (w[2] + w[3]) / max(k, 1) / 100
+    print(f"wave-max ncon {k:2d}: {m.sum() // 16:5d} waves | " + " ".join(f"{v / 1e3:7.1f}K" for v in w) +
+          f" | {per_contact:6.0f} cyc/contact-sweep | newton/env {newton[m].mean():8.0f}")
+print("newton steps per (contact, sweep) by env ncon:")
+for k in range(1, 17):
+    m = ncon == k
+    if m.sum():
+        print(f"  ncon {k:2d}: {m.sum():6d} envs, newton per env {newton[m].mean():8.0f} -> per contact-sweep {newton[m].mean() / k / 100:.2f}")
