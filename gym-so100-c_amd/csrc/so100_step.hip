@@ -1227,94 +1227,118 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
     if (has_fr) cost_part += 0.5f * fr_R * fr_f * fr_f + fr_f * (qs_r - fr_aref);
     if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
 
-    // ---------------- S6: per-contact Jacobian rows (-> HBM) and constraint setup (DPP row reductions)
+    // ---------------- S6a: per-contact Jacobian rows (-> HBM) and the row reductions (lane = dof, DPP).
+    // Lane c keeps contact c's reductions: the scalar setup below then runs once per contact, in parallel
+    // over the contacts, instead of redundantly on all 16 lanes for every contact.
+    float4 Jr[kMaxCon];
+    float cA[10], cV[4], cAc[4], cW[4];     // contact `lane`: (A)_upper, J qvel, J qacc_smooth, J qacc_warmstart
+#pragma unroll
+    for (int k = 0; k < 10; k++) cA[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; r++) cV[r] = cAc[r] = cW[r] = 0.f;
 #pragma unroll
     for (int c = 0; c < kMaxCon; c++) {
+      Jr[c] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (c < ncon_max) {
         float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c < ncon && lane < SO100_NV) {
           J = contact_jac(m, sh, c, lane);
           reinterpret_cast<float4*>(crec + c * kConRec + 36)[lane] = J;
         }
+        Jr[c] = J;
         const float4 M = minv_times(J, minv_row, invmc, lane);   // M^-1 J' column of this dof
         const float jv[4] = {J.x, J.y, J.z, J.w}, mv[4] = {M.x, M.y, M.z, M.w};
-        float ARb[4][4], vel[4], acc[4], ws[4];
+        const bool mine = lane == c;
+        int k = 0;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
 #pragma unroll
-          for (int q = r; q < 4; q++) { ARb[r][q] = rowsum16(jv[r] * mv[q]); ARb[q][r] = ARb[r][q]; }
-          vel[r] = rowsum16(jv[r] * qvel_r);
-          acc[r] = rowsum16(jv[r] * qs_r);
-          ws[r] = rowsum16(jv[r] * warm_r);
-        }
-        float f[4] = {0.f, 0.f, 0.f, 0.f};
-        if (c < ncon) {
-          const int p = sh.con_pair[c];
-          const float dist = sh.con_dist[c];
-          const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
-          const float K = m->pair_K[p], Bd = m->pair_B[p];
-          const float mu0 = m->pair_mu0[p] * fscale, mu1 = m->pair_mu1[p] * fscale;
-          float R[4];
-          R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
-          R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
-          R[2] = R[1];
-          R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
-          float aref[4];
-          aref[0] = -Bd * vel[0] - K * imp * (dist - m->pair_margin[p]);
-          aref[1] = -Bd * vel[1]; aref[2] = -Bd * vel[2]; aref[3] = -Bd * vel[3];
-#pragma unroll
-          for (int r = 0; r < 4; r++) ARb[r][r] += R[r];
-          // warmstart force: dual map of jar = J qacc_warmstart - aref (elliptic zones)
-          float jar[4];
-#pragma unroll
-          for (int r = 0; r < 4; r++) jar[r] = ws[r] - aref[r];
-          const float mus[3] = {mu0, mu0, mu1};
-          {
-            const float mu = mu0 * sqrtf(R[1] / R[0]);
-            float U[4], T = 0.f;
-            U[0] = jar[0] * mu;
-#pragma unroll
-            for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
-            T = sqrtf(T);
-            const float N = U[0];
-            if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
-              f[0] = f[1] = f[2] = f[3] = 0.f;
-            } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
-#pragma unroll
-              for (int k = 0; k < 4; k++) f[k] = -jar[k] / R[k];
-            } else {
-              const float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
-              const float NmT = N - mu * T;
-              f[0] = -Dm * NmT * mu;
-#pragma unroll
-              for (int k = 1; k < 4; k++) f[k] = -f[0] / T * U[k] * mus[k - 1];
-            }
+          for (int q = r; q < 4; q++, k++) {
+            const float a = rowsum16(jv[r] * mv[q]);
+            cA[k] = mine ? a : cA[k];
           }
-          // QCQP data: eigen-decomposition of the cone-scaled friction block (constant over the sweeps)
-          float As[3][3], Qe[3][3], lam[3];
-#pragma unroll
-          for (int a = 0; a < 3; a++)
-#pragma unroll
-            for (int b2 = 0; b2 < 3; b2++) As[a][b2] = ARb[1 + a][1 + b2] * mus[a] * mus[b2];
-          eig3_sym(As, lam, Qe);
-          ConSolve& cs = sh.con[c].s;
-          cs.ar[0] = ARb[0][0]; cs.ar[1] = ARb[0][1]; cs.ar[2] = ARb[0][2]; cs.ar[3] = ARb[0][3];
-          cs.ar[4] = ARb[1][1]; cs.ar[5] = ARb[1][2]; cs.ar[6] = ARb[1][3];
-          cs.ar[7] = ARb[2][2]; cs.ar[8] = ARb[2][3]; cs.ar[9] = ARb[3][3];
-#pragma unroll
-          for (int k = 0; k < 9; k++) cs.q[k] = Qe[k / 3][k % 3];
-          cs.lam[0] = lam[0]; cs.lam[1] = lam[1]; cs.lam[2] = lam[2];
-          cs.mu0 = mu0; cs.mu1 = mu1;
-          cs.aref = make_float4(aref[0], aref[1], aref[2], aref[3]);
-          cs.R0 = R[0]; cs.R1 = R[1]; cs.R3 = R[3];
-          cs.f = make_float4(f[0], f[1], f[2], f[3]);
-          cs.arinv0 = 1.f / ARb[0][0];
-          if (lane == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * f[r] * f[r] + f[r] * (acc[r] - aref[r]);
-          }
+          const float v = rowsum16(jv[r] * qvel_r), ac = rowsum16(jv[r] * qs_r), w = rowsum16(jv[r] * warm_r);
+          cV[r] = mine ? v : cV[r];
+          cAc[r] = mine ? ac : cAc[r];
+          cW[r] = mine ? w : cW[r];
         }
-        phi += J.x * f[0] + J.y * f[1] + J.z * f[2] + J.w * f[3];
+      }
+    }
+    // ---------------- S6b: scalar setup of contact `lane` (impedance, regularisers, warmstart dual map,
+    // eigen-decomposition for the QCQP) -> solver block in the HBM record
+    float cf[4] = {0.f, 0.f, 0.f, 0.f};
+    if (lane < ncon) {
+      const int p = sh.con_pair[lane];
+      const float dist = sh.con_dist[lane];
+      const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
+      const float K = m->pair_K[p], Bd = m->pair_B[p];
+      const float mu0 = m->pair_mu0[p] * fscale, mu1 = m->pair_mu1[p] * fscale;
+      float R[4];
+      R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
+      R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
+      R[2] = R[1];
+      R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
+      float aref[4];
+      aref[0] = -Bd * cV[0] - K * imp * (dist - m->pair_margin[p]);
+      aref[1] = -Bd * cV[1]; aref[2] = -Bd * cV[2]; aref[3] = -Bd * cV[3];
+      // A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
+      float ar[10];
+#pragma unroll
+      for (int k = 0; k < 10; k++) ar[k] = cA[k];
+      ar[0] += R[0]; ar[4] += R[1]; ar[7] += R[2]; ar[9] += R[3];
+      // warmstart force: dual map of jar = J qacc_warmstart - aref (elliptic zones)
+      float jar[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) jar[r] = cW[r] - aref[r];
+      const float mus[3] = {mu0, mu0, mu1};
+      {
+        const float mu = mu0 * sqrtf(R[1] / R[0]);
+        float U[4], T = 0.f;
+        U[0] = jar[0] * mu;
+#pragma unroll
+        for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
+        T = sqrtf(T);
+        const float N = U[0];
+        if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
+          cf[0] = cf[1] = cf[2] = cf[3] = 0.f;
+        } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) cf[k] = -jar[k] / R[k];
+        } else {
+          const float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
+          const float NmT = N - mu * T;
+          cf[0] = -Dm * NmT * mu;
+#pragma unroll
+          for (int k = 1; k < 4; k++) cf[k] = -cf[0] / T * U[k] * mus[k - 1];
+        }
+      }
+      // QCQP data: eigen-decomposition of the cone-scaled friction block (constant over the sweeps)
+      const float A11[3][3] = {{ar[4], ar[5], ar[6]}, {ar[5], ar[7], ar[8]}, {ar[6], ar[8], ar[9]}};
+      float As[3][3], Qe[3][3], lam[3];
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b2 = 0; b2 < 3; b2++) As[a][b2] = A11[a][b2] * mus[a] * mus[b2];
+      eig3_sym(As, lam, Qe);
+      // ConSolve layout (so100_common.h), f written after the warmstart decision
+      float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
+      cs[0] = make_float4(ar[0], ar[1], ar[2], ar[3]);
+      cs[1] = make_float4(ar[4], ar[5], ar[6], ar[7]);
+      cs[2] = make_float4(ar[8], ar[9], Qe[0][0], Qe[0][1]);
+      cs[3] = make_float4(Qe[0][2], Qe[1][0], Qe[1][1], Qe[1][2]);
+      cs[4] = make_float4(Qe[2][0], Qe[2][1], Qe[2][2], lam[0]);
+      cs[5] = make_float4(lam[1], lam[2], R[0], 1.f / ar[0]);
+      cs[6] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+      cs[8] = make_float4(mu0, mu1, R[1], R[3]);
+#pragma unroll
+      for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
+    }
+    // J' f of the warmstart forces: contact c's forces broadcast from lane c
+#pragma unroll
+    for (int c = 0; c < kMaxCon; c++) {
+      if (c < ncon_max) {
+        const float4 fc = bcast_row4(make_float4(cf[0], cf[1], cf[2], cf[3]), c);
+        phi += Jr[c].x * fc.x + Jr[c].y * fc.y + Jr[c].z * fc.z + Jr[c].w * fc.w;
       }
     }
     // ---------------- S7: warmstart dual cost 0.5 f'ARf + f'b (keep the warmstart only if <= 0)
@@ -1332,12 +1356,11 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
       fr_f = 0.f;
       lim_f = 0.f;
 #pragma unroll
-      for (int c = 0; c < kMaxCon; c++)
-        if (c < ncon_max && c < ncon) sh.con[c].s.f = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < 4; r++) cf[r] = 0.f;
     } else {
       qacc_c += dq;
     }
-    __syncthreads();
+    if (lane < ncon) reinterpret_cast<float4*>(crec + lane * kConRec)[7] = make_float4(cf[0], cf[1], cf[2], cf[3]);
 
     // ---------------- solver record -> HBM (consumed by so100_pgs_kernel)
     if (valid) {
@@ -1362,9 +1385,6 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
         }
         if (k == 0) hd[H_NCON] = __int_as_float(ncon);
       }
-
-      for (int c = 0; c < ncon; c++)
-        if (lane < 9) reinterpret_cast<float4*>(crec + c * kConRec)[lane] = reinterpret_cast<const float4*>(&sh.con[c].s)[lane];
       if (kMode == 1) {
         if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
         if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
