@@ -28,23 +28,6 @@ constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;
 
-// ------------------------------------------------------------------ LDS layout (per env)
-struct __attribute__((aligned(16))) ConSolve {   // per-contact PGS data (144 B = 9 x ds_read_b128;
-                                                 // the PGS reads it as float4[9], keep the order)
-  // symmetric 4x4 block of A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
-  float ar[10];
-  // eigen-decomposition of the cone-scaled friction block As = D A11 D (D = diag(mu0, mu0, mu1)):
-  // As = Q diag(lam) Q', Q row-major (columns = eigenvectors) — QCQP Newton without 3x3 inverses
-  float q[9];
-  float lam[3];
-  float R0, arinv0;    // normal-row regulariser, 1 / AR00
-  float4 aref;
-  float4 f;            // current forces (normal, t1, t2, torsion)
-  float mu0, mu1;      // cone coefficients (mu0, mu0, mu1)
-  float R1, R3;        // friction-row regularisers (R2 = R1)
-};
-static_assert(sizeof(ConSolve) == 144 && offsetof(ConSolve, aref) == 96 && offsetof(ConSolve, f) == 112 &&
-                  offsetof(ConSolve, mu0) == 128, "ConSolve layout is read as float4[9] in the PGS");
 // ------------------------------------------------------------------ cross-lane (16-lane row) primitives
 template <int CTRL>
 DEV float dpp(float v) {
@@ -63,8 +46,9 @@ DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 
 // MuJoCo mju_QCQP3 restated (engine_util_solve.c): min 0.5 x'Ax + x'b s.t. sum (x_i/d_i)^2 <= r^2.
 // The minimiser is y(la) = -(As + la I)^-1 D b for the multiplier la >= 0 that puts y on the sphere
-// |y| = r (As = D A D, D = diag(mu0, mu0, mu1)).  In the eigenbasis of As (precomputed per substep)
-// y_i(la) = c_i / (lam_i + la) with c = -Q' D b, so an iterate costs three reciprocals.
+// |y| = r (As = D A D, D = diag(mu0, mu0, mu1)).  In the eigenbasis of As (precomputed per substep,
+// with P = Q' D and 1/lam) y_i(la) = c_i / (lam_i + la) with c = -P b, so an iterate costs three
+// reciprocals, and x = D Q w = P' w.
 // Root finding: MuJoCo runs Newton on |y|^2 - r^2 from la = 0, which on this 1/la^2-shaped function
 // advances la by at most x1.5 per step while far from the root (3.5-7 steps per contact-sweep on
 // sliding grasp contacts).  We solve the same equation with Newton on 1/|y(la)| - 1/r (the trust-region
@@ -72,17 +56,14 @@ DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 // bound la0 = max(0, |c|/r - max lam) <= la*: from the left it converges monotonically to the same root,
 // with MuJoCo's exit tests (val < 1e-10, delta < 1e-10) plus an fp32 step test.  1-2 steps typical.
 // Returns the number of Newton steps taken (diagnostics).
-DEV int qcqp3_eig(float* x, const float* Q, const float* lam, const float* b0, float mu0, float mu1, float r,
+DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* laminv, const float* b, float r,
                   bool live = true) {
   int nit = 0;
-  const float dd[3] = {mu0, mu0, mu1};
-  float bs[3], c[3], w[3], d[3];
+  float c[3], w[3], d[3];
 #pragma unroll
-  for (int i = 0; i < 3; i++) bs[i] = b0[i] * dd[i];
+  for (int i = 0; i < 3; i++) c[i] = -(P[3 * i] * b[0] + P[3 * i + 1] * b[1] + P[3 * i + 2] * b[2]);   // -P b
 #pragma unroll
-  for (int i = 0; i < 3; i++) c[i] = -(Q[i] * bs[0] + Q[3 + i] * bs[1] + Q[6 + i] * bs[2]);   // -Q' b
-#pragma unroll
-  for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i]); w[i] = c[i] * d[i]; }
+  for (int i = 0; i < 3; i++) { d[i] = laminv[i]; w[i] = c[i] * d[i]; }
   float s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   if (live && s - r * r >= 1e-10f) {
     const float rinv = __builtin_amdgcn_rcpf(r);
@@ -104,9 +85,9 @@ DEV int qcqp3_eig(float* x, const float* Q, const float* lam, const float* b0, f
       s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     }
   }
-  // y = Q w, x = D y
+  // x = D Q w = P' w
 #pragma unroll
-  for (int i = 0; i < 3; i++) x[i] = (Q[3 * i] * w[0] + Q[3 * i + 1] * w[1] + Q[3 * i + 2] * w[2]) * dd[i];
+  for (int j = 0; j < 3; j++) x[j] = P[j] * w[0] + P[3 + j] * w[1] + P[6 + j] * w[2];
   return nit;
 }
 

@@ -88,10 +88,18 @@ struct DevModel {
 // the constraint rows, the PGS kernel (4 lanes per env, 3 dofs per lane) solves them.  The hand-off
 // is a per-env record in HBM, laid out for the solver's lanes:
 //   hdr[env][q][kHdrLane]  lane q owns dofs 3q..3q+2 (q = 0,1: arm, q = 2,3: cube)
-//   con[env][c][kConRec]   ConSolve (36 floats) then J[dof][row] (12 x 4 floats)
+//   con[env][c][kConRec]   solver block (kBlk float4) then J[dof][row] (12 x 4 floats)
 constexpr int kHdrLane = 40;
 constexpr int kHdrEnv = 4 * kHdrLane;
-constexpr int kConRec = 36 + 48;
+// Solver block of one contact, read by the PGS as kBlk x ds_read_b128 (float index: content):
+//   0-9  A+R upper triangle 00 01 02 03 11 12 13 22 23 33     10-18  P = Q' D (row-major)
+//   19-21 lam (eigenvalues of D A11 D = Q diag(lam) Q')       22-24  1 / lam
+//   25 R0   26 1/(A+R)00   27 R1 (= R2)   28 R3   29-31 pad  32-35 aref   36-39 f (normal, t1, t2, torsion)
+constexpr int kBlk = 10;
+constexpr int kBlkAref = 8;       // float4 slots
+constexpr int kBlkF = 9;
+constexpr int kJOff = 4 * kBlk;   // float offset of the J rows in the record
+constexpr int kConRec = kJOff + 48;
 enum HdrField : int {
   H_QACC = 0,       // qacc at the solver start (qacc_smooth, plus M^-1 J' f of the kept warmstart)
   H_FRAREF = 3,     // frictionloss rows: aref = -B vel

@@ -37,19 +37,20 @@ struct PgsArgs {
 // M^-1 J' (f_new - f_old).  Straight-line apart from the QCQP's Newton loop: every lane evaluates the
 // block and `active` selects the result, so the block's LDS reads issue together at the top instead of
 // being sunk into branches (three serialised LDS round trips per contact otherwise).
-DEV void contact_update(const float4 (&v)[9], const float4 (&J)[3], float (&qacc)[3], const float (&mrow)[3][6],
+DEV void contact_update(const float4 (&v)[kBlk], const float4 (&J)[3], float (&qacc)[3], const float (&mrow)[3][6],
                         bool active, bool lead, float& impr, float4& fout, int& newton) {
   const float j0 = quadsum(J[0].x * qacc[0] + J[1].x * qacc[1] + J[2].x * qacc[2]);
   const float j1 = quadsum(J[0].y * qacc[0] + J[1].y * qacc[1] + J[2].y * qacc[2]);
   const float j2 = quadsum(J[0].z * qacc[0] + J[1].z * qacc[1] + J[2].z * qacc[2]);
   const float j3 = quadsum(J[0].w * qacc[0] + J[1].w * qacc[1] + J[2].w * qacc[2]);
-  // unpack (layout of ConSolve)
+  // unpack (solver block layout: so100_device.h)
   const float a00 = v[0].x, a01 = v[0].y, a02 = v[0].z, a03 = v[0].w, a11 = v[1].x, a12 = v[1].y, a13 = v[1].z;
   const float a22 = v[1].w, a23 = v[2].x, a33 = v[2].y;
-  const float Qe[9] = {v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w, v[4].x, v[4].y, v[4].z};
+  const float P[9] = {v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w, v[4].x, v[4].y, v[4].z};
   const float lam[3] = {v[4].w, v[5].x, v[5].y};
-  const float R0 = v[5].z, arinv0 = v[5].w, mu0 = v[8].x, mu1 = v[8].y, R1 = v[8].z, R3 = v[8].w;
-  const float4 ar = v[6], f4 = v[7];
+  const float laminv[3] = {v[5].z, v[5].w, v[6].x};
+  const float R0 = v[6].y, arinv0 = v[6].z, R1 = v[6].w, R3 = v[7].x;
+  const float4 ar = v[kBlkAref], f4 = v[kBlkF];
   const float res[4] = {j0 - ar.x + R0 * f4.x, j1 - ar.y + R1 * f4.y, j2 - ar.z + R1 * f4.z, j3 - ar.w + R3 * f4.w};
   const float old[4] = {f4.x, f4.y, f4.z, f4.w};
   float f[4];
@@ -62,7 +63,7 @@ DEV void contact_update(const float4 (&v)[9], const float4 (&J)[3], float (&qacc
     bf[1] = res[2] + a02 * dn - (a12 * old[1] + a22 * old[2] + a23 * old[3]);
     bf[2] = res[3] + a03 * dn - (a13 * old[1] + a23 * old[2] + a33 * old[3]);
     float x[3];
-    newton += qcqp3_eig(x, Qe, lam, bf, mu0, mu1, f[0], active && open);
+    newton += qcqp3_eig(x, P, lam, laminv, bf, f[0], active && open);
     f[1] = open ? x[0] : 0.f;
     f[2] = open ? x[1] : 0.f;
     f[3] = open ? x[2] : 0.f;
@@ -92,7 +93,7 @@ DEV void contact_update(const float4 (&v)[9], const float4 (&J)[3], float (&qacc
 }
 
 __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs a) {
-  __shared__ float4 blk[kResident][kPgsEnvs][9];
+  __shared__ float4 blk[kResident][kPgsEnvs][kBlk];
   __shared__ float4 fov[kMaxCon - kResident][kPgsEnvs];   // forces of the streamed (overflow) contacts
   const DevModel* __restrict__ m = a.m;
   const int tid = threadIdx.x;
@@ -158,13 +159,13 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
   for (int c = 0; c < kResident; c++) {
     const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
 #pragma unroll
-    for (int i = 0; i < 3; i++) J[c][i] = rec[9 + 3 * q + i];
+    for (int i = 0; i < 3; i++) J[c][i] = rec[kBlk + 3 * q + i];
     blk[c][ew][q] = rec[q];
     blk[c][ew][q + 4] = rec[q + 4];
-    if (q == 0) blk[c][ew][8] = rec[8];
+    if (q < 2) blk[c][ew][q + 8] = rec[q + 8];
   }
   for (int c = kResident + q; c < ncon_max; c += 4)
-    fov[c - kResident][ew] = reinterpret_cast<const float4*>(crec + c * kConRec)[7];
+    fov[c - kResident][ew] = reinterpret_cast<const float4*>(crec + c * kConRec)[kBlkF];
   __syncthreads();
 
   STAMP(0);
@@ -216,40 +217,40 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
 #pragma unroll
     for (int c = 0; c < kResident; c++) {
       if (c < ncon_max) {
-        float4 v[9];
+        float4 v[kBlk];
 #pragma unroll
-        for (int k = 0; k < 9; k++) v[k] = blk[c][ew][k];
+        for (int k = 0; k < kBlk; k++) v[k] = blk[c][ew][k];
         float4 fn;
         const bool act = c < ncon && !done;
         contact_update(v, J[c], qacc, mrow, act, q == 0, impr, fn, newton);
-        if (act) blk[c][ew][7] = fn;
+        if (act) blk[c][ew][kBlkF] = fn;
       }
     }
     STAMP(2);
     // contact blocks beyond kResident (rare: >4 contacts): solver block and J rows streamed from the
     // record (read-only; the next contact's prefetched while the current one is solved), forces in LDS
     if (ncon_max > kResident) {
-      float4 vn[9], Jn[3];
+      float4 vn[kBlk], Jn[3];
       {
         const float4* rec = reinterpret_cast<const float4*>(crec + kResident * kConRec);
 #pragma unroll
-        for (int k = 0; k < 9; k++) vn[k] = k == 7 ? make_float4(0.f, 0.f, 0.f, 0.f) : rec[k];
+        for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? make_float4(0.f, 0.f, 0.f, 0.f) : rec[k];
 #pragma unroll
-        for (int i = 0; i < 3; i++) Jn[i] = rec[9 + 3 * q + i];
+        for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
       }
       for (int c = kResident; c < ncon_max; c++) {
-        float4 v[9], Jo[3];
+        float4 v[kBlk], Jo[3];
 #pragma unroll
-        for (int k = 0; k < 9; k++) v[k] = vn[k];
+        for (int k = 0; k < kBlk; k++) v[k] = vn[k];
 #pragma unroll
         for (int i = 0; i < 3; i++) Jo[i] = Jn[i];
-        v[7] = fov[c - kResident][ew];
+        v[kBlkF] = fov[c - kResident][ew];
         if (c + 1 < ncon_max) {
           const float4* rec = reinterpret_cast<const float4*>(crec + (c + 1) * kConRec);
 #pragma unroll
-          for (int k = 0; k < 9; k++) vn[k] = k == 7 ? make_float4(0.f, 0.f, 0.f, 0.f) : rec[k];
+          for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? make_float4(0.f, 0.f, 0.f, 0.f) : rec[k];
 #pragma unroll
-          for (int i = 0; i < 3; i++) Jn[i] = rec[9 + 3 * q + i];
+          for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
         }
         const bool act = c < ncon && !done;
         float4 fn;
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
         dbg[2] = last_impr;
         for (int c = 0; c < kMaxCon; c++) {
           float f0 = 0.f;
-          if (c < ncon) f0 = c < kResident ? blk[c][ew][7].x : fov[c - kResident][ew].x;
+          if (c < ncon) f0 = c < kResident ? blk[c][ew][kBlkF].x : fov[c - kResident][ew].x;
           dbg[32 + c] = f0;
         }
       }

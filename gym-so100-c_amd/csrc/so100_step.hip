@@ -27,7 +27,6 @@ struct __attribute__((aligned(16))) ConGeom {    // per-contact geometry (collis
   float frame[12];     // normal (geom1 -> geom2), tangent1, tangent2
 };
 union ConSlot {
-  ConSolve s;
   ConGeom g;
 };
 struct __attribute__((aligned(16))) SerialScratch {   // per-body arrays of the 6-link chain
@@ -847,52 +846,6 @@ DEV void make_frame(float* f) {
   cross3(f + 6, n, t1);
 }
 
-// ------------------------------------------------------------------ QCQP (MuJoCo mju_QCQP3 restated)
-DEV void qcqp3(float* x, const float A0[3][3], const float* b0, const float* dd, float r) {
-  float A[3][3], b[3], y[3] = {0.f, 0.f, 0.f}, la = 0.f;
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    b[i] = b0[i] * dd[i];
-#pragma unroll
-    for (int j = 0; j < 3; j++) A[i][j] = A0[i][j] * dd[i] * dd[j];
-  }
-  for (int it = 0; it < 20; it++) {
-    float P[3][3], Pi[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) P[i][j] = A[i][j] + (i == j ? la : 0.f);
-    Pi[0][0] = P[1][1] * P[2][2] - P[1][2] * P[2][1];
-    Pi[0][1] = P[0][2] * P[2][1] - P[0][1] * P[2][2];
-    Pi[0][2] = P[0][1] * P[1][2] - P[0][2] * P[1][1];
-    Pi[1][0] = P[1][2] * P[2][0] - P[1][0] * P[2][2];
-    Pi[1][1] = P[0][0] * P[2][2] - P[0][2] * P[2][0];
-    Pi[1][2] = P[0][2] * P[1][0] - P[0][0] * P[1][2];
-    Pi[2][0] = P[1][0] * P[2][1] - P[1][1] * P[2][0];
-    Pi[2][1] = P[0][1] * P[2][0] - P[0][0] * P[2][1];
-    Pi[2][2] = P[0][0] * P[1][1] - P[0][1] * P[1][0];
-    float det = P[0][0] * Pi[0][0] + P[0][1] * Pi[1][0] + P[0][2] * Pi[2][0];
-    if (det < kMinVal) { x[0] = x[1] = x[2] = 0.f; return; }
-    float id = 1.f / det;
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) Pi[i][j] *= id;
-#pragma unroll
-    for (int i = 0; i < 3; i++) y[i] = -(Pi[i][0] * b[0] + Pi[i][1] * b[1] + Pi[i][2] * b[2]);
-    float val = y[0] * y[0] + y[1] * y[1] + y[2] * y[2] - r * r;
-    if (val < 1e-10f) break;
-    float deriv = 0.f;
-#pragma unroll
-    for (int i = 0; i < 3; i++) deriv += y[i] * (Pi[i][0] * y[0] + Pi[i][1] * y[1] + Pi[i][2] * y[2]);
-    deriv *= -2.f;
-    float delta = -val / deriv;
-    if (delta < 1e-10f) break;
-    la += delta;
-  }
-  x[0] = y[0] * dd[0]; x[1] = y[1] * dd[1]; x[2] = y[2] * dd[2];
-}
-
 // ------------------------------------------------------------------ row broadcast (DPP row_newbcast, gfx90a+)
 template <int L>
 DEV float bcast_row_c(float v) { return dpp<0x150 + L>(v); }
@@ -969,25 +922,6 @@ DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int 
   }
   return make_float4(fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2], fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2],
                      fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2], fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2]);
-}
-
-// 3x3 inverse by adjugate (det <= kMinVal -> zero matrix, the QCQP then returns 0 like the oracle)
-DEV void inv3(float Pi[3][3], const float P[3][3]) {
-  Pi[0][0] = P[1][1] * P[2][2] - P[1][2] * P[2][1];
-  Pi[0][1] = P[0][2] * P[2][1] - P[0][1] * P[2][2];
-  Pi[0][2] = P[0][1] * P[1][2] - P[0][2] * P[1][1];
-  Pi[1][0] = P[1][2] * P[2][0] - P[1][0] * P[2][2];
-  Pi[1][1] = P[0][0] * P[2][2] - P[0][2] * P[2][0];
-  Pi[1][2] = P[0][2] * P[1][0] - P[0][0] * P[1][2];
-  Pi[2][0] = P[1][0] * P[2][1] - P[1][1] * P[2][0];
-  Pi[2][1] = P[0][1] * P[2][0] - P[0][0] * P[2][1];
-  Pi[2][2] = P[0][0] * P[1][1] - P[0][1] * P[1][0];
-  const float det = P[0][0] * Pi[0][0] + P[0][1] * Pi[1][0] + P[0][2] * Pi[2][0];
-  const float id = det > kMinVal ? 1.f / det : 0.f;
-#pragma unroll
-  for (int i = 0; i < 3; i++)
-#pragma unroll
-    for (int j = 0; j < 3; j++) Pi[i][j] *= id;
 }
 
 // Symmetric 3x3 eigen-decomposition by cyclic Jacobi (5 sweeps: quadratic convergence reaches fp32
@@ -1243,7 +1177,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
         float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c < ncon && lane < SO100_NV) {
           J = contact_jac(m, sh, c, lane);
-          reinterpret_cast<float4*>(crec + c * kConRec + 36)[lane] = J;
+          reinterpret_cast<float4*>(crec + c * kConRec + kJOff)[lane] = J;
         }
         Jr[c] = J;
         const float4 M = minv_times(J, minv_row, invmc, lane);   // M^-1 J' column of this dof
@@ -1320,16 +1254,22 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
 #pragma unroll
         for (int b2 = 0; b2 < 3; b2++) As[a][b2] = A11[a][b2] * mus[a] * mus[b2];
       eig3_sym(As, lam, Qe);
-      // ConSolve layout (so100_common.h), f written after the warmstart decision
+      // solver block (layout: so100_device.h), f written after the warmstart decision
+      float P[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) P[i][j] = Qe[j][i] * mus[j];
       float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
       cs[0] = make_float4(ar[0], ar[1], ar[2], ar[3]);
       cs[1] = make_float4(ar[4], ar[5], ar[6], ar[7]);
-      cs[2] = make_float4(ar[8], ar[9], Qe[0][0], Qe[0][1]);
-      cs[3] = make_float4(Qe[0][2], Qe[1][0], Qe[1][1], Qe[1][2]);
-      cs[4] = make_float4(Qe[2][0], Qe[2][1], Qe[2][2], lam[0]);
-      cs[5] = make_float4(lam[1], lam[2], R[0], 1.f / ar[0]);
-      cs[6] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-      cs[8] = make_float4(mu0, mu1, R[1], R[3]);
+      cs[2] = make_float4(ar[8], ar[9], P[0][0], P[0][1]);
+      cs[3] = make_float4(P[0][2], P[1][0], P[1][1], P[1][2]);
+      cs[4] = make_float4(P[2][0], P[2][1], P[2][2], lam[0]);
+      cs[5] = make_float4(lam[1], lam[2], 1.f / lam[0], 1.f / lam[1]);
+      cs[6] = make_float4(1.f / lam[2], R[0], 1.f / ar[0], R[1]);
+      cs[7] = make_float4(R[3], 0.f, 0.f, 0.f);
+      cs[kBlkAref] = make_float4(aref[0], aref[1], aref[2], aref[3]);
 #pragma unroll
       for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
     }
@@ -1360,7 +1300,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
     } else {
       qacc_c += dq;
     }
-    if (lane < ncon) reinterpret_cast<float4*>(crec + lane * kConRec)[7] = make_float4(cf[0], cf[1], cf[2], cf[3]);
+    if (lane < ncon) reinterpret_cast<float4*>(crec + lane * kConRec)[kBlkF] = make_float4(cf[0], cf[1], cf[2], cf[3]);
 
     // ---------------- solver record -> HBM (consumed by so100_pgs_kernel)
     if (valid) {
