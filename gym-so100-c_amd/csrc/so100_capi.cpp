@@ -14,7 +14,7 @@
 #include "so100_device.h"
 
 namespace so100 {
-hipError_t launch_step(const DevModel*, int, const Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
+hipError_t launch_step(const DevModel*, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
                        hipStream_t);
 hipError_t alloc_workspace(int, Workspace*);
 hipError_t free_workspace(Workspace*);

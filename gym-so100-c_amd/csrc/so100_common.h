@@ -67,7 +67,7 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
   float s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   if (live && s - r * r >= 1e-10f) {
     const float rinv = __builtin_amdgcn_rcpf(r);
-    const float cn = sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const float cn = __builtin_amdgcn_sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);   // raw v_sqrt (1 ulp)
     float la = fmaxf(0.f, cn * rinv - fmaxf(lam[0], fmaxf(lam[1], lam[2])));
 #pragma unroll
     for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
@@ -77,7 +77,7 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
       nit++;
       // d|y|^2/dla = -2 sum w_i^2 d_i;  Newton on g = 1/|y|: delta = (1/r - g) / g' = s (|y|/r - 1) / t
       const float t = w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2];
-      const float delta = s * (sqrtf(s) * rinv - 1.f) * __builtin_amdgcn_rcpf(t);
+      const float delta = s * (__builtin_amdgcn_sqrtf(s) * rinv - 1.f) * __builtin_amdgcn_rcpf(t);
       if (delta < 1e-10f || delta <= 4e-7f * la) break;
       la += delta;
 #pragma unroll

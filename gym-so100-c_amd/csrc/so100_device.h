@@ -113,9 +113,18 @@ enum HdrField : int {
   H_NCON = 39,      // contact count (int bits)
 };
 static_assert(H_NCON + 1 == kHdrLane && kHdrLane % 4 == 0 && kConRec % 4 == 0, "workspace record layout");
+constexpr int kPgsEnvs = 16;      // solver: envs per wave64 (4 lanes each) = one "group"
+constexpr int kResident = 4;      // solver: contacts per env held on-chip across the sweeps
+constexpr int kHeavyCap = 512;    // solver: groups with > kResident contacts dispatched first (cap)
 struct Workspace {
   float* hdr;
   float* con;
+  // heavy-group list, double-buffered by substep parity: the stage kernel flags/list groups holding an
+  // env with more than kResident contacts, the solver dispatches those first and clears the other set
+  uint32_t* gflag;  // [2][ngroups]  1 = listed, 3 = heavy but over the cap (solved in place)
+  int* hcount;      // [2]
+  int* hlist;       // [2][kHeavyCap]
+  uint32_t sub_count;   // host-side substep counter (parity)
 };
 
 }  // namespace so100

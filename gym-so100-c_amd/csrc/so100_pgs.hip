@@ -17,8 +17,6 @@
 
 namespace so100 {
 
-constexpr int kPgsEnvs = 16;     // envs per wave64 (4 lanes each)
-constexpr int kResident = 4;     // contacts per env held on-chip across the sweeps
 #ifndef SO100_PGS_WAVES
 #define SO100_PGS_WAVES 2        // waves per SIMD the register budget is sized for
 #endif
@@ -30,6 +28,8 @@ struct PgsArgs {
   float* debug;
   int n;
   int last;                      // last substep of the env step: write the debug record
+  int par;                       // substep parity (heavy-group list set)
+  int nheavy_slots;              // leading blocks reserved for heavy groups
 };
 
 // One contact block (elliptic cone, condim 4) of a sweep: normal row by projection, then the friction
@@ -99,7 +99,23 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
   const int tid = threadIdx.x;
   const int q = tid & 3;
   const int ew = tid >> 2;
-  const int env = blockIdx.x * kPgsEnvs + ew;
+  // groups holding an env with many contacts take longest: they run in the leading blocks so their
+  // tail overlaps the bulk; the in-place block of a listed group exits
+  const int ngroups = (a.n + kPgsEnvs - 1) / kPgsEnvs;
+  int grp;
+  if ((int)blockIdx.x < a.nheavy_slots) {
+    const int cnt = min(a.w.hcount[a.par], kHeavyCap);
+    if ((int)blockIdx.x >= cnt) return;
+    grp = a.w.hlist[a.par * kHeavyCap + blockIdx.x];
+  } else {
+    grp = blockIdx.x - a.nheavy_slots;
+    if (tid == 0) {
+      a.w.gflag[(a.par ^ 1) * ngroups + grp] = 0u;      // reset the set the next stage kernel fills
+      if (grp == 0) a.w.hcount[a.par ^ 1] = 0;
+    }
+    if (a.w.gflag[a.par * ngroups + grp] == 1u) return;
+  }
+  const int env = grp * kPgsEnvs + ew;
   const bool valid = env < a.n;
   const int e = valid ? env : 0;
   STAMP_DECL
@@ -202,7 +218,7 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
         const float lim_AR = mrow[k][k] + lim_R;
         const bool own = (q == j / 3) && lim_on[k] && !done;
         const float res = lim_s * qacc[k] - lim_aref + lim_R * lim_f[k];
-        const float fn = fmaxf(lim_f[k] - res / lim_AR, 0.f);
+        const float fn = fmaxf(lim_f[k] - res * __builtin_amdgcn_rcpf(lim_AR), 0.f);
         float dlt = own ? fn - lim_f[k] : 0.f;
         lim_f[k] += dlt;
         impr -= dlt * (res + 0.5f * lim_AR * dlt);
@@ -277,7 +293,7 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     if (a.last && a.debug && tid == 0) {
-      float* dbg = a.debug + (size_t)(blockIdx.x * kPgsEnvs) * SO100_DBG_STRIDE;   // record of the wave's first env
+      float* dbg = a.debug + (size_t)(grp * kPgsEnvs) * SO100_DBG_STRIDE;   // record of the wave's first env
       dbg[92] = __uint_as_float((uint32_t)tl_start);
       dbg[93] = __uint_as_float((uint32_t)tl_end);
       dbg[94] = __uint_as_float(hw);
@@ -314,10 +330,12 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
   }
 }
 
-hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
+hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last, int par,
                       hipStream_t s) {
-  PgsArgs a{m, w, qacc_out, debug, n, last};
-  hipLaunchKernelGGL(so100_pgs_kernel, dim3((n + kPgsEnvs - 1) / kPgsEnvs), dim3(64), 0, s, a);
+  const int ngroups = (n + kPgsEnvs - 1) / kPgsEnvs;
+  const int heavy = ngroups < kHeavyCap ? ngroups : kHeavyCap;
+  PgsArgs a{m, w, qacc_out, debug, n, last, par, heavy};
+  hipLaunchKernelGGL(so100_pgs_kernel, dim3(ngroups + heavy), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

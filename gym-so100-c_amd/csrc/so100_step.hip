@@ -978,6 +978,7 @@ struct StageArgs {
   uint64_t base_seed;
   int env_offset;
   int sub;             // substep index (kMode 2: nsubstep)
+  int par;             // substep parity (heavy-group list set)
 };
 
 DEV int wave_max_i(int v) {
@@ -1117,6 +1118,16 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
     __syncthreads();
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
+    if (lane == 0 && ncon > kResident) {
+      // this env's solver group is heavy: list it once for first dispatch (so100_pgs.hip)
+      const int g = env / kPgsEnvs, ngroups = (args.n + kPgsEnvs - 1) / kPgsEnvs;
+      uint32_t* fl = args.w.gflag + args.par * ngroups + g;
+      if (atomicOr(fl, 1u) == 0u) {
+        const int idx = atomicAdd(args.w.hcount + args.par, 1);
+        if (idx < kHeavyCap) args.w.hlist[args.par * kHeavyCap + idx] = g;
+        else atomicOr(fl, 2u);
+      }
+    }
     float* const crec = args.w.con + (size_t)e * kMaxCon * kConRec;
 
     // ---------------- S4/S5: M^-1 rows, frictionloss and joint-limit rows (lane = dof)
@@ -1557,25 +1568,27 @@ __global__ void so100_goal_reward_kernel(const DevModel* m, int n, const float* 
 }
 
 // ------------------------------------------------------------------ launchers (called by so100_capi.cpp)
-hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
+hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last, int par,
                       hipStream_t s);
 
 
 // One env step = nsubstep x (stage, solve) + the final stage: 2 * nsubstep + 1 launches on one stream.
-hipError_t launch_step(const DevModel* m, int nsubstep, const Workspace& w, const so100_buffers& b, int n, int task,
+hipError_t launch_step(const DevModel* m, int nsubstep, Workspace& w, const so100_buffers& b, int n, int task,
                        int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s) {
-  StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0};
+  StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0, 0};
   const dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
   for (int sub = 0; sub <= nsubstep; sub++) {
     a.sub = sub;
+    a.par = (int)(w.sub_count & 1u);
     if (sub == 0) hipLaunchKernelGGL(so100_stage_kernel<0>, grid, dim3(kThreads), 0, s, a);
     else if (sub < nsubstep) hipLaunchKernelGGL(so100_stage_kernel<1>, grid, dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL(so100_stage_kernel<2>, grid, dim3(kThreads), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (sub < nsubstep) {
-      e = launch_pgs(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, s);
+      e = launch_pgs(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, a.par, s);
       if (e != hipSuccess) return e;
+      w.sub_count++;
     }
   }
   return hipSuccess;
@@ -1583,21 +1596,28 @@ hipError_t launch_step(const DevModel* m, int nsubstep, const Workspace& w, cons
 
 hipError_t free_workspace(Workspace* w);
 hipError_t alloc_workspace(int n, Workspace* w) {
-  w->hdr = nullptr;
-  w->con = nullptr;
+  *w = Workspace{};
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kMaxCon * kConRec * sizeof(float));
+  const size_t ngroups = (size_t)(n + kPgsEnvs - 1) / kPgsEnvs;
+  if (e == hipSuccess) e = hipMalloc(&w->gflag, 2 * ngroups * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&w->hcount, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&w->hlist, 2 * kHeavyCap * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(w->gflag, 0, 2 * ngroups * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(w->hcount, 0, 2 * sizeof(int));
   if (e != hipSuccess) (void)free_workspace(w);
   return e;
 }
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
-  for (void* p : {(void*)w->hdr, (void*)w->con}) {
+  for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
   }
   w->hdr = w->con = nullptr;
+  w->gflag = nullptr;
+  w->hcount = w->hlist = nullptr;
   return r;
 }
 hipError_t launch_reset(const DevModel* m, const so100_buffers& b, int n, int task, uint64_t base_seed,
