@@ -7,7 +7,8 @@
 
 One "step" = one batched env step of every env on every GPU: action prologue, 10 physics substeps
 (kinematics, CRBA/RNE, box-box contacts, PGS, semi-implicit Euler), the final position stage,
-reward/obs epilogue, TimeLimit + in-kernel auto-reset — one HIP launch per GPU per step.
+reward/obs epilogue, TimeLimit + in-kernel auto-reset — 21 HIP launches per GPU per step (per substep a
+stage kernel and a solver kernel, then the final stage kernel).
 Envs are sharded contiguously (global ids drive the seeds); there is no collective on the data path:
 only the barrier + max-over-ranks timing reduction around the timed region.
 Rank 0 prints ONE JSON line.  See DESIGN.md §6 for the roofline bytes and the CPU baseline.
@@ -22,10 +23,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 
 METRIC = "env steps/sec (whole node), 65k parallel bin-a-cube envs at 1/2/4/8 MI355X"
-# algorithmic HBM bytes per env step: reads action 24 + qpos 52 + qvel 48 + warmstart 48
-# + elapsed 4 + episode 4 = 180; writes qpos 52 + qvel 48 + warmstart 48 + obs 60 + reward 4 +
-# terminated/truncated/success/diverged 4 + contact_bits 4 + elapsed 4 + episode 4 = 228.
+# algorithmic HBM bytes per env step at the boundary: reads action 24 + qpos 52 + qvel 48
+# + warmstart 48 + elapsed 4 + episode 4 = 180; writes qpos 52 + qvel 48 + warmstart 48 + obs 60 + reward 4
+# + terminated/truncated/success/diverged 4 + contact_bits 4 + elapsed 4 + episode 4 = 228.
 BYTES_PER_ENV_STEP = 408
+# dominant kernel = the PGS solver (so100_pgs.hip).  Algorithmic bytes per launch: per env the solver
+# record header (4 lanes x 40 floats = 640 B) read + qacc (48 B) written; per contact the solver block
+# (160 B) + J rows (192 B) read once.
+SOLVER_BYTES_PER_ENV = 640 + 48
+SOLVER_BYTES_PER_CONTACT = 160 + 192
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
@@ -49,6 +55,8 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample duration")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-kernel-timing", action="store_true", help="skip the per-launch HIP events")
+    p.add_argument("--contact-steps", type=int, default=10, help="untimed steps sampling contacts/env")
     return p.parse_args(argv)
 
 
@@ -81,7 +89,7 @@ def cpu_baseline(seconds):
 
 
 def load_traffic(n_envs):
-    """HBM traffic per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    """HBM traffic per solver launch from the committed rocprofv3 PMC pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -133,6 +141,8 @@ def main(argv=None):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    if not args.no_kernel_timing:
+        env.profile_enable(args.steps)      # HIP events on the launch stream around every kernel
     torch.cuda.synchronize(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
@@ -146,11 +156,24 @@ def main(argv=None):
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kernel_ms = ev[0].elapsed_time(ev[1]) / args.steps     # one step kernel per step on this stream
+    step_ms = ev[0].elapsed_time(ev[1]) / args.steps        # device time per env step on this stream
+    solver_ms = stage_ms = float("nan")
+    if not args.no_kernel_timing:
+        s_ms, s_n, t_ms, t_n = env.profile_read()
+        env.profile_enable(0)
+        solver_ms, stage_ms = s_ms / max(s_n, 1), t_ms / max(t_n, 1)
+    # untimed: contacts per env per solver launch (for the solver's algorithmic bytes)
+    accum = torch.zeros(1, dtype=torch.int64, device=dev)
+    for i in range(args.contact_steps):
+        env.set_action_buffer(pool[i % len(pool)])
+        env.step_async_raw()
+        env.contact_count(accum)
+    torch.cuda.synchronize(dev)
+    contacts_per_env = float(accum.item()) / max(1, args.contact_steps * count)
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, step_ms, solver_ms, stage_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed, step_ms, solver_ms, stage_ms = (float(x) for x in t)
 
     # sanity: the state stayed finite
     assert torch.isfinite(env.qpos).all().item(), "non-finite state after the benchmark"
@@ -158,7 +181,8 @@ def main(argv=None):
     if rank == 0:
         env_steps = total * args.steps
         value = env_steps / elapsed
-        achieved = BYTES_PER_ENV_STEP * count / (kernel_ms * 1e-3)
+        solver_bytes = count * (SOLVER_BYTES_PER_ENV + SOLVER_BYTES_PER_CONTACT * contacts_per_env)
+        achieved = solver_bytes / (solver_ms * 1e-3)
         traffic = load_traffic(count)
         line = {
             "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
@@ -171,10 +195,13 @@ def main(argv=None):
                        "pgs_iterations": env.model.iterations, "parallelism": f"env-sharded x{world}, no collectives",
                        "actions": "U[-1,1]^6 pool resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK,
-                         "traffic": traffic,
-                         "kernel_ms": kernel_ms, "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "note": "step kernel is VALU/latency-bound (DESIGN.md §6); HBM fraction reported per north_star"},
+                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "kernel": "so100_pgs_kernel", "kernel_ms": solver_ms,
+                         "bytes_per_launch": solver_bytes, "contacts_per_env": contacts_per_env,
+                         "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
+                         "boundary_bytes_per_env_step": BYTES_PER_ENV_STEP,
+                         "note": ("solver = serial Gauss-Seidel chains per env: issue/latency-bound, not HBM-bound "
+                                  "(DESIGN.md §6); traffic = measured PMC bytes per solver launch")},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -10,12 +10,14 @@
 #include <stdio.h>
 #include <string.h>
 #include <string>
+#include <vector>
 #include "so100.h"
 #include "so100_device.h"
 
 namespace so100 {
 hipError_t launch_step(const DevModel*, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
-                       hipStream_t);
+                       hipStream_t, hipEvent_t*);
+hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
 hipError_t alloc_workspace(int, Workspace*);
 hipError_t free_workspace(Workspace*);
 hipError_t launch_reset(const DevModel*, const so100_buffers&, int, int, uint64_t, int, const uint8_t*, const uint32_t*,
@@ -39,7 +41,16 @@ struct so100_env {
   int max_steps;
   uint64_t base_seed;
   int env_offset;
+  // profiling (so100_profile_enable): events[step][2 nsubstep + 2]
+  std::vector<hipEvent_t> prof_ev;
+  int prof_cap = 0, prof_used = 0;
 };
+
+static void profile_free(so100_env* env) {
+  for (hipEvent_t e : env->prof_ev) (void)hipEventDestroy(e);
+  env->prof_ev.clear();
+  env->prof_cap = env->prof_used = 0;
+}
 
 static thread_local std::string g_err;
 
@@ -247,13 +258,14 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   Workspace ws;
   e = so100::alloc_workspace(n_envs, &ws);
   if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: workspace hipMalloc", e); return nullptr; }
-  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, ws, SO100_TASK_CUBE_TO_BIN, 700, 0, 0};
+  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, ws, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
   return env;
 }
 
 int so100_destroy(so100_env* env) {
   if (!env) return 0;
   DeviceGuard g(env->device);
+  profile_free(env);
   hipError_t e = hipFree(env->d_model);
   hipError_t e2 = so100::free_workspace(&env->ws);
   if (e == hipSuccess) e = e2;
@@ -298,9 +310,57 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
   if ((flags & SO100_FLAG_DR) && !b->dr_params) return fail("so100_step: FLAG_DR needs dr_params");
   if ((flags & SO100_FLAG_AUTORESET) && !b->episode) return fail("so100_step: FLAG_AUTORESET needs episode");
   DeviceGuard g(env->device);
-  hipError_t e = so100::launch_step(env->d_model, env->nsubstep, env->ws, *b, env->n, env->task, flags, env->max_steps, env->base_seed, env->env_offset,
-                                    (hipStream_t)stream);
+  hipEvent_t* ev = nullptr;
+  const int per = 2 * env->nsubstep + 2;
+  if (env->prof_used < env->prof_cap) ev = env->prof_ev.data() + (size_t)(env->prof_used++) * per;
+  hipError_t e = so100::launch_step(env->d_model, env->nsubstep, env->ws, *b, env->n, env->task, flags, env->max_steps,
+                                    env->base_seed, env->env_offset, (hipStream_t)stream, ev);
   return e == hipSuccess ? 0 : fail_hip("so100_step", e);
+}
+
+int so100_profile_enable(so100_env* env, int max_steps) {
+  if (!env) return fail("so100_profile_enable: env is NULL");
+  if (max_steps < 0) return fail("so100_profile_enable: max_steps < 0");
+  DeviceGuard g(env->device);
+  profile_free(env);
+  const size_t count = (size_t)max_steps * (2 * env->nsubstep + 2);
+  env->prof_ev.resize(count);
+  for (size_t i = 0; i < count; i++) {
+    hipError_t e = hipEventCreate(&env->prof_ev[i]);
+    if (e != hipSuccess) { env->prof_ev.resize(i); profile_free(env); return fail_hip("so100_profile_enable", e); }
+  }
+  env->prof_cap = max_steps;
+  return 0;
+}
+
+int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms, int* stage_launches) {
+  if (!env || !solver_ms || !solver_launches || !stage_ms || !stage_launches) return fail("so100_profile_read: bad arguments");
+  DeviceGuard g(env->device);
+  *solver_ms = *stage_ms = 0.0;
+  *solver_launches = *stage_launches = 0;
+  const int per = 2 * env->nsubstep + 2;
+  if (env->prof_used > 0) {
+    hipError_t e = hipEventSynchronize(env->prof_ev[(size_t)env->prof_used * per - 1]);
+    if (e != hipSuccess) return fail_hip("so100_profile_read", e);
+  }
+  for (int st = 0; st < env->prof_used; st++) {
+    const hipEvent_t* ev = env->prof_ev.data() + (size_t)st * per;
+    for (int k = 0; k + 1 < per; k++) {   // launch order: stage, solver, stage, solver, ..., final stage
+      float ms = 0.f;
+      hipError_t e = hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
+      if (e != hipSuccess) return fail_hip("so100_profile_read", e);
+      if (k & 1) { *solver_ms += ms; (*solver_launches)++; }
+      else { *stage_ms += ms; (*stage_launches)++; }
+    }
+  }
+  return 0;
+}
+
+int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
+  if (!env || !accum) return fail("so100_contact_count: bad arguments");
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_contact_count(env->ws, env->n, accum, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_contact_count", e);
 }
 
 int so100_goal_reward(so100_env* env, int n, const float* a, const float* d, float* out, void* stream) {

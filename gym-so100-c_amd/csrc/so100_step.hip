@@ -1573,10 +1573,13 @@ hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, fl
 
 
 // One env step = nsubstep x (stage, solve) + the final stage: 2 * nsubstep + 1 launches on one stream.
+// ev (optional, profiling): 2 nsubstep + 2 events, recorded before the first launch and after each.
 hipError_t launch_step(const DevModel* m, int nsubstep, Workspace& w, const so100_buffers& b, int n, int task,
-                       int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s) {
+                       int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s, hipEvent_t* ev) {
   StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0, 0};
   const dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
+  int k = 0;
+  if (ev) (void)hipEventRecord(ev[k++], s);
   for (int sub = 0; sub <= nsubstep; sub++) {
     a.sub = sub;
     a.par = (int)(w.sub_count & 1u);
@@ -1585,13 +1588,37 @@ hipError_t launch_step(const DevModel* m, int nsubstep, Workspace& w, const so10
     else hipLaunchKernelGGL(so100_stage_kernel<2>, grid, dim3(kThreads), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (ev) (void)hipEventRecord(ev[k++], s);
     if (sub < nsubstep) {
       e = launch_pgs(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, a.par, s);
       if (e != hipSuccess) return e;
+      if (ev) (void)hipEventRecord(ev[k++], s);
       w.sub_count++;
     }
   }
   return hipSuccess;
+}
+
+// Sum of the contact counts in the solver records of the last substep (H_NCON of lane-0 records).
+__global__ void so100_contact_count_kernel(const float* __restrict__ hdr, int n, unsigned long long* accum) {
+  __shared__ int part[256];
+  int s = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    s += __float_as_int(hdr[(size_t)i * kHdrEnv + H_NCON]);
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 128; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) part[threadIdx.x] += part[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(accum, (unsigned long long)part[0]);
+}
+hipError_t launch_contact_count(const Workspace& w, int n, uint64_t* accum, hipStream_t s) {
+  int blocks = (n + 255) / 256;
+  if (blocks > 256) blocks = 256;
+  hipLaunchKernelGGL(so100_contact_count_kernel, dim3(blocks), dim3(256), 0, s, w.hdr, n,
+                     reinterpret_cast<unsigned long long*>(accum));
+  return hipGetLastError();
 }
 
 hipError_t free_workspace(Workspace* w);

@@ -32,6 +32,9 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
+ABI_VERSION = 2          # include/so100.h SO100_ABI_VERSION
+
+
 def load():
     """Load libso100_hip.so once; raise NativeLibraryError loudly if it is missing or broken."""
     global _lib
@@ -55,12 +58,16 @@ def load():
     lib.so100_eval_reward.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
     lib.so100_spawn_pose.argtypes = [_P, ctypes.c_int, _P, _P, _P]
     lib.so100_unnormalize.argtypes = [_P, ctypes.c_int, _P, _P, _P]
+    lib.so100_profile_enable.argtypes = [_P, ctypes.c_int]
+    lib.so100_profile_read.argtypes = [_P, _P, _P, _P, _P]
+    lib.so100_contact_count.argtypes = [_P, _P, _P]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
-               "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize"):
+               "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
+               "so100_profile_enable", "so100_profile_read", "so100_contact_count"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
     lib.so100_struct_sizes.restype = ctypes.c_int
-    if lib.so100_abi_version() != 1:
+    if lib.so100_abi_version() != ABI_VERSION:
         raise NativeLibraryError("libso100_hip.so ABI mismatch")
     mb, bb = ctypes.c_int(0), ctypes.c_int(0)
     lib.so100_struct_sizes(ctypes.byref(mb), ctypes.byref(bb))
@@ -74,7 +81,8 @@ def load():
 
 EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
-                    "so100_spawn_pose", "so100_unnormalize")
+                    "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
+                    "so100_contact_count")
 
 
 def check(rc, what):

@@ -277,6 +277,23 @@ class SO100VecEnv:
                                                  self._stream()), "so100_unnormalize")
         return out
 
+    # ---------------------------------------------------------------- benchmark instrumentation
+    def profile_enable(self, max_steps):
+        """Record HIP events around every stage/solver launch of the next max_steps steps (0 = off)."""
+        _native.check(self.lib.so100_profile_enable(self._handle, int(max_steps)), "so100_profile_enable")
+
+    def profile_read(self):
+        """(solver_ms, solver_launches, stage_ms, stage_launches) summed since profile_enable; synchronises."""
+        sm, sn, tm, tn = ctypes.c_double(0), ctypes.c_int(0), ctypes.c_double(0), ctypes.c_int(0)
+        _native.check(self.lib.so100_profile_read(self._handle, ctypes.byref(sm), ctypes.byref(sn),
+                                                  ctypes.byref(tm), ctypes.byref(tn)), "so100_profile_read")
+        return sm.value, sn.value, tm.value, tn.value
+
+    def contact_count(self, accum):
+        """accum (int64 device tensor, 1 element) += contacts in the last solver launch, summed over envs."""
+        _native.check(self.lib.so100_contact_count(self._handle, _native.ptr(accum), self._stream()),
+                      "so100_contact_count")
+
     def close(self):
         if getattr(self, "_handle", None):
             self.lib.so100_destroy(self._handle)

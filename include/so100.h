@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 1
+#define SO100_ABI_VERSION 2
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -91,6 +91,19 @@ int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, con
 
 /* One env step for all N envs (10 physics substeps + final position stage + reward/obs epilogue). */
 int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream);
+
+/* Kernel timing for the benchmark's roofline (not needed for stepping).  so100_profile_enable(env,
+ * max_steps) allocates HIP events for up to max_steps subsequent so100_step calls (0 frees them and
+ * stops recording); while enabled each step records an event on its stream before its first launch
+ * and after every launch (stage / solver kernels).  so100_profile_read synchronises on the last event
+ * and returns the summed device time of the solver and of the stage launches since enabling. */
+int so100_profile_enable(so100_env* env, int max_steps);
+int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms,
+                       int* stage_launches);
+
+/* Adds the contact count of the last solver launch, summed over the N envs, to *accum (DEVICE
+ * uint64).  Enqueued on `stream`, no synchronisation. */
+int so100_contact_count(so100_env* env, uint64_t* accum, void* stream);
 
 /* Batched sparse GoalEnv reward (env.py:341-353): out[i] = ||a_i - d_i|| < threshold ? 0 : -1. */
 int so100_goal_reward(so100_env* env, int n, const float* achieved, const float* desired, float* out,
