@@ -21,7 +21,7 @@ reference.  It restates what MuJoCo's compiler does for the parts of
   actuator kv = dampratio * 2 * sqrt(kp * dof_M0).
 
 MuJoCo itself is not available here; these restatements are [3P-unverified] against MuJoCo 3.3.3
-and are re-checked by tools/mujoco_crosscheck.py wherever mujoco is importable.
+(parity unpinned) and are pinned by the analytic tests in tests/test_oracle_physics.py.
 """
 import json
 import math

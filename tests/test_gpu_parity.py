@@ -267,3 +267,52 @@ def test_single_env_api():
     assert r in (0.0, -1.0)
     rb = g.compute_reward(np.zeros((4, 3)), np.zeros((4, 3)) + 0.001, {})
     assert rb.dtype == np.float32 and (rb == 0).all()
+
+
+def test_heavy_contact_parity(model, oracle64, oracle32):
+    """Cube pressed into a bin corner: floor + two walls give up to 12 contacts, beyond the solver's 4
+    on-chip slots — exercises the streamed-overflow contacts and the heavy-group first dispatch."""
+    from gym_so100 import SO100VecEnv
+    n = 32
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True)
+    env.reset(seed=5)
+    rng = np.random.default_rng(7)
+    qpos = env.qpos.cpu().numpy().astype(np.float64)
+    pen = rng.uniform(2e-4, 1e-3, (n, 3))
+    # bin inner faces (assets: bin_wall3 x = -0.14 - 0.005, bin_wall y = 0.76 - 0.005, floor top z = 0.001)
+    qpos[:, 6] = -0.145 - 0.02 + pen[:, 0]
+    qpos[:, 7] = 0.755 - 0.02 + pen[:, 1]
+    qpos[:, 8] = 0.001 + 0.02 - pen[:, 2]
+    ang = rng.uniform(-0.01, 0.01, n)
+    qpos[:, 9:13] = np.stack([np.cos(ang / 2), np.zeros(n), np.zeros(n), np.sin(ang / 2)], 1)
+    qvel = np.zeros((n, 12))
+    qvel[:, 6:9] = rng.normal(0, 0.02, (n, 3))
+    env.set_state(qpos.astype(np.float32), qvel.astype(np.float32), np.zeros((n, 12), np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, ncon = [], [], []
+    for step in range(3):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = rng.uniform(-0.2, 0.2, (n, 6)).astype(np.float32)
+        env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        ncon.append(env.debug.cpu().numpy()[:, 0])
+        for i in range(n):
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(model, d64, 0, act[i])
+            oracle32.env_step(model, d32, 0, act[i])
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+    qv_err, qv_floor, ncon = np.array(qv_err), np.array(qv_floor), np.concatenate(ncon)
+    print(f"\nheavy contacts: GPU ncon mean {ncon.mean():.1f} max {ncon.max():.0f} | qvel rel GPU median "
+          f"{np.median(qv_err):.2e} p90 {np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median "
+          f"{np.median(qv_floor):.2e} p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
+    assert (ncon > 4).mean() > 0.5                      # the overflow path is really exercised
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    env.close()
