@@ -94,8 +94,10 @@ constexpr int kHdrEnv = 4 * kHdrLane;
 // Solver block of one contact, read by the PGS as kBlk x ds_read_b128 (float index: content):
 //   0-9  A+R upper triangle 00 01 02 03 11 12 13 22 23 33     10-18  P = Q' D (row-major)
 //   19-21 lam (eigenvalues of D A11 D = Q diag(lam) Q')       22-24  1 / lam
-//   25 R0   26 1/(A+R)00   27 R1 (= R2)   28 R3   29-31 pad  32-35 aref   36-39 f (normal, t1, t2, torsion)
+//   25 R0   26 1/(A+R)00   27 R1 (= R2)   28 R3   29 1 if a gripper-pad contact (J has arm entries) else 0
+//   30-31 pad  32-35 aref   36-39 f (normal, t1, t2, torsion)
 constexpr int kBlk = 10;
+constexpr int kBlkFlags = 7;      // float4 slot holding R3 (x) and the arm flag (y)
 constexpr int kBlkAref = 8;       // float4 slots
 constexpr int kBlkF = 9;
 constexpr int kJOff = 4 * kBlk;   // float offset of the J rows in the record

@@ -38,7 +38,7 @@ struct PgsArgs {
 // block and `active` selects the result, so the block's LDS reads issue together at the top instead of
 // being sunk into branches (three serialised LDS round trips per contact otherwise).
 DEV void contact_update(const float4 (&v)[kBlk], const float4 (&J)[3], float (&qacc)[3], const float (&mrow)[3][6],
-                        bool active, bool lead, float& impr, float4& fout, int& newton) {
+                        bool active, bool lead, bool arm, float& impr, float4& fout, int& newton) {
   const float j0 = quadsum(J[0].x * qacc[0] + J[1].x * qacc[1] + J[2].x * qacc[2]);
   const float j1 = quadsum(J[0].y * qacc[0] + J[1].y * qacc[1] + J[2].y * qacc[2]);
   const float j2 = quadsum(J[0].z * qacc[0] + J[1].z * qacc[1] + J[2].z * qacc[2]);
@@ -84,12 +84,20 @@ DEV void contact_update(const float4 (&v)[kBlk], const float4 (&J)[3], float (&q
   float g[3], gp[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) g[i] = (J[i].x * dl[0] + J[i].y * dl[1]) + (J[i].z * dl[2] + J[i].w * dl[3]);
+  if (!arm) {
+    // cube-only contact (table / bin): J has no arm entries, the arm lanes' g is 0 and the cube block
+    // of M^-1 is diagonal: the full update below reduces to this exactly
+#pragma unroll
+    for (int i = 0; i < 3; i++) qacc[i] += mrow[i][i] * g[i];
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 3; i++) gp[i] = quad_swap1(g[i]);
 #pragma unroll
   for (int i = 0; i < 3; i++)
     qacc[i] += (mrow[i][0] * g[0] + mrow[i][1] * g[1] + mrow[i][2] * g[2]) +
                (mrow[i][3] * gp[0] + mrow[i][4] * gp[1] + mrow[i][5] * gp[2]);
+
 }
 
 __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs a) {
@@ -106,6 +114,9 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
   if ((int)blockIdx.x < a.nheavy_slots) {
     const int cnt = min(a.w.hcount[a.par], kHeavyCap);
     if ((int)blockIdx.x >= cnt) return;
+#ifdef SO100_EXPERIMENT_SKIP_HEAVY
+    return;   // timing experiment only: heavy groups left unsolved
+#endif
     grp = a.w.hlist[a.par * kHeavyCap + blockIdx.x];
   } else {
     grp = blockIdx.x - a.nheavy_slots;
@@ -168,20 +179,31 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
   const int iterations = m->iterations;
   const float tolerance = m->tolerance, pgs_scale = m->pgs_scale;
 
-  // every env owns kMaxCon record slots: loads of slots >= ncon are in bounds (stale, never used)
+  // every env owns kMaxCon record slots: loads of slots >= ncon are in bounds but stale (or never
+  // written); J of such slots is zeroed so that masked lanes contribute exactly 0 to g = J d
   float* const crec = a.w.con + (size_t)e * kMaxCon * kConRec;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 J[kResident][3];
 #pragma unroll
   for (int c = 0; c < kResident; c++) {
     const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
 #pragma unroll
-    for (int i = 0; i < 3; i++) J[c][i] = rec[kBlk + 3 * q + i];
+    for (int i = 0; i < 3; i++) {
+      const float4 t = rec[kBlk + 3 * q + i];
+      J[c][i] = c < ncon ? t : zero4;
+    }
     blk[c][ew][q] = rec[q];
     blk[c][ew][q + 4] = rec[q + 4];
     if (q < 2) blk[c][ew][q + 8] = rec[q + 8];
   }
   for (int c = kResident + q; c < ncon_max; c += 4)
     fov[c - kResident][ew] = reinterpret_cast<const float4*>(crec + c * kConRec)[kBlkF];
+  __syncthreads();
+  // resident contact slots in which some env of the wave has a gripper contact (J with arm entries)
+  uint32_t arm_res = 0;
+#pragma unroll
+  for (int c = 0; c < kResident; c++)
+    arm_res |= (__ballot(valid && c < ncon && blk[c][ew][kBlkFlags].y != 0.f) != 0ull) ? (1u << c) : 0u;
   __syncthreads();
 
   STAMP(0);
@@ -238,7 +260,7 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
         for (int k = 0; k < kBlk; k++) v[k] = blk[c][ew][k];
         float4 fn;
         const bool act = c < ncon && !done;
-        contact_update(v, J[c], qacc, mrow, act, q == 0, impr, fn, newton);
+        contact_update(v, J[c], qacc, mrow, act, q == 0, (arm_res >> c) & 1u, impr, fn, newton);
         if (act) blk[c][ew][kBlkF] = fn;
       }
     }
@@ -259,7 +281,7 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
 #pragma unroll
         for (int k = 0; k < kBlk; k++) v[k] = vn[k];
 #pragma unroll
-        for (int i = 0; i < 3; i++) Jo[i] = Jn[i];
+        for (int i = 0; i < 3; i++) Jo[i] = c < ncon ? Jn[i] : zero4;
         v[kBlkF] = fov[c - kResident][ew];
         if (c + 1 < ncon_max) {
           const float4* rec = reinterpret_cast<const float4*>(crec + (c + 1) * kConRec);
@@ -269,8 +291,9 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
           for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
         }
         const bool act = c < ncon && !done;
+        const bool arm = __ballot(c < ncon && v[kBlkFlags].y != 0.f) != 0ull;
         float4 fn;
-        contact_update(v, Jo, qacc, mrow, act, q == 0, impr, fn, newton);
+        contact_update(v, Jo, qacc, mrow, act, q == 0, arm, impr, fn, newton);
         if (act) fov[c - kResident][ew] = fn;
       }
     }

@@ -1279,7 +1279,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
       cs[4] = make_float4(P[2][0], P[2][1], P[2][2], lam[0]);
       cs[5] = make_float4(lam[1], lam[2], 1.f / lam[0], 1.f / lam[1]);
       cs[6] = make_float4(1.f / lam[2], R[0], 1.f / ar[0], R[1]);
-      cs[7] = make_float4(R[3], 0.f, 0.f, 0.f);
+      cs[kBlkFlags] = make_float4(R[3], p < SO100_NPAIR_GRIPPER ? 1.f : 0.f, 0.f, 0.f);
       cs[kBlkAref] = make_float4(aref[0], aref[1], aref[2], aref[3]);
 #pragma unroll
       for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
@@ -1626,6 +1626,9 @@ hipError_t alloc_workspace(int n, Workspace* w) {
   *w = Workspace{};
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kMaxCon * kConRec * sizeof(float));
+  // zero once: record slots a solver lane reads but never uses are then finite, never garbage
+  if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(w->con, 0, (size_t)n * kMaxCon * kConRec * sizeof(float));
   const size_t ngroups = (size_t)(n + kPgsEnvs - 1) / kPgsEnvs;
   if (e == hipSuccess) e = hipMalloc(&w->gflag, 2 * ngroups * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->hcount, 2 * sizeof(int));
