@@ -612,6 +612,22 @@ DEV void cull_points8(const Poly8& p, int mm, int i0, int* iret) {
   }
 }
 
+// Runtime-indexed reads of small register arrays as masked blends a0 w0 + a1 w1 + a2 w2 (one weight 1,
+// exact for finite values).  A pointer, a dynamic index, or a select chain (which the compiler folds back
+// into an index) would force the array into scratch memory.
+DEV void onehot3(int i, float* w) { w[0] = i == 0 ? 1.f : 0.f; w[1] = i == 1 ? 1.f : 0.f; w[2] = i == 2 ? 1.f : 0.f; }
+DEV float sel3(const float* a, int i) {
+  float w[3];
+  onehot3(i, w);
+  return a[0] * w[0] + a[1] * w[1] + a[2] * w[2];
+}
+DEV void col3(float* o, const float* R, int c) {          // column c of a row-major 3x3
+  float w[3];
+  onehot3(c, w);
+#pragma unroll
+  for (int t = 0; t < 3; t++) o[t] = R[3 * t] * w[0] + R[3 * t + 1] * w[1] + R[3 * t + 2] * w[2];
+}
+
 DEV void box_box(const float* p1, const float* R1, const float* A, const float* p2, const float* R2,
                  const float* B, float margin, PairContacts& out) {
   out.n = 0;
@@ -671,19 +687,24 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   if (code > 6) {
     const int i = (code - 7) / 3, j = (code - 7) % 3;
     float pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+#pragma unroll
     for (int k = 0; k < 3; k++) {
-      if (k != i) {
+      {
         float ax[3] = {R1[k], R1[3 + k], R1[6 + k]};
-        float sg = dot3(normal, ax) > 0 ? 1.f : -1.f;
+        float sg = k == i ? 0.f : (dot3(normal, ax) > 0 ? 1.f : -1.f);
+#pragma unroll
         for (int t = 0; t < 3; t++) pa[t] += sg * A[k] * ax[t];
       }
-      if (k != j) {
+      {
         float ax[3] = {R2[k], R2[3 + k], R2[6 + k]};
-        float sg = dot3(normal, ax) > 0 ? -1.f : 1.f;
+        float sg = k == j ? 0.f : (dot3(normal, ax) > 0 ? -1.f : 1.f);
+#pragma unroll
         for (int t = 0; t < 3; t++) pb[t] += sg * B[k] * ax[t];
       }
     }
-    float ua[3] = {R1[i], R1[3 + i], R1[6 + i]}, ub[3] = {R2[j], R2[3 + j], R2[6 + j]};
+    float ua[3], ub[3];
+    col3(ua, R1, i);
+    col3(ub, R2, j);
     float pq[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
     float uaub = dot3(ua, ub), q1 = dot3(ua, pq), q2 = -dot3(ub, pq);
     float den = 1.f - uaub * uaub, al = 0.f, be = 0.f;
@@ -698,32 +719,42 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
     return;
   }
 
-  const float *pR, *RR, *SR, *pI, *RI, *SI;
-  float nref[3];
-  int codeN;
-  if (code <= 3) {
-    pR = p1; RR = R1; SR = A; pI = p2; RI = R2; SI = B; codeN = code - 1;
-    nref[0] = normal[0]; nref[1] = normal[1]; nref[2] = normal[2];
-  } else {
-    pR = p2; RR = R2; SR = B; pI = p1; RI = R1; SI = A; codeN = code - 4;
-    nref[0] = -normal[0]; nref[1] = -normal[1]; nref[2] = -normal[2];
+  // reference box (face normal) and incident box, selected by value (no pointer / dynamic index)
+  const bool ref1 = code <= 3;
+  float pR[3], RR[9], SR[3], pI[3], RI[9], SI[3], nref[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    pR[k] = ref1 ? p1[k] : p2[k]; pI[k] = ref1 ? p2[k] : p1[k];
+    SR[k] = ref1 ? A[k] : B[k];   SI[k] = ref1 ? B[k] : A[k];
+    nref[k] = ref1 ? normal[k] : -normal[k];
   }
+#pragma unroll
+  for (int k = 0; k < 9; k++) { RR[k] = ref1 ? R1[k] : R2[k]; RI[k] = ref1 ? R2[k] : R1[k]; }
+  const int codeN = ref1 ? code - 1 : code - 4;
   float nr[3], anr[3];
+#pragma unroll
   for (int k = 0; k < 3; k++) {
     float ax[3] = {RI[k], RI[3 + k], RI[6 + k]};
     nr[k] = dot3(nref, ax);
     anr[k] = fabsf(nr[k]);
   }
   int lanr = (anr[1] > anr[0]) ? ((anr[1] > anr[2]) ? 1 : 2) : ((anr[0] > anr[2]) ? 0 : 2);
-  float center[3];
-  for (int t = 0; t < 3; t++) center[t] = pI[t] - pR[t] + (nr[lanr] < 0 ? SI[lanr] : -SI[lanr]) * RI[3 * t + lanr];
+  float center[3], ril[3];
+  col3(ril, RI, lanr);
+  const float sil = sel3(SI, lanr), nrl = sel3(nr, lanr);
+#pragma unroll
+  for (int t = 0; t < 3; t++) center[t] = pI[t] - pR[t] + (nrl < 0 ? sil : -sil) * ril[t];
   const int c1 = (codeN == 0) ? 1 : 0, c2 = (codeN == 2) ? 1 : 2;
   const int a1 = (lanr == 0) ? 1 : 0, a2 = (lanr == 2) ? 1 : 2;
-  float u1[3] = {RR[c1], RR[3 + c1], RR[6 + c1]}, u2[3] = {RR[c2], RR[3 + c2], RR[6 + c2]};
-  float v1[3] = {RI[a1], RI[3 + a1], RI[6 + a1]}, v2[3] = {RI[a2], RI[3 + a2], RI[6 + a2]};
+  float u1[3], u2[3], v1[3], v2[3];
+  col3(u1, RR, c1);
+  col3(u2, RR, c2);
+  col3(v1, RI, a1);
+  col3(v2, RI, a2);
   float cc1 = dot3(center, u1), cc2 = dot3(center, u2);
   float m11 = dot3(u1, v1), m12 = dot3(u1, v2), m21 = dot3(u2, v1), m22 = dot3(u2, v2);
-  float k1 = m11 * SI[a1], k2 = m21 * SI[a1], k3 = m12 * SI[a2], k4 = m22 * SI[a2];
+  const float sia1 = sel3(SI, a1), sia2 = sel3(SI, a2);
+  float k1 = m11 * sia1, k2 = m21 * sia1, k3 = m12 * sia2, k4 = m22 * sia2;
   Poly8 P, Pq;
   P.n = 4;
   P.x[0] = cc1 - k1 - k3; P.y[0] = cc2 - k2 - k4;
@@ -732,10 +763,11 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   P.x[3] = cc1 + k1 - k3; P.y[3] = cc2 + k2 - k4;
 #pragma unroll
   for (int k = 4; k < 8; k++) { P.x[k] = 0.f; P.y[k] = 0.f; }
-  clip_stage(P, Pq, 0, -1.f, SR[c1]);
-  clip_stage(Pq, P, 0, 1.f, SR[c1]);
-  clip_stage(P, Pq, 1, -1.f, SR[c2]);
-  clip_stage(Pq, P, 1, 1.f, SR[c2]);
+  const float src1 = sel3(SR, c1), src2 = sel3(SR, c2), srcN = sel3(SR, codeN);
+  clip_stage(P, Pq, 0, -1.f, src1);
+  clip_stage(Pq, P, 0, 1.f, src1);
+  clip_stage(P, Pq, 1, -1.f, src2);
+  clip_stage(Pq, P, 1, 1.f, src2);
   const int n = P.n;
   if (n < 1) return;
   float det = m11 * m22 - m12 * m21;
@@ -755,7 +787,7 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
       const float s1 = i11 * x + i12 * y, s2 = i21 * x + i22 * y;
       float pt[3];
       for (int t = 0; t < 3; t++) pt[t] = center[t] + s1 * v1[t] + s2 * v2[t];
-      const float dp = SR[codeN] - dot3(nref, pt);
+      const float dp = srcN - dot3(nref, pt);
       if (dp > -margin) {
 #pragma unroll
         for (int q2 = 0; q2 < 8; q2++) D[q2] = (q2 == K.n) ? dp : D[q2];
@@ -1016,6 +1048,24 @@ DEV void write_obs(const DevModel* __restrict__ m, const EnvShared& sh, int lane
   if (lane < SO100_NOBS) dst[lane] = v;
 }
 
+// Diagnostic build only (-DSO100_STAGE_STAMPS): per-phase cycle attribution of the stage kernel
+// (substep nsubstep-1, mode 1), written to debug[88..93].
+#ifdef SO100_STAGE_STAMPS
+#define SSTAMP_DECL unsigned long long sst_prev_ = 0, sst_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SSTAMP(slot)                                                                             \
+  do {                                                                                           \
+    unsigned long long t_;                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if ((slot) >= 0) sst_acc_[(slot) & 7] += t_ - sst_prev_;                                     \
+    sst_prev_ = t_;                                                                              \
+  } while (0)
+#else
+#define SSTAMP_DECL
+#define SSTAMP(slot) do {} while (0)
+#endif
+
 // Euler (mj_Euler) of the previous substep on the state held in registers: qvel += h qacc, then qpos
 // with the new qvel; the cube quaternion by the exponential map (lanes 9..12, staged through LDS).
 DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_r, float& qvel_r) {
@@ -1046,7 +1096,10 @@ DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_
 //   kMode 2: Euler, then the mj_step1 position stage and the task epilogue (reward, obs, autoreset).
 // Assembly writes the solver's per-env record (Workspace) that so100_pgs_kernel consumes.
 template <int kMode>
-__global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args) {
+#ifndef SO100_STAGE_WAVES
+#define SO100_STAGE_WAVES 3      // waves per SIMD the stage kernel's register budget is sized for
+#endif
+__global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kernel(StageArgs args) {
   __shared__ EnvShared shm[kEnvsPerBlock];
   const DevModel* __restrict__ m = args.m;
   const int tid = threadIdx.x;
@@ -1071,8 +1124,11 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
   const int elapsed0 = B.elapsed ? B.elapsed[e] : 0;
   const uint32_t episode0 = B.episode ? B.episode[e] : 0u;
   const float h = m->timestep;
+  SSTAMP_DECL
+  SSTAMP(-1);
 
   if (kMode != 0) euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
+  SSTAMP(0);
 
   if (kMode != 2) {
     // control (the same every substep of the env step: elapsed/episode only change in the epilogue)
@@ -1090,6 +1146,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
     // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
     if (lane == 0) serial_stage(m, sh, true, mscale);
     __syncthreads();
+    SSTAMP(1);
     // ---------------- S3: collision, one pair per lane, compaction in pair order
     PairContacts pc;
     pc.n = 0;
@@ -1100,9 +1157,10 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
       int off = 0, tot = 0;
 #pragma unroll
       for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
-      for (int c = 0; c < pc.n; c++) {
+#pragma unroll
+      for (int c = 0; c < SO100_MAXCONPAIR; c++) {
         int slot = off + c;
-        if (slot < kMaxCon) {
+        if (c < pc.n && slot < kMaxCon) {
           float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
           make_frame(fr);
 #pragma unroll
@@ -1118,6 +1176,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
     __syncthreads();
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
+    SSTAMP(2);
     if (lane == 0 && ncon > kResident) {
       // this env's solver group is heavy: list it once for first dispatch (so100_pgs.hip)
       const int g = env / kPgsEnvs, ngroups = (args.n + kPgsEnvs - 1) / kPgsEnvs;
@@ -1209,6 +1268,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
         }
       }
     }
+    SSTAMP(3);
     // ---------------- S6b: scalar setup of contact `lane` (impedance, regularisers, warmstart dual map,
     // eigen-decomposition for the QCQP) -> solver block in the HBM record
     float cf[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1284,6 +1344,7 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
 #pragma unroll
       for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
     }
+    SSTAMP(4);
     // J' f of the warmstart forces: contact c's forces broadcast from lane c
 #pragma unroll
     for (int c = 0; c < kMaxCon; c++) {
@@ -1340,6 +1401,13 @@ __global__ void __launch_bounds__(kThreads, 3) so100_stage_kernel(StageArgs args
         if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
         if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
       }
+      SSTAMP(5);
+#ifdef SO100_STAGE_STAMPS
+      if (B.debug && args.sub == m->nsubstep - 1 && lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
+      }
+#endif
       // debug: contact set of the last substep (forces / iterations come from the solver kernel)
       if (B.debug && args.sub == m->nsubstep - 1) {
         float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
