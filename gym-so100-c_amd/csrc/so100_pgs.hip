@@ -11,14 +11,15 @@
 //   * the arm and cube trees are decoupled (M block-diagonal, cube M diagonal: COM at the free-joint
 //     origin, principal axes = body axes), so arm frictionloss row j and cube row 6+j update together;
 //   * the first kResident contacts keep J in VGPRs and the solver block in LDS for all sweeps; further
-//     contacts (rare: >4 per env) stream both from the HBM record every sweep.
+//     contacts (rare: >4 per env) stream both from the HBM record every sweep, loaded at use so the
+//     register peak stays at 168 (3 waves/SIMD); their forces stay in LDS.
 #include "so100_common.h"
 #include "so100.h"
 
 namespace so100 {
 
 #ifndef SO100_PGS_WAVES
-#define SO100_PGS_WAVES 2        // waves per SIMD the register budget is sized for
+#define SO100_PGS_WAVES 3        // waves per SIMD the register budget is sized for
 #endif
 
 struct PgsArgs {
@@ -266,30 +267,48 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
     }
     STAMP(2);
     // contact blocks beyond kResident (rare: >4 contacts): solver block and J rows streamed from the
-    // record (read-only; the next contact's prefetched while the current one is solved), forces in LDS
+    // record (read-only), forces in LDS.  -DSO100_OVF_PREFETCH prefetches the next contact (52 more
+    // VGPRs: 2 waves/SIMD; measured 4% slower overall than 3 waves/SIMD without it)
     if (ncon_max > kResident) {
+#ifdef SO100_OVF_PREFETCH
       float4 vn[kBlk], Jn[3];
       {
         const float4* rec = reinterpret_cast<const float4*>(crec + kResident * kConRec);
 #pragma unroll
-        for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? make_float4(0.f, 0.f, 0.f, 0.f) : rec[k];
+        for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? zero4 : rec[k];
 #pragma unroll
         for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
       }
+#endif
       for (int c = kResident; c < ncon_max; c++) {
         float4 v[kBlk], Jo[3];
+#ifdef SO100_OVF_PREFETCH
 #pragma unroll
         for (int k = 0; k < kBlk; k++) v[k] = vn[k];
 #pragma unroll
         for (int i = 0; i < 3; i++) Jo[i] = c < ncon ? Jn[i] : zero4;
-        v[kBlkF] = fov[c - kResident][ew];
         if (c + 1 < ncon_max) {
           const float4* rec = reinterpret_cast<const float4*>(crec + (c + 1) * kConRec);
 #pragma unroll
-          for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? make_float4(0.f, 0.f, 0.f, 0.f) : rec[k];
+          for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? zero4 : rec[k];
 #pragma unroll
           for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
         }
+#else
+        // loaded at use: keeps the register peak at the resident path's (3 waves/SIMD); the latency is
+        // paid only by waves holding an env with > kResident contacts (dispatched first)
+        {
+          const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
+#pragma unroll
+          for (int k = 0; k < kBlk; k++) v[k] = k == kBlkF ? zero4 : rec[k];
+#pragma unroll
+          for (int i = 0; i < 3; i++) {
+            const float4 t = rec[kBlk + 3 * q + i];
+            Jo[i] = c < ncon ? t : zero4;
+          }
+        }
+#endif
+        v[kBlkF] = fov[c - kResident][ew];
         const bool act = c < ncon && !done;
         const bool arm = __ballot(c < ncon && v[kBlkFlags].y != 0.f) != 0ull;
         float4 fn;
