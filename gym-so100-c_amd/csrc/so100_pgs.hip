@@ -10,9 +10,9 @@
 //     partner's 3 dof values arrive by one quad_perm swap;
 //   * the arm and cube trees are decoupled (M block-diagonal, cube M diagonal: COM at the free-joint
 //     origin, principal axes = body axes), so arm frictionloss row j and cube row 6+j update together;
-//   * the first kResident contacts keep J in VGPRs and the solver block in LDS for all sweeps; further
-//     contacts (rare: >4 per env) stream both from the HBM record every sweep, loaded at use so the
-//     register peak stays at 168 (3 waves/SIMD); their forces stay in LDS.
+//   * the first kResident contacts keep J in VGPRs and the solver block in LDS (10 KB per wave) for all
+//     sweeps; further contacts (rare: >4 per env) stream both from the HBM record every sweep, loaded at
+//     use so the register peak stays at 168 (3 waves/SIMD), forces written back to the record.
 #include "so100_common.h"
 #include "so100.h"
 
@@ -103,7 +103,6 @@ DEV void contact_update(const float4 (&v)[kBlk], const float4 (&J)[3], float (&q
 
 __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs a) {
   __shared__ float4 blk[kResident][kPgsEnvs][kBlk];
-  __shared__ float4 fov[kMaxCon - kResident][kPgsEnvs];   // forces of the streamed (overflow) contacts
   const DevModel* __restrict__ m = a.m;
   const int tid = threadIdx.x;
   const int q = tid & 3;
@@ -197,8 +196,6 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
     blk[c][ew][q + 4] = rec[q + 4];
     if (q < 2) blk[c][ew][q + 8] = rec[q + 8];
   }
-  for (int c = kResident + q; c < ncon_max; c += 4)
-    fov[c - kResident][ew] = reinterpret_cast<const float4*>(crec + c * kConRec)[kBlkF];
   __syncthreads();
   // resident contact slots in which some env of the wave has a gripper contact (J with arm entries)
   uint32_t arm_res = 0;
@@ -267,54 +264,26 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
     }
     STAMP(2);
     // contact blocks beyond kResident (rare: >4 contacts): solver block and J rows streamed from the
-    // record (read-only), forces in LDS.  -DSO100_OVF_PREFETCH prefetches the next contact (52 more
-    // VGPRs: 2 waves/SIMD; measured 4% slower overall than 3 waves/SIMD without it)
+    // record at use (a prefetch's double buffers would cost the third wave per SIMD), forces written
+    // back to the record by lane 0
     if (ncon_max > kResident) {
-#ifdef SO100_OVF_PREFETCH
-      float4 vn[kBlk], Jn[3];
-      {
-        const float4* rec = reinterpret_cast<const float4*>(crec + kResident * kConRec);
-#pragma unroll
-        for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? zero4 : rec[k];
-#pragma unroll
-        for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
-      }
-#endif
       for (int c = kResident; c < ncon_max; c++) {
         float4 v[kBlk], Jo[3];
-#ifdef SO100_OVF_PREFETCH
+        const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
 #pragma unroll
-        for (int k = 0; k < kBlk; k++) v[k] = vn[k];
+        for (int k = 0; k < kBlk; k++) v[k] = rec[k];
 #pragma unroll
-        for (int i = 0; i < 3; i++) Jo[i] = c < ncon ? Jn[i] : zero4;
-        if (c + 1 < ncon_max) {
-          const float4* rec = reinterpret_cast<const float4*>(crec + (c + 1) * kConRec);
-#pragma unroll
-          for (int k = 0; k < kBlk; k++) vn[k] = k == kBlkF ? zero4 : rec[k];
-#pragma unroll
-          for (int i = 0; i < 3; i++) Jn[i] = rec[kBlk + 3 * q + i];
+        for (int i = 0; i < 3; i++) {
+          const float4 t = rec[kBlk + 3 * q + i];
+          Jo[i] = c < ncon ? t : zero4;
         }
-#else
-        // loaded at use: keeps the register peak at the resident path's (3 waves/SIMD); the latency is
-        // paid only by waves holding an env with > kResident contacts (dispatched first)
-        {
-          const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
-#pragma unroll
-          for (int k = 0; k < kBlk; k++) v[k] = k == kBlkF ? zero4 : rec[k];
-#pragma unroll
-          for (int i = 0; i < 3; i++) {
-            const float4 t = rec[kBlk + 3 * q + i];
-            Jo[i] = c < ncon ? t : zero4;
-          }
-        }
-#endif
-        v[kBlkF] = fov[c - kResident][ew];
         const bool act = c < ncon && !done;
         const bool arm = __ballot(c < ncon && v[kBlkFlags].y != 0.f) != 0ull;
         float4 fn;
         contact_update(v, Jo, qacc, mrow, act, q == 0, arm, impr, fn, newton);
-        if (act) fov[c - kResident][ew] = fn;
+        if (act && q == 0) reinterpret_cast<float4*>(crec + c * kConRec)[kBlkF] = fn;
       }
+      __threadfence_block();   // the forces are re-read by all 4 lanes next sweep
     }
     STAMP(3);
     const float improvement = quadsum(impr) * pgs_scale;
@@ -364,7 +333,7 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
         dbg[2] = last_impr;
         for (int c = 0; c < kMaxCon; c++) {
           float f0 = 0.f;
-          if (c < ncon) f0 = c < kResident ? blk[c][ew][kBlkF].x : fov[c - kResident][ew].x;
+          if (c < ncon) f0 = c < kResident ? blk[c][ew][kBlkF].x : crec[c * kConRec + 4 * kBlkF];
           dbg[32 + c] = f0;
         }
       }
