@@ -395,20 +395,20 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
   }
   // ---- Cholesky + explicit inverse of the 6x6 arm block (symmetrised) -> LDS
   {
-    float L[6][6];
+    float L[6][6], Linv[6];       // Linv: the 6 diagonal reciprocals, shared by all 12 triangular solves
 #pragma unroll
     for (int j = 0; j < 6; j++) {
       float sdiag = M[j][j];
 #pragma unroll
       for (int k = 0; k < j; k++) sdiag -= L[j][k] * L[j][k];
       L[j][j] = sqrtf(fmaxf(sdiag, kMinVal));
-      const float inv = 1.0f / L[j][j];
+      Linv[j] = 1.0f / L[j][j];
 #pragma unroll
       for (int i = j + 1; i < 6; i++) {
         float t = M[i][j];
 #pragma unroll
         for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
-        L[i][j] = t * inv;
+        L[i][j] = t * Linv[j];
       }
     }
     for (int c = 0; c < 6; c++) {   // solve M x = e_c
@@ -418,14 +418,14 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
         float sacc = (i == c) ? 1.f : 0.f;
 #pragma unroll
         for (int k = 0; k < i; k++) sacc -= L[i][k] * z[k];
-        z[i] = sacc / L[i][i];
+        z[i] = sacc * Linv[i];
       }
 #pragma unroll
       for (int i = 5; i >= 0; i--) {
         float sacc = z[i];
 #pragma unroll
         for (int k = i + 1; k < 6; k++) sacc -= L[k][i] * x[k];
-        x[i] = sacc / L[i][i];
+        x[i] = sacc * Linv[i];
       }
 #pragma unroll
       for (int i = 0; i < 6; i++) sh.ser.cfrc[i][c] = x[i];   // temporary M^-1 column storage
@@ -667,13 +667,14 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
       n[i2] = R[3 * i1 + j];
       float l = sqrtf(n[i1] * n[i1] + n[i2] * n[i2]);
       if (l < 1e-5f) continue;
+      const float linv = 1.0f / l;
       float e = pp[i2] * R[3 * i1 + j] - pp[i1] * R[3 * i2 + j];
       float ex = A[i1] * Q[3 * i2 + j] + A[i2] * Q[3 * i1 + j] + B[j1] * Q[3 * i + j2] + B[j2] * Q[3 * i + j1];
-      float s = (fabsf(e) - ex) / l;
+      float s = (fabsf(e) - ex) * linv;
       if (s > margin) return;
       if (s * 1.05f > best) {
         best = s; code = 7 + 3 * i + j; invert = e < 0;
-        nb[0] = n[0] / l; nb[1] = n[1] / l; nb[2] = n[2] / l;
+        nb[0] = n[0] * linv; nb[1] = n[1] * linv; nb[2] = n[2] * linv;
       }
     }
   }
