@@ -972,9 +972,11 @@ DEV void eig3_sym(const float A0[3][3], float lam[3], float Q[3][3]) {
       const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
       const float apq = a[p][q];
       if (fabsf(apq) > 1e-30f) {
-        const float theta = (a[q][q] - a[p][p]) / (2.f * apq);
-        const float t = copysignf(1.f, theta) / (fabsf(theta) + sqrtf(theta * theta + 1.f));
-        const float c = 1.f / sqrtf(t * t + 1.f), sn = t * c;
+        // hardware rcp / sqrt / rsq (~1 ulp): each rotation stays orthogonal to fp32 precision and the
+        // cyclic sweeps correct any residual, at a fraction of the IEEE division / sqrt sequences
+        const float theta = (a[q][q] - a[p][p]) * __builtin_amdgcn_rcpf(2.f * apq);
+        const float t = copysignf(__builtin_amdgcn_rcpf(fabsf(theta) + __builtin_amdgcn_sqrtf(theta * theta + 1.f)), theta);
+        const float c = __builtin_amdgcn_rsqf(t * t + 1.f), sn = t * c;
 #pragma unroll
         for (int k = 0; k < 3; k++) {           // columns p, q
           const float akp = a[k][p], akq = a[k][q];
