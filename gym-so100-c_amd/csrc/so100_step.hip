@@ -35,6 +35,12 @@ struct __attribute__((aligned(16))) SerialScratch {   // per-body arrays of the 
   float cin[6][16];    // spatial inertia about the Base origin: I(9), m*d(3), m
   float cdof[6][8];    // motion subspace (angular; linear)
   float cfrc[6][8];    // RNE body forces
+  float M[6][8];       // joint-space inertia of the arm (CRBA)
+  float F[6][8];       // composite inertia times motion subspace, per body
+  float L[6][8];       // Cholesky factor of M; L[i][6] = 1 / L[i][i]
+  float X[6][8];       // M^-1 columns (X[c][i] = M^-1[i][c])
+  float cdd[6][8];     // RNE: cdof_dot per body
+  float tau[8];        // actuator force minus bias
 };
 struct __attribute__((aligned(16))) EnvShared {
   float qpos[16];
@@ -277,7 +283,9 @@ DEV void cube_frame(const float* qp, float* pos, float* mat) {
 }
 
 // full serial stage; writes frames, M^-1, qacc_smooth, sites into sh
-DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynamics, float mscale) {
+// Forward kinematics of the 6-link chain (lane 0 of the env's row): body frames, joint anchors/axes,
+// jaw frames, sites, cube frame.  dynamics_par continues from these.
+DEV void fk_stage(const DevModel* __restrict__ m, EnvShared& sh) {
   // ---- forward kinematics along the chain; frames staged in LDS to bound register pressure
   {
     float pos[3] = {m->base_pos[0], m->base_pos[1], m->base_pos[2]};
@@ -332,16 +340,23 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
 #pragma unroll
     for (int k = 0; k < 3; k++) sh.site_cube[k] = cpos[k] + t[k];
   }
-  if (!dynamics) return;
+}
 
-  // ---- comPos: cinert about the tree reference point r = Base xpos; cdof
-  const float* r = m->base_pos;
-  for (int a = 0; a < 6; a++) {
+// Lane-parallel dynamics stage (all 16 lanes of the env's row; lanes 0..5 = bodies/dofs of the arm):
+// comPos, CRBA, Cholesky (lane 0) + M^-1 columns, RNE and actuation, with every sum in the serial
+// order of the lane-0 version (prefix sums of cvel/cacc, suffix sums of crb/bias) so results are the
+// same bit-for-bit.  Requires fk_stage first and a barrier.
+DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale) {
+  SerialScratch& S = sh.ser;
+  // ---- comPos (body a = lane): cinert about the tree reference point r = Base xpos; cdof
+  if (lane < 6) {
+    const int a = lane;
+    const float* r = m->base_pos;
     float xm[9], xp[3], ax[3];
 #pragma unroll
-    for (int k = 0; k < 9; k++) xm[k] = sh.ser.xm[a][k];
+    for (int k = 0; k < 9; k++) xm[k] = S.xm[a][k];
 #pragma unroll
-    for (int k = 0; k < 3; k++) { xp[k] = sh.ser.xp[a][k]; ax[k] = sh.axis[a][k]; }
+    for (int k = 0; k < 3; k++) { xp[k] = S.xp[a][k]; ax[k] = sh.axis[a][k]; }
     float ip[3], xi[3], IM[9], diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Ib[9], RT[9], Iw[9];
     mulmv3(ip, xm, m->body_ipos[a]);
 #pragma unroll
@@ -359,151 +374,190 @@ DEV void serial_stage(const DevModel* __restrict__ m, EnvShared& sh, bool dynami
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-      for (int j = 0; j < 3; j++) sh.ser.cin[a][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0.f) - xi[i] * xi[j]);
+      for (int j = 0; j < 3; j++) S.cin[a][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0.f) - xi[i] * xi[j]);
 #pragma unroll
-    for (int k = 0; k < 3; k++) sh.ser.cin[a][9 + k] = mass * xi[k];
-    sh.ser.cin[a][12] = mass;
+    for (int k = 0; k < 3; k++) S.cin[a][9 + k] = mass * xi[k];
+    S.cin[a][12] = mass;
     float off[3] = {r[0] - xp[0], r[1] - xp[1], r[2] - xp[2]}, lin[3];
     cross3(lin, ax, off);
 #pragma unroll
-    for (int k = 0; k < 3; k++) { sh.ser.cdof[a][k] = ax[k]; sh.ser.cdof[a][3 + k] = lin[k]; }
+    for (int k = 0; k < 3; k++) { S.cdof[a][k] = ax[k]; S.cdof[a][3 + k] = lin[k]; }
   }
-  asm volatile("" ::: "memory");
-  // ---- CRBA (chain): composite inertia bottom-up, M(i,j) = cdof_j . (crb_i cdof_i), j <= i
-  float M[6][6];
-  {
+  __syncthreads();
+  // ---- CRBA: composite inertia crb_i = cin_5 + ... + cin_i (that order), F_i = crb_i cdof_i
+  if (lane < 6) {
+    const int i = lane;
     float crb[13];
 #pragma unroll
     for (int k = 0; k < 13; k++) crb[k] = 0.f;
 #pragma unroll
-    for (int i = 5; i >= 0; i--) {
+    for (int b = 5; b >= 0; b--) {
+      if (b >= i) {
 #pragma unroll
-      for (int k = 0; k < 13; k++) crb[k] += sh.ser.cin[i][k];
-      float F[6], cd[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) cd[k] = sh.ser.cdof[i][k];
-      mul_inert(F, crb, cd);
-#pragma unroll
-      for (int j = 0; j <= i; j++) {
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 6; k++) v += sh.ser.cdof[j][k] * F[k];
-        M[i][j] = v; M[j][i] = v;
+        for (int k = 0; k < 13; k++) crb[k] += S.cin[b][k];
       }
-      M[i][i] += m->armature[i];
     }
-  }
-  // ---- Cholesky + explicit inverse of the 6x6 arm block (symmetrised) -> LDS
-  {
-    float L[6][6], Linv[6];       // Linv: the 6 diagonal reciprocals, shared by all 12 triangular solves
+    float F[6], cd[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) cd[k] = S.cdof[i][k];
+    mul_inert(F, crb, cd);
+#pragma unroll
+    for (int k = 0; k < 6; k++) S.F[i][k] = F[k];
+    // row i of M (j <= i) and its mirror: M(i,j) = cdof_j . F_i
 #pragma unroll
     for (int j = 0; j < 6; j++) {
-      float sdiag = M[j][j];
+      if (j <= i) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) v += S.cdof[j][k] * F[k];
+        if (j == i) v += m->armature[i];
+        S.M[i][j] = v;
+        S.M[j][i] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- Cholesky of the 6x6 (lane 0), diagonal reciprocals stored for the column solves
+  if (lane == 0) {
+    float L[6][6], Linv[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      float sdiag = S.M[j][j];
 #pragma unroll
       for (int k = 0; k < j; k++) sdiag -= L[j][k] * L[j][k];
       L[j][j] = sqrtf(fmaxf(sdiag, kMinVal));
       Linv[j] = 1.0f / L[j][j];
 #pragma unroll
       for (int i = j + 1; i < 6; i++) {
-        float t = M[i][j];
+        float t = S.M[i][j];
 #pragma unroll
         for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
         L[i][j] = t * Linv[j];
       }
     }
-    for (int c = 0; c < 6; c++) {   // solve M x = e_c
-      float z[6], x[6];
 #pragma unroll
-      for (int i = 0; i < 6; i++) {
-        float sacc = (i == c) ? 1.f : 0.f;
+    for (int i = 0; i < 6; i++) {
 #pragma unroll
-        for (int k = 0; k < i; k++) sacc -= L[i][k] * z[k];
-        z[i] = sacc * Linv[i];
-      }
-#pragma unroll
-      for (int i = 5; i >= 0; i--) {
-        float sacc = z[i];
-#pragma unroll
-        for (int k = i + 1; k < 6; k++) sacc -= L[k][i] * x[k];
-        x[i] = sacc * Linv[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; i++) sh.ser.cfrc[i][c] = x[i];   // temporary M^-1 column storage
+      for (int k = 0; k <= i; k++) S.L[i][k] = L[i][k];
+      S.L[i][6] = Linv[i];
     }
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-#pragma unroll
-      for (int j = 0; j < 6; j++) sh.minv[i][j] = 0.5f * (sh.ser.cfrc[i][j] + sh.ser.cfrc[j][i]);
   }
-  asm volatile("" ::: "memory");
-  // ---- RNE (flg_acc = 0) on the chain: cvel, cdof_dot, cacc, cfrc, backward accumulation
-  {
+  __syncthreads();
+  // ---- M^-1 columns: lane c solves M x = e_c
+  if (lane < 6) {
+    const int c = lane;
+    float L[6][6], Linv[6], z[6], x[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+#pragma unroll
+      for (int k = 0; k <= i; k++) L[i][k] = S.L[i][k];
+      Linv[i] = S.L[i][6];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      float sacc = (i == c) ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < i; k++) sacc -= L[i][k] * z[k];
+      z[i] = sacc * Linv[i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+      float sacc = z[i];
+#pragma unroll
+      for (int k = i + 1; k < 6; k++) sacc -= L[k][i] * x[k];
+      x[i] = sacc * Linv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) S.X[c][i] = x[i];
+  }
+  // ---- RNE (flg_acc = 0), part 1: cvel_a = sum_{k<=a} cdof_k qd_k, cdof_dot_a = cvel_a x cdof_a
+  if (lane < 6) {
+    const int a = lane;
+    float cvel[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      if (b <= a) {
+        const float qd = sh.qvel[b];
+#pragma unroll
+        for (int k = 0; k < 6; k++) cvel[k] += S.cdof[b][k] * qd;
+      }
+    }
+    float cd[6], cdd[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) cd[k] = S.cdof[a][k];
+    cross_motion(cdd, cvel, cd);
+#pragma unroll
+    for (int k = 0; k < 6; k++) S.cdd[a][k] = cdd[k];
+  }
+  __syncthreads();
+  // symmetrised M^-1 -> LDS (minv), RNE part 2: cacc_a = -g + sum_{k<=a} cdd_k qd_k, body forces
+  if (lane < 6) {
+    const int a = lane;
+#pragma unroll
+    for (int j = 0; j < 6; j++) sh.minv[a][j] = 0.5f * (S.X[j][a] + S.X[a][j]);
     float cvel[6] = {0, 0, 0, 0, 0, 0};
     float cacc[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-    for (int a = 0; a < 6; a++) {
-      float cd[6], cin[13];
 #pragma unroll
-      for (int k = 0; k < 6; k++) cd[k] = sh.ser.cdof[a][k];
+    for (int b = 0; b < 6; b++) {
+      if (b <= a) {
+        const float qd = sh.qvel[b];
 #pragma unroll
-      for (int k = 0; k < 13; k++) cin[k] = sh.ser.cin[a][k];
-      const float qd = sh.qvel[a];
+        for (int k = 0; k < 6; k++) cvel[k] += S.cdof[b][k] * qd;
 #pragma unroll
-      for (int k = 0; k < 6; k++) cvel[k] += cd[k] * qd;
-      float cdd[6];
-      cross_motion(cdd, cvel, cd);
-#pragma unroll
-      for (int k = 0; k < 6; k++) cacc[k] += cdd[k] * qd;
-      float f1[6], Iv[6], f2[6];
-      mul_inert(f1, cin, cacc);
-      mul_inert(Iv, cin, cvel);
-      cross_force(f2, cvel, Iv);
-#pragma unroll
-      for (int k = 0; k < 6; k++) sh.ser.cfrc[a][k] = f1[k] + f2[k];
+        for (int k = 0; k < 6; k++) cacc[k] += S.cdd[b][k] * qd;
+      }
     }
+    float cin[13];
+#pragma unroll
+    for (int k = 0; k < 13; k++) cin[k] = S.cin[a][k];
+    float f1[6], Iv[6], f2[6];
+    mul_inert(f1, cin, cacc);
+    mul_inert(Iv, cin, cvel);
+    cross_force(f2, cvel, Iv);
+#pragma unroll
+    for (int k = 0; k < 6; k++) S.cfrc[a][k] = f1[k] + f2[k];
   }
-  asm volatile("" ::: "memory");
-  float bias[6];
-  {
+  __syncthreads();
+  // ---- bias_a = cdof_a . sum_{k>=a} cfrc_k (suffix, from body 5 down); actuation
+  if (lane < 6) {
+    const int a = lane;
     float acc[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int a = 5; a >= 0; a--) {
+    for (int b = 5; b >= 0; b--) {
+      if (b >= a) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) acc[k] += sh.ser.cfrc[a][k];
-      float v = 0.f;
-#pragma unroll
-      for (int k = 0; k < 6; k++) v += sh.ser.cdof[a][k] * acc[k];
-      bias[a] = v;
+        for (int k = 0; k < 6; k++) acc[k] += S.cfrc[b][k];
+      }
     }
-  }
-  // ---- actuation: position actuators (ctrl clamped to ctrlrange, force to forcerange)
-  float tau[6];
+    float bias = 0.f;
 #pragma unroll
-  for (int i = 0; i < 6; i++) {
-    const float c = fminf(fmaxf(sh.ctrl[i], m->act_clo[i]), m->act_chi[i]);
-    float f = m->act_kp[i] * c - m->act_kp[i] * sh.qpos[i] - m->act_kv[i] * sh.qvel[i];
-    f = fminf(fmaxf(f, m->act_flo[i]), m->act_fhi[i]);
-    tau[i] = f - bias[i];
+    for (int k = 0; k < 6; k++) bias += S.cdof[a][k] * acc[k];
+    const float c = fminf(fmaxf(sh.ctrl[a], m->act_clo[a]), m->act_chi[a]);
+    float f = m->act_kp[a] * c - m->act_kp[a] * sh.qpos[a] - m->act_kv[a] * sh.qvel[a];
+    f = fminf(fmaxf(f, m->act_flo[a]), m->act_fhi[a]);
+    S.tau[a] = f - bias;
   }
-#pragma unroll
-  for (int i = 0; i < 6; i++) {
+  __syncthreads();
+  if (lane < 6) {
+    const int i = lane;
     float sacc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 6; j++) sacc += sh.minv[i][j] * tau[j];
+    for (int j = 0; j < 6; j++) sacc += sh.minv[i][j] * S.tau[j];
     sh.qacc_smooth[i] = sacc;
-  }
-  // ---- cube (free body)
-  const float mc = m->cube_mass * mscale;
-  const float I3[3] = {m->cube_inertia[0] * mscale, m->cube_inertia[1] * mscale, m->cube_inertia[2] * mscale};
-  const float w[3] = {sh.qvel[9], sh.qvel[10], sh.qvel[11]};
-  float Iw3[3] = {I3[0] * w[0], I3[1] * w[1], I3[2] * w[2]}, gyro[3];
-  cross3(gyro, w, Iw3);
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    sh.qacc_smooth[6 + k] = (mc * m->gravity[k]) / mc;   // -bias/m with bias = -m g
-    sh.qacc_smooth[9 + k] = -gyro[k] / I3[k];
+  } else if (lane < 9) {
+    // cube (free body): -bias / m = g, gyroscopic term on the rotational dofs
+    const int k = lane - 6;
+    const float mc = m->cube_mass * mscale;
+    const float I3[3] = {m->cube_inertia[0] * mscale, m->cube_inertia[1] * mscale, m->cube_inertia[2] * mscale};
+    const float w[3] = {sh.qvel[9], sh.qvel[10], sh.qvel[11]};
+    float Iw3[3] = {I3[0] * w[0], I3[1] * w[1], I3[2] * w[2]}, gyro[3];
+    cross3(gyro, w, Iw3);
+    const float gk = k == 0 ? gyro[0] : (k == 1 ? gyro[1] : gyro[2]);
+    const float Ik = k == 0 ? I3[0] : (k == 1 ? I3[1] : I3[2]);
+    sh.qacc_smooth[6 + k] = (mc * m->gravity[k]) / mc;
+    sh.qacc_smooth[9 + k] = -gk / Ik;
     sh.inv_mcube[k] = 1.0f / mc;
-    sh.inv_mcube[3 + k] = 1.0f / I3[k];
+    sh.inv_mcube[3 + k] = 1.0f / Ik;
   }
 }
 
@@ -1147,7 +1201,9 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
     __syncthreads();
     // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
-    if (lane == 0) serial_stage(m, sh, true, mscale);
+    if (lane == 0) fk_stage(m, sh);
+    __syncthreads();
+    dynamics_par(m, sh, lane, mscale);
     __syncthreads();
     SSTAMP(1);
     // ---------------- S3: collision, one pair per lane, compaction in pair order
@@ -1432,7 +1488,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
   __syncthreads();
-  if (lane == 0) serial_stage(m, sh, false, mscale);
+  if (lane == 0) fk_stage(m, sh);
   __syncthreads();
   PairContacts pc;
   pc.n = 0;
@@ -1502,7 +1558,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     __syncthreads();
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
     __syncthreads();
-    if (lane == 0 && do_reset && valid) serial_stage(m, sh, false, mscale);
+    if (lane == 0 && do_reset && valid) fk_stage(m, sh);
     __syncthreads();
     const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
     if (do_reset && valid) {
@@ -1572,7 +1628,7 @@ __global__ void __launch_bounds__(kThreads) so100_reset_kernel(ResetArgs args) {
   }
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   __syncthreads();
-  if (lane == 0 && act) serial_stage(m, sh, false, 1.f);
+  if (lane == 0 && act) fk_stage(m, sh);
   __syncthreads();
   const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
   if (act) {
