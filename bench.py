@@ -181,9 +181,11 @@ def main(argv=None):
     if rank == 0:
         env_steps = total * args.steps
         value = env_steps / elapsed
-        solver_bytes = count * (SOLVER_BYTES_PER_ENV + SOLVER_BYTES_PER_CONTACT * contacts_per_env)
+        # the timed launches are chunk 0's (n0 envs), concurrent with the other chunks' (so100_chunk_info)
+        nchunks, n0 = env.chunk_info()
+        solver_bytes = n0 * (SOLVER_BYTES_PER_ENV + SOLVER_BYTES_PER_CONTACT * contacts_per_env)
         achieved = solver_bytes / (solver_ms * 1e-3)
-        traffic = load_traffic(count)
+        traffic = load_traffic(n0)
         line = {
             "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
@@ -197,7 +199,8 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "kernel": "so100_pgs_kernel", "kernel_ms": solver_ms,
-                         "bytes_per_launch": solver_bytes, "contacts_per_env": contacts_per_env,
+                         "bytes_per_launch": solver_bytes, "envs_per_launch": n0, "concurrent_chunks": nchunks,
+                         "contacts_per_env": contacts_per_env,
                          "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
                          "boundary_bytes_per_env_step": BYTES_PER_ENV_STEP,
                          "note": ("solver = serial Gauss-Seidel chains per env: issue/latency-bound, not HBM-bound "

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -31,12 +32,23 @@ hipError_t launch_goal_reward(const DevModel*, int, const float*, const float*, 
 using so100::DevModel;
 using so100::Workspace;
 
+// A contiguous env range with its own substep workspace and stream.  With more than one chunk the
+// chunks' launch sequences run concurrently (forked from / joined to the caller's stream), so one
+// chunk's stage kernel fills the SIMD slots left idle by another chunk's solver tail.
+struct Chunk {
+  int start = 0, count = 0;
+  Workspace ws{};               // substep hand-off record between the stage and solver kernels
+  hipStream_t s = nullptr;      // nullptr: the caller's stream (single chunk)
+  hipEvent_t done = nullptr;
+};
+
 struct so100_env {
   int device;
   int n;
   DevModel* d_model;
   int nsubstep;
-  Workspace ws;                 // substep hand-off record between the stage and solver kernels
+  std::vector<Chunk> chunks;
+  hipEvent_t fork = nullptr;
   int task;
   int max_steps;
   uint64_t base_seed;
@@ -45,6 +57,88 @@ struct so100_env {
   std::vector<hipEvent_t> prof_ev;
   int prof_cap = 0, prof_used = 0;
 };
+
+static hipError_t free_chunks(so100_env* env) {
+  hipError_t e = hipSuccess;
+  for (Chunk& c : env->chunks) {
+    hipError_t e2 = so100::free_workspace(&c.ws);
+    if (e == hipSuccess) e = e2;
+    if (c.done) (void)hipEventDestroy(c.done);
+    if (c.s) (void)hipStreamDestroy(c.s);
+  }
+  env->chunks.clear();
+  if (env->fork) (void)hipEventDestroy(env->fork);
+  env->fork = nullptr;
+  return e;
+}
+
+// Chunk count: SO100_CHUNKS overrides; otherwise as many chunks as the process has hardware queues
+// (GPU_MAX_HW_QUEUES, HIP's default 4; chunk 0 shares the caller's), at least 1,024 envs each.  More
+// streams than queues serialise on shared queues (measured: 5-8 chunks run 1.6x slower than 4).
+static int default_chunks(int n) {
+  if (const char* v = getenv("SO100_CHUNKS")) {
+    const int k = atoi(v);
+    if (k >= 1 && k <= 16) return k;
+  }
+  int q = 4;
+  if (const char* v = getenv("GPU_MAX_HW_QUEUES")) {
+    const int k = atoi(v);
+    if (k >= 1) q = k;
+  }
+  if (q > 4) q = 4;
+  const int k = n / 1024;
+  return k < 1 ? 1 : (k > q ? q : k);
+}
+
+static hipError_t make_chunks(so100_env* env, int nchunk) {
+  const int n = env->n;
+  const int unit = 64;                                   // whole stage blocks and solver groups
+  const int units = (n + unit - 1) / unit;
+  if (nchunk > units) nchunk = units;
+  hipError_t e = hipSuccess;
+  if (nchunk > 1) e = hipEventCreateWithFlags(&env->fork, hipEventDisableTiming);
+  int start = 0;
+  for (int k = 0; k < nchunk && e == hipSuccess; k++) {
+    Chunk c;
+    c.start = start;
+    const int end = k == nchunk - 1 ? n : (int)((long)units * (k + 1) / nchunk) * unit;
+    c.count = end - start;
+    start = end;
+    e = so100::alloc_workspace(c.count, &c.ws);
+    // chunk 0 runs on the caller's stream: K chunks take K - 1 extra hardware queues
+    if (e == hipSuccess && k > 0) e = hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking);
+    if (e == hipSuccess && k > 0) e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming);
+    env->chunks.push_back(c);
+  }
+  return e;
+}
+
+// per-env buffer pointers of the env range starting at `s`
+static so100_buffers offset_buffers(const so100_buffers& b, int s) {
+  so100_buffers o = b;
+  const size_t k = (size_t)s;
+  auto off = [k](auto* p, int dim) { return p ? p + k * dim : p; };
+  o.qpos = off(b.qpos, SO100_NQ);
+  o.qvel = off(b.qvel, SO100_NV);
+  o.qacc_warmstart = off(b.qacc_warmstart, SO100_NV);
+  o.elapsed = off(b.elapsed, 1);
+  o.episode = off(b.episode, 1);
+  o.action = off(b.action, SO100_NU);
+  o.obs = off(b.obs, SO100_NOBS);
+  o.reward = off(b.reward, 1);
+  o.terminated = off(b.terminated, 1);
+  o.truncated = off(b.truncated, 1);
+  o.success = off(b.success, 1);
+  o.final_obs = off(b.final_obs, SO100_NOBS);
+  o.diverged = off(b.diverged, 1);
+  o.contact_bits = off(b.contact_bits, 1);
+  o.achieved_goal = off(b.achieved_goal, 3);
+  o.desired_goal = off(b.desired_goal, 3);
+  o.total_steps = off(b.total_steps, 1);
+  o.dr_params = off(b.dr_params, 4);
+  o.debug = off(b.debug, SO100_DBG_STRIDE);
+  return o;
+}
 
 static void profile_free(so100_env* env) {
   for (hipEvent_t e : env->prof_ev) (void)hipEventDestroy(e);
@@ -255,10 +349,15 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (e != hipSuccess) { fail_hip("so100_create: hipMalloc", e); return nullptr; }
   e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
-  Workspace ws;
-  e = so100::alloc_workspace(n_envs, &ws);
-  if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: workspace hipMalloc", e); return nullptr; }
-  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, ws, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
+  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
+  e = make_chunks(env, default_chunks(n_envs));
+  if (e != hipSuccess) {
+    (void)free_chunks(env);
+    (void)hipFree(dm);
+    delete env;
+    fail_hip("so100_create: workspace", e);
+    return nullptr;
+  }
   return env;
 }
 
@@ -267,7 +366,7 @@ int so100_destroy(so100_env* env) {
   DeviceGuard g(env->device);
   profile_free(env);
   hipError_t e = hipFree(env->d_model);
-  hipError_t e2 = so100::free_workspace(&env->ws);
+  hipError_t e2 = free_chunks(env);
   if (e == hipSuccess) e = e2;
   delete env;
   return e == hipSuccess ? 0 : fail_hip("so100_destroy", e);
@@ -313,8 +412,29 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
   hipEvent_t* ev = nullptr;
   const int per = 2 * env->nsubstep + 2;
   if (env->prof_used < env->prof_cap) ev = env->prof_ev.data() + (size_t)(env->prof_used++) * per;
-  hipError_t e = so100::launch_step(env->d_model, env->nsubstep, env->ws, *b, env->n, env->task, flags, env->max_steps,
-                                    env->base_seed, env->env_offset, (hipStream_t)stream, ev);
+  const hipStream_t s = (hipStream_t)stream;
+  if (env->chunks.size() == 1) {
+    Chunk& c = env->chunks[0];
+    hipError_t e = so100::launch_step(env->d_model, env->nsubstep, c.ws, *b, c.count, env->task, flags, env->max_steps,
+                                      env->base_seed, env->env_offset, s, ev);
+    return e == hipSuccess ? 0 : fail_hip("so100_step", e);
+  }
+  // fork: chunks 1.. wait for the caller's prior work, chunk 0 runs on the caller's stream; join: the
+  // caller's stream waits for every other chunk.  The profiling events (if any) ride on chunk 0.
+  hipError_t e = hipEventRecord(env->fork, s);
+  for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) {
+    Chunk& c = env->chunks[k];
+    e = hipStreamWaitEvent(c.s, env->fork, 0);
+    if (e == hipSuccess)
+      e = so100::launch_step(env->d_model, env->nsubstep, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
+                             env->max_steps, env->base_seed, env->env_offset + c.start, c.s, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(c.done, c.s);
+  }
+  Chunk& c0 = env->chunks[0];
+  if (e == hipSuccess)
+    e = so100::launch_step(env->d_model, env->nsubstep, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
+                           env->base_seed, env->env_offset, s, ev);
+  for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) e = hipStreamWaitEvent(s, env->chunks[k].done, 0);
   return e == hipSuccess ? 0 : fail_hip("so100_step", e);
 }
 
@@ -356,10 +476,19 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
   return 0;
 }
 
+int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs) {
+  if (!env) return fail("so100_chunk_info: env is NULL");
+  if (nchunks) *nchunks = (int)env->chunks.size();
+  if (profiled_envs) *profiled_envs = env->chunks.empty() ? 0 : env->chunks[0].count;
+  return 0;
+}
+
 int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
   if (!env || !accum) return fail("so100_contact_count: bad arguments");
   DeviceGuard g(env->device);
-  hipError_t e = so100::launch_contact_count(env->ws, env->n, accum, (hipStream_t)stream);
+  hipError_t e = hipSuccess;
+  for (const Chunk& c : env->chunks)
+    if (e == hipSuccess) e = so100::launch_contact_count(c.ws, c.count, accum, (hipStream_t)stream);
   return e == hipSuccess ? 0 : fail_hip("so100_contact_count", e);
 }
 

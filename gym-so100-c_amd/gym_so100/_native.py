@@ -32,7 +32,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 2          # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 3          # include/so100.h SO100_ABI_VERSION
 
 
 def load():
@@ -61,9 +61,10 @@ def load():
     lib.so100_profile_enable.argtypes = [_P, ctypes.c_int]
     lib.so100_profile_read.argtypes = [_P, _P, _P, _P, _P]
     lib.so100_contact_count.argtypes = [_P, _P, _P]
+    lib.so100_chunk_info.argtypes = [_P, _P, _P]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
-               "so100_profile_enable", "so100_profile_read", "so100_contact_count"):
+               "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
     lib.so100_struct_sizes.restype = ctypes.c_int
@@ -82,7 +83,7 @@ def load():
 EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
-                    "so100_contact_count")
+                    "so100_contact_count", "so100_chunk_info")
 
 
 def check(rc, what):

@@ -289,6 +289,12 @@ class SO100VecEnv:
                                                   ctypes.byref(tm), ctypes.byref(tn)), "so100_profile_read")
         return sm.value, sn.value, tm.value, tn.value
 
+    def chunk_info(self):
+        """(chunks, envs of chunk 0): the env split of a step; profile_read times chunk 0's launches."""
+        k, n0 = ctypes.c_int(0), ctypes.c_int(0)
+        _native.check(self.lib.so100_chunk_info(self._handle, ctypes.byref(k), ctypes.byref(n0)), "so100_chunk_info")
+        return k.value, n0.value
+
     def contact_count(self, accum):
         """accum (int64 device tensor, 1 element) += contacts in the last solver launch, summed over envs."""
         _native.check(self.lib.so100_contact_count(self._handle, _native.ptr(accum), self._stream()),

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 2
+#define SO100_ABI_VERSION 3
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -89,17 +89,24 @@ int so100_configure(so100_env* env, int task, int max_episode_steps, uint64_t ba
 int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, const uint32_t* seeds,
                 void* stream);
 
-/* One env step for all N envs (10 physics substeps + final position stage + reward/obs epilogue). */
+/* One env step for all N envs (10 physics substeps + final position stage + reward/obs epilogue).
+ * The N envs are split into up to 4 contiguous chunks (so100_chunk_info) whose launch sequences run
+ * concurrently on internal streams forked from and joined back to `stream`: from the caller's side
+ * the step is one ordered operation on `stream`. */
 int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream);
 
 /* Kernel timing for the benchmark's roofline (not needed for stepping).  so100_profile_enable(env,
  * max_steps) allocates HIP events for up to max_steps subsequent so100_step calls (0 frees them and
  * stops recording); while enabled each step records an event on its stream before its first launch
- * and after every launch (stage / solver kernels).  so100_profile_read synchronises on the last event
- * and returns the summed device time of the solver and of the stage launches since enabling. */
+ * and after every launch (stage / solver kernels) of the first chunk.  so100_profile_read synchronises
+ * on the last event and returns the summed device time of the solver and of the stage launches since
+ * enabling. */
 int so100_profile_enable(so100_env* env, int max_steps);
 int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms,
                        int* stage_launches);
+
+/* Number of env chunks and the env count of chunk 0 (the launches so100_profile_read times). */
+int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs);
 
 /* Adds the contact count of the last solver launch, summed over the N envs, to *accum (DEVICE
  * uint64).  Enqueued on `stream`, no synchronisation. */

@@ -215,6 +215,34 @@ def test_sharding_invariance():
     assert torch.equal(full.obs, torch.cat([a0.obs, a1.obs]))
 
 
+def test_chunking_invariance(monkeypatch):
+    """The env-range chunks of a step (concurrent streams, so100_capi.cpp) change nothing: 4 ragged
+    chunks == 1 chunk, bitwise, through auto-resets and the solver's debug record."""
+    from gym_so100 import SO100VecEnv
+    n = 4160
+    kw = dict(device="cuda:0", seed=4, max_episode_steps=5, debug=True)
+    monkeypatch.setenv("SO100_CHUNKS", "1")
+    one = SO100VecEnv(n, **kw)
+    monkeypatch.setenv("SO100_CHUNKS", "4")
+    four = SO100VecEnv(n, **kw)
+    assert one.chunk_info() == (1, n)
+    k, n0 = four.chunk_info()
+    assert k == 4 and n0 < n
+    for e in (one, four):
+        e.reset()
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(12):
+        a = torch.rand(n, 6, generator=g, device="cuda") * 2 - 1
+        r1 = one.step(a)
+        r4 = four.step(a)
+        torch.cuda.synchronize()
+        assert torch.equal(r1[1], r4[1]) and torch.equal(r1[2], r4[2]) and torch.equal(r1[3], r4[3])
+    for name in ("qpos", "qvel", "qacc_warmstart", "obs", "debug"):
+        assert torch.equal(getattr(one, name), getattr(four, name)), name
+    one.close()
+    four.close()
+
+
 def test_goal_env_semantics():
     from gym_so100 import SO100VecEnv
     env = SO100VecEnv(32, task="so100_goal", device="cuda:0", seed=2)
