@@ -33,6 +33,8 @@ BYTES_PER_ENV_STEP = 408
 SOLVER_BYTES_PER_ENV = 640 + 48
 SOLVER_BYTES_PER_CONTACT = 160 + 192
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+CLOCK_HZ = 2.4e9             # MI355X peak engine clock (valu_busy uses it: a lower real clock only raises the share)
+SIMDS = 1024                 # 256 CUs x 4 SIMDs
 
 
 def shard(total, world, rank):
@@ -89,17 +91,19 @@ def cpu_baseline(seconds):
 
 
 def load_traffic(n_envs):
-    """HBM traffic per solver launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    """(HBM bytes per solver launch of n_envs envs, VALU wave-instructions per env step) from the
+    committed rocprofv3 PMC passes (profiles/pmc_traffic.json, tests/_pmc_traffic.py), or (None, None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         d = json.load(open(path))
         if int(d.get("n_envs", -1)) != n_envs:
-            return None
-        return float(d["hbm_bytes_per_launch"])
+            return None, None
+        v = d.get("valu_insts_per_step")
+        return float(d["hbm_bytes_per_launch"]), (float(v) if v else None)
     except Exception:
-        return None
+        return None, None
 
 
 def main(argv=None):
@@ -185,7 +189,9 @@ def main(argv=None):
         nchunks, n0 = env.chunk_info()
         solver_bytes = n0 * (SOLVER_BYTES_PER_ENV + SOLVER_BYTES_PER_CONTACT * contacts_per_env)
         achieved = solver_bytes / (solver_ms * 1e-3)
-        traffic = load_traffic(n0)
+        traffic, valu_insts = load_traffic(n0)
+        # VALU issue share of the timed run: insts x 2 cyc (wave64 on SIMD-32) / (step x 2.4 GHz x 1024 SIMDs)
+        valu_busy = valu_insts * 2.0 / (step_ms * 1e-3 * CLOCK_HZ * SIMDS) if valu_insts else None
         line = {
             "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
@@ -197,14 +203,16 @@ def main(argv=None):
                        "pgs_iterations": env.model.iterations, "parallelism": f"env-sharded x{world}, no collectives",
                        "actions": "U[-1,1]^6 pool resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK, "traffic": traffic, "valu_busy": valu_busy,
                          "kernel": "so100_pgs_kernel", "kernel_ms": solver_ms,
                          "bytes_per_launch": solver_bytes, "envs_per_launch": n0, "concurrent_chunks": nchunks,
                          "contacts_per_env": contacts_per_env,
                          "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
                          "boundary_bytes_per_env_step": BYTES_PER_ENV_STEP,
                          "note": ("solver = serial Gauss-Seidel chains per env: issue/latency-bound, not HBM-bound "
-                                  "(DESIGN.md §6); traffic = measured PMC bytes per solver launch")},
+                                  "(DESIGN.md §3.5); traffic = measured PMC bytes per solver launch; valu_busy = PMC SQ_INSTS_VALU "
+                                  "per step x 2 cyc / (step time x 2.4 GHz x 1024 SIMDs): VALU issue share beside the HBM share "
+                                  "(SURVEY §8d)")},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

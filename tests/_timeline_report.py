@@ -5,7 +5,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv
-n = 65536
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 env = SO100VecEnv(n, device="cuda:0", debug=True)
 env.reset(seed=1000)
 g = torch.Generator(device="cuda").manual_seed(0)

@@ -80,3 +80,11 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h", "Makefile")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert not pat.search(txt), os.path.join(dirpath, f)
+
+
+def test_sb3_adapter_interface():
+    """The SB3 adapter exposes SB3's VecEnv surface (constructed only on a GPU: test_gpu_sb3.py)."""
+    from gym_so100.sb3 import SO100SB3VecEnv
+    for name in ("reset", "step_async", "step_wait", "step", "close", "seed", "get_attr", "set_attr",
+                 "env_method", "env_is_wrapped", "get_images"):
+        assert callable(getattr(SO100SB3VecEnv, name)), name
