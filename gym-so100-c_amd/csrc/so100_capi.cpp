@@ -214,8 +214,16 @@ int build_device_model(const so100_model* s, DevModel* d) {
     if (fabs(s->body_ipos[SO100_CUBE_BODY][k]) > 1e-12) return fail("model: cube COM must be at the body origin");
   if (fabs(s->body_iquat[SO100_CUBE_BODY][0] - 1) > 1e-12) return fail("model: cube inertia must be body-aligned");
   if (s->site_ee_body != 6 || s->site_cube_body != SO100_CUBE_BODY) return fail("model: unexpected site bodies");
-  for (int p = 0; p < SO100_NPAIR; p++)
-    if (s->pair_condim[p] != SO100_CONDIM) return fail("model: every pair must have condim 4");
+  for (int p = 0; p < SO100_NPAIR_BOX; p++)
+    if (s->pair_condim[p] != 4) return fail("model: box-box pairs must have condim 4");
+  for (int p = SO100_NPAIR_BOX; p < SO100_NPAIR; p++) {
+    const int k = p - SO100_NPAIR_BOX;
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: hull pairs must have condim 3 or 4");
+    if (s->pair_body1[p] != 0 || s->pair_body2[p] != s->hull_body[k]) return fail("model: hull pair k must be (table, hull k)");
+    if (s->hull_body[k] < 2 || s->hull_body[k] > 7) return fail("model: hulls must sit on arm bodies 2..7");
+    if (s->hull_start[k] < 0 || s->hull_count[k] < 1 || s->hull_start[k] + s->hull_count[k] > SO100_HULL_NVERT)
+      return fail("model: hull vertex range out of bounds");
+  }
   for (int g = 0; g < SO100_NGEOM; g++) {
     int b = s->geom_body[g];
     if (!(b == 0 || b == 6 || b == 7 || b == SO100_CUBE_BODY)) return fail("model: geoms must be static, on the jaws or the cube");
@@ -294,9 +302,29 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->pair_mu0[p] = (float)s->pair_friction[p][0];
     d->pair_mu1[p] = (float)s->pair_friction[p][1];
     d->pair_margin[p] = (float)s->pair_margin[p];
-    int b1 = s->geom_body[s->pair_geom1[p]], b2 = s->geom_body[s->pair_geom2[p]];
+    const int b1 = s->pair_body1[p], b2 = s->pair_body2[p];
+    if (b1 < 0 || b1 >= SO100_NBODY || b2 < 0 || b2 >= SO100_NBODY) return fail("model: pair body out of range");
+    d->pair_b1[p] = b1;
+    d->pair_b2[p] = b2;
+    d->pair_cond4[p] = s->pair_condim[p] == 4;
+    d->pair_arm[p] = (b1 >= 2 && b1 <= 7) || (b2 >= 2 && b2 <= 7);
+    d->pair_cube[p] = b1 == SO100_CUBE_BODY || b2 == SO100_CUBE_BODY;
     d->pair_tran[p] = (float)(s->body_invweight0[b1][0] + s->body_invweight0[b2][0]);
     d->pair_rot[p] = (float)(s->body_invweight0[b1][1] + s->body_invweight0[b2][1]);
+  }
+  for (int k = 0; k < SO100_NHULL; k++) {
+    d->hull_body[k] = s->hull_body[k];
+    d->hull_start[k] = s->hull_start[k];
+    d->hull_count[k] = s->hull_count[k];
+    d->hull_center[k] = {(float)s->hull_center[k][0], (float)s->hull_center[k][1], (float)s->hull_center[k][2], 0.f};
+    d->hull_half[k] = {(float)s->hull_half[k][0], (float)s->hull_half[k][1], (float)s->hull_half[k][2], 0.f};
+  }
+  for (int v = 0; v < SO100_HULL_NVERT; v++)
+    d->hull_vert[v] = {(float)s->hull_vert[v][0], (float)s->hull_vert[v][1], (float)s->hull_vert[v][2], 0.f};
+  d->table_top = (float)s->table_top;
+  for (int k = 0; k < 2; k++) {
+    d->table_lo[k] = (float)s->table_lo[k];
+    d->table_hi[k] = (float)s->table_hi[k];
   }
   for (int k = 0; k < 3; k++) {
     d->site_cube[k] = (float)s->site_cube_pos[k];

@@ -5,6 +5,8 @@
 
 namespace so100 {
 
+struct alignas(16) float4_t { float x, y, z, w; };   // host-visible float4 (the device reads it as float4)
+
 constexpr int kLanes = 16;            // lanes per env ("env lane-group" = one DPP row)
 constexpr int kEnvsPerBlock = 4;      // one wave64 per workgroup
 constexpr int kThreads = kLanes * kEnvsPerBlock;
@@ -59,13 +61,23 @@ struct DevModel {
   float geom_mat[SO100_NGEOM][9];
   float geom_size[SO100_NGEOM][3];
 
-  // pairs
+  // pairs (0..13 box-box, 14..22 table-hull)
   int pair_g1[SO100_NPAIR], pair_g2[SO100_NPAIR];
+  int pair_b1[SO100_NPAIR], pair_b2[SO100_NPAIR];
+  int pair_cond4[SO100_NPAIR];      // 1: condim 4 (torsion row), 0: condim 3 (J row 3 zero)
+  int pair_arm[SO100_NPAIR];        // a body of the pair is an arm link: J has arm entries
+  int pair_cube[SO100_NPAIR];       // the cube is in the pair: the DR friction scale applies
   float pair_K[SO100_NPAIR], pair_B[SO100_NPAIR];
   float pair_solimp[SO100_NPAIR][5];
   float pair_mu0[SO100_NPAIR], pair_mu1[SO100_NPAIR];
   float pair_margin[SO100_NPAIR];
   float pair_tran[SO100_NPAIR], pair_rot[SO100_NPAIR];   // diagApprox (body invweight sums)
+
+  // arm/jaw collision hulls vs the table top (body-frame vertices and bounding box: center, half extents)
+  int hull_body[SO100_NHULL], hull_start[SO100_NHULL], hull_count[SO100_NHULL];
+  float4_t hull_center[SO100_NHULL], hull_half[SO100_NHULL];
+  float4_t hull_vert[SO100_HULL_NVERT];
+  float table_top, table_lo[2], table_hi[2];
 
   // sites
   float site_cube[3];               // cube body frame

@@ -919,6 +919,73 @@ DEV void collide_pair(const DevModel* __restrict__ m, const EnvShared& sh, int p
   box_box(p1, R1, A, p2, R2, B, margin, pc);
 }
 
+// Arm/jaw hulls vs the table top (pairs SO100_NPAIR_BOX + k; oracle collision()): hull k's lowest
+// vertex inside the top face's x-y footprint, a contact when it is below the top.
+//  * broadphase, in parallel: lane k < SO100_NHULL of each env tests hull k's body-frame bounding box
+//    against the top; only hulls that are candidates in some env of the wave are scanned;
+//  * scan: the 16 lanes of the env's row split the vertices (lane, lane + 16, ...) and a 16-lane
+//    lexicographic (z, vertex index) min gives the oracle's first lowest vertex.
+// Needs the link frames of fk_stage (sh.ser.xm / xp).  Lane k < SO100_NHULL returns hull k's contact
+// flag and its lowest vertex.
+DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lane, int grp, bool valid, float& hx,
+                    float& hy, float& hz) {
+  bool found = false;
+  hx = hy = hz = 0.f;
+#ifdef SO100_EXPERIMENT_NO_HULLS
+  return false;   // timing experiment only: hull contacts off
+#endif
+  const float top = m->table_top;
+  bool cand = false;
+  if (valid && lane < SO100_NHULL) {
+    const int a = m->hull_body[lane] - 2;
+    const float4 hc = reinterpret_cast<const float4*>(m->hull_center)[lane];
+    const float4 hh = reinterpret_cast<const float4*>(m->hull_half)[lane];
+    const float r6 = sh.ser.xm[a][6], r7 = sh.ser.xm[a][7], r8 = sh.ser.xm[a][8];
+    const float cz = (r6 * hc.x + r7 * hc.y + r8 * hc.z) + sh.ser.xp[a][2];
+    const float ext = fabsf(r6) * hh.x + fabsf(r7) * hh.y + fabsf(r8) * hh.z;
+    cand = cz - ext < top + m->pair_margin[SO100_NPAIR_BOX + lane];
+  }
+  const uint64_t cm = __ballot(cand);
+  const uint32_t env_cand = (uint32_t)(cm >> (grp * 16)) & 0xFFFFu;
+  uint32_t wave_cand = (uint32_t)((cm | (cm >> 16) | (cm >> 32) | (cm >> 48)) & 0xFFFFull);
+  const float lo0 = m->table_lo[0], lo1 = m->table_lo[1], hi0 = m->table_hi[0], hi1 = m->table_hi[1];
+  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert);
+  while (wave_cand) {
+    const int k = __builtin_ctz(wave_cand);
+    wave_cand &= wave_cand - 1u;
+    const bool mine = (env_cand >> k) & 1u;
+    float bz = __builtin_inff(), bx = 0.f, by = 0.f;
+    int bi = 0x7fffffff;
+    if (mine) {
+      const int a = m->hull_body[k] - 2;
+      const float* R = sh.ser.xm[a];
+      const float* P = sh.ser.xp[a];
+      const float r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5], r6 = R[6], r7 = R[7], r8 = R[8];
+      const float p0 = P[0], p1 = P[1], p2 = P[2];
+      const int n = m->hull_count[k], s0 = m->hull_start[k];
+      for (int i = lane; i < n; i += kLanes) {
+        const float4 v = verts[s0 + i];
+        const float wx = (r0 * v.x + r1 * v.y + r2 * v.z) + p0;
+        const float wy = (r3 * v.x + r4 * v.y + r5 * v.z) + p1;
+        const float wz = (r6 * v.x + r7 * v.y + r8 * v.z) + p2;
+        const bool in = wx >= lo0 && wx <= hi0 && wy >= lo1 && wy <= hi1;
+        if (in && wz < bz) { bz = wz; bx = wx; by = wy; bi = i; }
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < kLanes; off <<= 1) {
+      const float oz = __shfl_xor(bz, off, kLanes), ox = __shfl_xor(bx, off, kLanes), oy = __shfl_xor(by, off, kLanes);
+      const int oi = __shfl_xor(bi, off, kLanes);
+      if (oz < bz || (oz == bz && oi < bi)) { bz = oz; bx = ox; by = oy; bi = oi; }
+    }
+    if (lane == k) {
+      found = mine && bi != 0x7fffffff && (bz - top < m->pair_margin[SO100_NPAIR_BOX + k]);
+      hx = bx; hy = by; hz = bz;
+    }
+  }
+  return found;
+}
+
 DEV void make_frame(float* f) {
   float* n = f;
   float* t1 = f + 3;
@@ -983,7 +1050,7 @@ DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int 
   float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
 #pragma unroll
   for (int side = 0; side < 2; side++) {
-    const int b = m->geom_body[side ? m->pair_g2[p] : m->pair_g1[p]];
+    const int b = side ? m->pair_b2[p] : m->pair_b1[p];
     const float sg = side ? 1.f : -1.f;
     if (lane < 6) {
       if (b >= 2 && b <= 7 && lane + 2 <= b) {
@@ -1007,8 +1074,12 @@ DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int 
       }
     }
   }
+  // condim 3 (hull-table): no torsion row.  A zero 4th row makes the 4-row block exactly the condim-3
+  // block: its A row/column is R3 on the diagonal only, the eigen-component it adds to the QCQP carries
+  // c = w = 0, and its force stays 0 (so100_pgs.hip)
+  const float jt = m->pair_cond4[p] ? fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2] : 0.f;
   return make_float4(fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2], fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2],
-                     fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2], fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2]);
+                     fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2], jt);
 }
 
 // Symmetric 3x3 eigen-decomposition by cyclic Jacobi (5 sweeps: quadratic convergence reaches fp32
@@ -1206,10 +1277,14 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     dynamics_par(m, sh, lane, mscale);
     __syncthreads();
     SSTAMP(1);
-    // ---------------- S3: collision, one pair per lane, compaction in pair order
+    // ---------------- S3: collision: hulls vs the table (lane k = hull k), one box pair per lane;
+    // compaction in pair order (box pairs, then hull pairs)
+    float hx, hy, hz;
+    const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
+    const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
     PairContacts pc;
     pc.n = 0;
-    if (lane < SO100_NPAIR) collide_pair(m, sh, lane, pc);
+    if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
     sh.cnt[lane] = pc.n;
     __syncthreads();
     {
@@ -1230,6 +1305,19 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
           sh.con_pair[slot] = lane;
         }
       }
+      const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
+      if (hfound && hslot < kMaxCon) {
+        float fr[9] = {0.f, 0.f, 1.f, 0, 0, 0, 0, 0, 0};
+        make_frame(fr);
+#pragma unroll
+        for (int t = 0; t < 9; t++) sh.con[hslot].g.frame[t] = fr[t];
+        const float top = m->table_top;
+        sh.con[hslot].g.pos[0] = hx; sh.con[hslot].g.pos[1] = hy;
+        sh.con[hslot].g.pos[2] = 0.5f * (hz + top); sh.con[hslot].g.pos[3] = hz - top;
+        sh.con_dist[hslot] = hz - top;
+        sh.con_pair[hslot] = SO100_NPAIR_BOX + lane;
+      }
+      tot += __popc(hrow);
       if (lane == 0) sh.ncon = tot < kMaxCon ? tot : kMaxCon;
     }
     __syncthreads();
@@ -1336,7 +1424,8 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
       const float dist = sh.con_dist[lane];
       const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
       const float K = m->pair_K[p], Bd = m->pair_B[p];
-      const float mu0 = m->pair_mu0[p] * fscale, mu1 = m->pair_mu1[p] * fscale;
+      const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
+      const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
       float R[4];
       R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
       R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
@@ -1398,7 +1487,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
       cs[4] = make_float4(P[2][0], P[2][1], P[2][2], lam[0]);
       cs[5] = make_float4(lam[1], lam[2], 1.f / lam[0], 1.f / lam[1]);
       cs[6] = make_float4(1.f / lam[2], R[0], 1.f / ar[0], R[1]);
-      cs[kBlkFlags] = make_float4(R[3], p < SO100_NPAIR_GRIPPER ? 1.f : 0.f, 0.f, 0.f);
+      cs[kBlkFlags] = make_float4(R[3], m->pair_arm[p] ? 1.f : 0.f, 0.f, 0.f);
       cs[kBlkAref] = make_float4(aref[0], aref[1], aref[2], aref[3]);
 #pragma unroll
       for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
@@ -1490,11 +1579,14 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
   __syncthreads();
   if (lane == 0) fk_stage(m, sh);
   __syncthreads();
+  float hx, hy, hz;
+  const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
+  const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
   PairContacts pc;
   pc.n = 0;
-  if (lane < SO100_NPAIR) collide_pair(m, sh, lane, pc);
+  if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
   const uint64_t hit = __ballot(pc.n > 0);
-  const uint32_t bits = (uint32_t)((hit >> (grp * 16)) & 0xFFFFull);
+  const uint32_t bits = (uint32_t)((hit >> (grp * 16)) & 0x3FFFull) | (hrow << SO100_NPAIR_BOX);
 
   // divergence check (dm_control PhysicsError analogue)
   bool bad = (lane < SO100_NQ) && !(fabsf(qpos_r) < 1e4f);

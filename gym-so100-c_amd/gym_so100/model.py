@@ -15,7 +15,9 @@ from . import constants as C
 
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so100_model.json")
 
-NBODY, NHINGE, NQ, NV, NU, NGEOM, NPAIR = 9, 6, 13, 12, 6, 15, 14
+NBODY, NHINGE, NQ, NV, NU, NGEOM = 9, 6, 13, 12, 6, 15
+NPAIR_BOX, NHULL, HULL_NVERT = 14, 9, 2560
+NPAIR = NPAIR_BOX + NHULL
 MAXCON, CONDIM, NOBS = 16, 4, 15
 NEFC_MAX = NV + NHINGE + MAXCON * CONDIM
 
@@ -45,9 +47,14 @@ class SO100Model(ctypes.Structure):
         ("act_ctrlrange", _arr(_d, NU, 2)),
         ("geom_body", _arr(_i, NGEOM)), ("geom_pos", _arr(_d, NGEOM, 3)), ("geom_quat", _arr(_d, NGEOM, 4)),
         ("geom_size", _arr(_d, NGEOM, 3)),
-        ("pair_geom1", _arr(_i, NPAIR)), ("pair_geom2", _arr(_i, NPAIR)), ("pair_condim", _arr(_i, NPAIR)),
+        ("pair_geom1", _arr(_i, NPAIR)), ("pair_geom2", _arr(_i, NPAIR)),
+        ("pair_body1", _arr(_i, NPAIR)), ("pair_body2", _arr(_i, NPAIR)), ("pair_condim", _arr(_i, NPAIR)),
         ("pair_friction", _arr(_d, NPAIR, 3)), ("pair_solref", _arr(_d, NPAIR, 2)),
         ("pair_solimp", _arr(_d, NPAIR, 5)), ("pair_margin", _arr(_d, NPAIR)),
+        ("hull_body", _arr(_i, NHULL)), ("hull_start", _arr(_i, NHULL)), ("hull_count", _arr(_i, NHULL)),
+        ("hull_center", _arr(_d, NHULL, 3)), ("hull_half", _arr(_d, NHULL, 3)),
+        ("hull_vert", _arr(_d, HULL_NVERT, 3)),
+        ("table_top", _d), ("table_lo", _arr(_d, 2)), ("table_hi", _arr(_d, 2)),
         ("site_cube_body", _i), ("site_cube_pos", _arr(_d, 3)), ("site_ee_body", _i), ("site_ee_pos", _arr(_d, 3)),
         ("bin_center", _arr(_d, 3)),
         ("start_qpos", _arr(_d, NU)), ("action_lo", _arr(_d, NU)), ("action_hi", _arr(_d, NU)),
@@ -112,6 +119,26 @@ def build_model(path=ASSET, iterations=None, nsubstep=None):
     _set(m, "pair_solref", np.asarray([x["solref"] for x in p]))
     _set(m, "pair_solimp", np.asarray([x["solimp"] for x in p]))
     _set(m, "pair_margin", np.asarray([x["margin"] - x["gap"] for x in p]))
+    _set(m, "pair_body1", np.asarray([x["body1"] for x in p], dtype=np.int64))
+    _set(m, "pair_body2", np.asarray([x["body2"] for x in p], dtype=np.int64))
+    h = d["hulls"]
+    assert len(h) == NHULL and len(p) == NPAIR
+    counts = [len(x["verts"]) for x in h]
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    verts = np.zeros((HULL_NVERT, 3))
+    allv = np.concatenate([np.asarray(x["verts"]) for x in h])
+    assert len(allv) <= HULL_NVERT
+    verts[:len(allv)] = allv
+    _set(m, "hull_body", np.asarray([x["body"] for x in h], dtype=np.int64))
+    _set(m, "hull_start", starts)
+    _set(m, "hull_count", np.asarray(counts, dtype=np.int64))
+    _set(m, "hull_center", np.asarray([x["center"] for x in h]))
+    _set(m, "hull_half", np.asarray([x["half"] for x in h]))
+    _set(m, "hull_vert", verts)
+    tp = d["table_plane"]
+    m.table_top = tp["top"]
+    _set(m, "table_lo", tp["lo"])
+    _set(m, "table_hi", tp["hi"])
     m.site_cube_body = d["site_cube"]["body"]
     _set(m, "site_cube_pos", d["site_cube"]["pos"])
     m.site_ee_body = d["site_ee"]["body"]

@@ -14,6 +14,9 @@ reference.  It restates what MuJoCo's compiler does for the parts of
 * collision boxes: finger pads (so_arm100.xml:60-62,113-120,139-146), cube (transfer_cube.xml:10-11),
   bin walls/floor (transfer_cube.xml:18-22), table = 8-vertex box hull of tabletop.stl
   (scene_so100.xml:3,20) emitted as an exact box
+* arm/jaw collision hulls: qhull convex hulls (scipy) of the class="collision" meshes on the moving arm
+  bodies (so_arm100.xml:79,87,95,103,111-112,136-138), vertices in the body frame, for the
+  hull-vs-table contacts; pair parameters mixed like the box pairs
 * contact-pair parameter mixing (MuJoCo mj_contactParam semantics, restated): condim=max,
   friction=elementwise max, solref/solimp = solmix-weighted mean (solmix defaults 1 -> mean)
 * setConst quantities at qpos0 (MuJoCo mj_setConst, restated): dof_M0 (diag of M incl. armature),
@@ -344,21 +347,54 @@ def compile_model():
         add_geom(g["name"], 0, binb["pos"] + vec(g["pos"], 3), [1, 0, 0, 0], vec(g["size"], 3), g)
     gid = {g["name"]: i for i, g in enumerate(geoms)}
 
+    # ---- arm/jaw collision hulls (convex hulls of the class="collision" meshes of the moving bodies) ----
+    from scipy.spatial import ConvexHull
+    hulls = []
+    for bname in ARM_BODIES[1:]:
+        for g in bodies[bname]["geoms"]:
+            if g.get("type") != "mesh" or g.get("group") != "3" or g.get("contype", "1") == "0":
+                continue
+            v = load_stl(os.path.join(ASSETS, "trs_so_arm100", g["mesh"] + ".stl"))
+            pos = vec(g.get("pos", "0 0 0"), 3)
+            assert not g.get("quat") and not g.get("euler"), "collision mesh with a rotated frame"
+            hv = v[ConvexHull(v).vertices] + pos
+            lo, hi = hv.min(0), hv.max(0)
+            c = (lo + hi) / 2
+            hulls.append(dict(name=g["mesh"], body=bid[bname], verts=hv.tolist(), center=c.tolist(),
+                              half=((hi - lo) / 2).tolist(),
+                              condim=int(g.get("condim", MJ_CONDIM)),
+                              friction=(vec(g["friction"]).tolist() if "friction" in g else MJ_FRICTION),
+                              solref=(vec(g["solref"]).tolist() if "solref" in g else MJ_SOLREF),
+                              solimp=((vec(g["solimp"]).tolist() + MJ_SOLIMP[3:])[:5] if "solimp" in g
+                                      else MJ_SOLIMP)))
+    tbl = geoms[gid["table"]]
+    table_plane = dict(top=tbl["pos"][2] + tbl["size"][2],
+                       lo=[tbl["pos"][0] - tbl["size"][0], tbl["pos"][1] - tbl["size"][1]],
+                       hi=[tbl["pos"][0] + tbl["size"][0], tbl["pos"][1] + tbl["size"][1]])
+
     # ---- contact pairs (geom1, geom2 in MuJoCo's orientation: type order box<mesh, then id) ----
     pair_names = ([(f"fixed_jaw_pad_{i}", "red_box") for i in range(1, 5)]
                   + [(f"moving_jaw_pad_{i}", "red_box") for i in range(1, 5)]
                   + [("red_box", "table")]
                   + [("red_box", n) for n in ("bin_wall", "bin_wall2", "bin_wall3", "bin_wall4", "bin_floor")])
     pairs = []
+
+    def mixed(g1, g2):
+        mix = 0.5   # solmix defaults 1 and 1
+        return dict(condim=max(g1["condim"], g2["condim"]),
+                    friction=[max(a, b) for a, b in zip(g1["friction"], g2["friction"])],
+                    solref=[mix * a + (1 - mix) * b for a, b in zip(g1["solref"], g2["solref"])],
+                    solimp=[mix * a + (1 - mix) * b for a, b in zip(g1["solimp"], g2["solimp"])],
+                    margin=0.0, gap=0.0)
+
     for n1, n2 in pair_names:
         g1, g2 = geoms[gid[n1]], geoms[gid[n2]]
-        mix = 0.5   # solmix defaults 1 and 1
-        pairs.append(dict(g1=gid[n1], g2=gid[n2], name1=n1, name2=n2,
-                          condim=max(g1["condim"], g2["condim"]),
-                          friction=[max(a, b) for a, b in zip(g1["friction"], g2["friction"])],
-                          solref=[mix * a + (1 - mix) * b for a, b in zip(g1["solref"], g2["solref"])],
-                          solimp=[mix * a + (1 - mix) * b for a, b in zip(g1["solimp"], g2["solimp"])],
-                          margin=0.0, gap=0.0))
+        pairs.append(dict(g1=gid[n1], g2=gid[n2], body1=g1["body"], body2=g2["body"], name1=n1, name2=n2,
+                          **mixed(g1, g2)))
+    # (table, hull k): geom1 = the table (world geom, lower id), normal from the table to the hull
+    for k, h in enumerate(hulls):
+        pairs.append(dict(g1=gid["table"], g2=-1 - k, body1=0, body2=h["body"], name1="table", name2=h["name"],
+                          hull=k, **mixed(tbl, h)))
 
     # ---- sites ----
     cube_site = vec(bodies["box"]["sites"][0]["pos"], 3)
@@ -376,7 +412,7 @@ def compile_model():
         dof_armature=dof_armature, dof_frictionloss=dof_frictionloss, dof_invweight0=dof_invweight0,
         dof_M0=dof_M0, dof_solref=MJ_SOLREF, dof_solimp=MJ_SOLIMP,
         act_kp=act_kp, act_kv=act_kv, act_forcerange=act_forcerange, act_ctrlrange=act_ctrlrange,
-        geoms=geoms, pairs=pairs,
+        geoms=geoms, pairs=pairs, hulls=hulls, table_plane=table_plane,
         site_cube=dict(body=bid["box"], pos=cube_site.tolist()),
         site_ee=dict(body=bid["Fixed_Jaw"], pos=ee_site.tolist()),
         site_bin_center=bin_center.tolist(),

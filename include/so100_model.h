@@ -12,7 +12,10 @@
  *          6..8 cube linear (world frame), 9..11 cube angular (body frame)  (MuJoCo free-joint layout)
  *   qpos   0..5 hinges, 6..8 cube position, 9..12 cube quaternion (w,x,y,z)
  *   geoms  0 table | 1..4 fixed_jaw_pad_1..4 | 5..8 moving_jaw_pad_1..4 | 9 red_box | 10..14 bin walls+floor
- *   pairs  0..7 pad-vs-red_box | 8 (red_box, table) | 9..13 (red_box, bin_*)
+ *   pairs  0..7 pad-vs-red_box | 8 (red_box, table) | 9..13 (red_box, bin_*)   (box-box)
+ *          14..22 (table, hull k): arm/jaw collision hulls vs the table top
+ *   hulls  0 Rotation_Pitch | 1 Upper_Arm | 2 Lower_Arm | 3 Wrist_Pitch_Roll |
+ *          4..5 Fixed_Jaw_Collision_1..2 | 6..8 Moving_Jaw_Collision_1..3
  */
 #ifndef SO100_MODEL_H
 #define SO100_MODEL_H
@@ -23,14 +26,17 @@
 #define SO100_NV 12
 #define SO100_NU 6
 #define SO100_NGEOM 15
-#define SO100_NPAIR 14
+#define SO100_NPAIR_BOX 14         /* box-box pairs 0..13 */
+#define SO100_NHULL 9               /* arm/jaw collision hulls */
+#define SO100_NPAIR (SO100_NPAIR_BOX + SO100_NHULL)   /* + (table, hull k) pairs 14..22 */
+#define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_CUBE_BODY 8
 #define SO100_CUBE_GEOM 9
 #define SO100_PAIR_TABLE 8          /* ("red_box", "table") — single_arm.py:354 touch_table */
 #define SO100_NPAIR_GRIPPER 8       /* pairs 0..7 — single_arm.py:348-352 touch_gripper   */
 #define SO100_MAXCONPAIR 4          /* contacts kept per box-box pair (deepest + spread)  */
 #define SO100_MAXCON 16             /* contacts kept per env per position stage           */
-#define SO100_CONDIM 4              /* every in-scope pair mixes to condim 4 (cube condim=4) */
+#define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, hull-table pairs are 3 */
 #define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_MAXCON * SO100_CONDIM)
 #define SO100_NOBS 15               /* box(3) bin(3) ee(3) qpos(6) — env.py:137-145      */
 
@@ -84,14 +90,29 @@ typedef struct so100_model {
   double geom_quat[SO100_NGEOM][4];
   double geom_size[SO100_NGEOM][3];
 
-  /* contact pairs with mixed parameters */
+  /* contact pairs with mixed parameters (geom2 of a hull pair: -1 - hull index) */
   int    pair_geom1[SO100_NPAIR];
   int    pair_geom2[SO100_NPAIR];
+  int    pair_body1[SO100_NPAIR];
+  int    pair_body2[SO100_NPAIR];
   int    pair_condim[SO100_NPAIR];
   double pair_friction[SO100_NPAIR][3];
   double pair_solref[SO100_NPAIR][2];
   double pair_solimp[SO100_NPAIR][5];
   double pair_margin[SO100_NPAIR];
+
+  /* arm/jaw collision hulls: convex hulls of the collision meshes, vertices in the body frame,
+   * body-frame bounding box (center, half extents) for the broadphase; the table's top face (z, x-y
+   * footprint) */
+  int    hull_body[SO100_NHULL];
+  int    hull_start[SO100_NHULL];
+  int    hull_count[SO100_NHULL];
+  double hull_center[SO100_NHULL][3];
+  double hull_half[SO100_NHULL][3];
+  double hull_vert[SO100_HULL_NVERT][3];
+  double table_top;
+  double table_lo[2];
+  double table_hi[2];
 
   /* sites */
   int    site_cube_body;

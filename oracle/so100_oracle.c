@@ -605,11 +605,26 @@ static void make_frame(real f[9]) {
 }
 
 /* [3P] mj_collision restricted to the in-scope pair table (mj_collideGeoms order: pair order, then
- * contact order within the pair); bounding-sphere broadphase. */
+ * contact order within the pair); bounding-sphere broadphase.
+ *   pairs 0..13   box-box (box_box above);
+ *   pairs 14..22  (table, hull k): an arm/jaw convex hull against the table top.  The
+ *     table is a box far larger than any hull, so where a hull dips through the top face inside its
+ *     footprint the convex-convex penetration (MuJoCo mjc_Convex, one contact per pair without
+ *     multiccd) has the face normal +z, depth = -(lowest vertex z - top), and witness points at that
+ *     vertex and its projection on the face: pos = their midpoint.  The lowest vertex is the first in
+ *     hull order among ties; vertices outside the top face's x-y footprint are not counted. */
+static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
+  if (d->ncon >= SO100_MAXCON) { d->ncon_dropped++; return; }
+  so100o_contact* con = &d->con[d->ncon++];
+  *con = *c;
+  con->pair = p;
+  make_frame(con->frame);
+}
+
 static void collision(const so100_model* m, so100o_data* d) {
   d->ncon = 0;
   d->ncon_dropped = 0;
-  for (int p = 0; p < SO100_NPAIR; p++) {
+  for (int p = 0; p < SO100_NPAIR_BOX; p++) {
     int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
     real A[3], B[3];
     load3(A, m->geom_size[g1]);
@@ -620,13 +635,39 @@ static void collision(const so100_model* m, so100o_data* d) {
     if (norm3(dp) > norm3(A) + norm3(B) + margin) continue;
     so100o_contact tmp[SO100_MAXCONPAIR];
     int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin, tmp);
-    for (int c = 0; c < n; c++) {
-      if (d->ncon >= SO100_MAXCON) { d->ncon_dropped++; continue; }
-      so100o_contact* con = &d->con[d->ncon++];
-      *con = tmp[c];
-      con->pair = p;
-      make_frame(con->frame);
+    for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
+  }
+  const real top = (real)m->table_top;
+  const real lo0 = (real)m->table_lo[0], lo1 = (real)m->table_lo[1];
+  const real hi0 = (real)m->table_hi[0], hi1 = (real)m->table_hi[1];
+  for (int k = 0; k < SO100_NHULL; k++) {
+    const int p = SO100_NPAIR_BOX + k, b = m->hull_body[k];
+    const real margin = (real)m->pair_margin[p];
+    /* broadphase: the lowest point of the hull's body-frame bounding box */
+    real c[3], wc[3];
+    load3(c, m->hull_center[k]);
+    mulmv3(wc, d->xmat[b], c);
+    const real* R = d->xmat[b];
+    real ext = (real)fabs((double)R[6]) * (real)m->hull_half[k][0] + (real)fabs((double)R[7]) * (real)m->hull_half[k][1] +
+               (real)fabs((double)R[8]) * (real)m->hull_half[k][2];
+    if (d->xpos[b][2] + wc[2] - ext >= top + margin) continue;
+    real best = 0, bx = 0, by = 0;
+    int found = 0;
+    for (int v = 0; v < m->hull_count[k]; v++) {
+      real hv[3], w[3];
+      load3(hv, m->hull_vert[m->hull_start[k] + v]);
+      mulmv3(w, d->xmat[b], hv);
+      for (int t = 0; t < 3; t++) w[t] += d->xpos[b][t];
+      if (w[0] < lo0 || w[0] > hi0 || w[1] < lo1 || w[1] > hi1) continue;
+      if (!found || w[2] < best) { best = w[2]; bx = w[0]; by = w[1]; found = 1; }
     }
+    if (!found || !(best - top < margin)) continue;
+    so100o_contact con;
+    memset(&con, 0, sizeof(con));
+    con.pos[0] = bx; con.pos[1] = by; con.pos[2] = (real)0.5 * (best + top);
+    con.frame[0] = 0; con.frame[1] = 0; con.frame[2] = 1;
+    con.dist = best - top;
+    add_contact(d, &con, p);
   }
 }
 
@@ -701,11 +742,12 @@ static void make_constraint(const so100_model* m, so100o_data* d) {
       r++;
     }
   }
-  /* contacts: condim 4 elliptic, J rows = frame . (jac(body2) - jac(body1)) at the contact point */
+  /* contacts: elliptic (condim 4 for cube pairs, 3 for hull-table pairs), J rows = frame .
+   * (jac(body2) - jac(body1)) at the contact point */
   for (int c = 0; c < d->ncon; c++) {
     const so100o_contact* con = &d->con[c];
     int p = con->pair;
-    int b1 = m->geom_body[m->pair_geom1[p]], b2 = m->geom_body[m->pair_geom2[p]];
+    int b1 = m->pair_body1[p], b2 = m->pair_body2[p];
     real jp[3][NV], jr[3][NV];                     /* jac difference body2 - body1 */
     memset(jp, 0, sizeof(jp)); memset(jr, 0, sizeof(jr));
     for (int side = 0; side < 2; side++) {

@@ -344,3 +344,64 @@ def test_heavy_contact_parity(model, oracle64, oracle32):
     assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     env.close()
+
+
+def test_hull_table_parity(model, oracle64, oracle32):
+    """Arm/jaw hulls resting on the table (pairs 14..22, condim 3): states made by the
+    fp64 oracle driving the arm down onto the table, then teacher-forced GPU steps against it."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import NPAIR_BOX
+    n = 24
+    rng = np.random.default_rng(11)
+    d = oracle64.new_data()
+    states, targets = [], []
+    lo, hi = np.array(model.action_lo[:]), np.array(model.action_hi[:])
+    for i in range(n):
+        oracle64.reset(model, d, np.array([0.4, 0.95, 0.6, 1, 0, 0, 0]))          # cube out of reach
+        target = np.array([rng.uniform(-0.6, 0.6), rng.uniform(0.6, 1.2), rng.uniform(-1.2, -0.6),
+                           rng.uniform(0.8, 1.5), rng.uniform(-1.5, 1.5), rng.uniform(-0.17, 1.0)])
+        for k in range(6):
+            d.ctrl[k] = target[k]
+        for _ in range(400):
+            oracle64.call("so100o_substep", model, d)
+        q, v, w, _ = oracle64.get_state(d)
+        states.append((q, v, w))
+        targets.append((target - lo) / (hi - lo) * 2 - 1)      # keep pressing: the same targets as actions
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True)
+    env.reset(seed=3)
+    env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
+                  np.array([s[2] for s in states], np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, hull_con, bit_bad = [], [], [], 0
+    for step in range(4):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = (np.array(targets) + rng.normal(0, 0.02, (n, 6))).astype(np.float32)
+        _, _, _, _, info = env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        dbg = env.debug.cpu().numpy()
+        gb = info["contact_bits"].cpu().numpy().astype(np.uint32)
+        for i in range(n):
+            pairs = dbg[i, 48:48 + int(dbg[i, 0])]
+            hull_con.append(int((pairs >= NPAIR_BOX).sum()))
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(model, d64, 0, act[i])
+            oracle32.env_step(model, d32, 0, act[i])
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+            bit_bad += oracle64.contact_bits(d64) != gb[i]
+    qv_err, qv_floor, hull_con = np.array(qv_err), np.array(qv_floor), np.array(hull_con)
+    print(f"\nhull-table: GPU hull contacts per env mean {hull_con.mean():.2f} (envs with any: "
+          f"{(hull_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
+          f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
+          f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e} | contact-bit mismatches {bit_bad}")
+    assert (hull_con > 0).mean() > 0.5                 # the arm really rests on the table
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    assert bit_bad <= max(2, 0.05 * len(qv_err))
+    env.close()
