@@ -216,13 +216,23 @@ int build_device_model(const so100_model* s, DevModel* d) {
   if (s->site_ee_body != 6 || s->site_cube_body != SO100_CUBE_BODY) return fail("model: unexpected site bodies");
   for (int p = 0; p < SO100_NPAIR_BOX; p++)
     if (s->pair_condim[p] != 4) return fail("model: box-box pairs must have condim 4");
-  for (int p = SO100_NPAIR_BOX; p < SO100_NPAIR; p++) {
+  for (int p = SO100_NPAIR_BOX; p < SO100_PAIR_MPR0; p++) {
     const int k = p - SO100_NPAIR_BOX;
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: hull pairs must have condim 3 or 4");
     if (s->pair_body1[p] != 0 || s->pair_body2[p] != s->hull_body[k]) return fail("model: hull pair k must be (table, hull k)");
     if (s->hull_body[k] < 2 || s->hull_body[k] > 7) return fail("model: hulls must sit on arm bodies 2..7");
     if (s->hull_start[k] < 0 || s->hull_count[k] < 1 || s->hull_start[k] + s->hull_count[k] > SO100_HULL_NVERT)
       return fail("model: hull vertex range out of bounds");
+  }
+  // (box, hull) pairs of the MPR collider: box j = cube (geom 9) then the bin boxes (geoms 10..14), hull k
+  for (int p = SO100_PAIR_MPR0; p < SO100_NPAIR; p++) {
+    const int q = p - SO100_PAIR_MPR0, j = q / SO100_NHULL, k = q % SO100_NHULL;
+    const int g = SO100_CUBE_GEOM + j;
+    if (s->pair_geom1[p] != g || s->pair_geom2[p] != -1 - k) return fail("model: MPR pair p must be (box j, hull k)");
+    if (s->pair_body1[p] != s->geom_body[g] || s->pair_body2[p] != s->hull_body[k]) return fail("model: MPR pair bodies");
+    if (j > 0 && s->geom_body[g] != 0) return fail("model: bin boxes must be static");
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: MPR pairs must have condim 3 or 4");
+    if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
   }
   for (int g = 0; g < SO100_NGEOM; g++) {
     int b = s->geom_body[g];
@@ -291,6 +301,8 @@ int build_device_model(const so100_model* s, DevModel* d) {
     for (int k = 0; k < 3; k++) d->geom_pos[g][k] = (float)s->geom_pos[g][k];
     for (int k = 0; k < 9; k++) d->geom_mat[g][k] = (float)gm[k];
     for (int k = 0; k < 3; k++) d->geom_size[g][k] = (float)s->geom_size[g][k];
+    d->geom_rbound[g] = (float)sqrt(s->geom_size[g][0] * s->geom_size[g][0] + s->geom_size[g][1] * s->geom_size[g][1] +
+                                    s->geom_size[g][2] * s->geom_size[g][2]);
   }
   for (int p = 0; p < SO100_NPAIR; p++) {
     d->pair_g1[p] = s->pair_geom1[p];
@@ -317,7 +329,10 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->hull_start[k] = s->hull_start[k];
     d->hull_count[k] = s->hull_count[k];
     d->hull_center[k] = {(float)s->hull_center[k][0], (float)s->hull_center[k][1], (float)s->hull_center[k][2], 0.f};
-    d->hull_half[k] = {(float)s->hull_half[k][0], (float)s->hull_half[k][1], (float)s->hull_half[k][2], 0.f};
+    d->hull_half[k] = {(float)s->hull_half[k][0], (float)s->hull_half[k][1], (float)s->hull_half[k][2],
+                       (float)sqrt(s->hull_half[k][0] * s->hull_half[k][0] + s->hull_half[k][1] * s->hull_half[k][1] +
+                                   s->hull_half[k][2] * s->hull_half[k][2])};
+    d->hull_centroid[k] = {(float)s->hull_centroid[k][0], (float)s->hull_centroid[k][1], (float)s->hull_centroid[k][2], 0.f};
   }
   for (int v = 0; v < SO100_HULL_NVERT; v++)
     d->hull_vert[v] = {(float)s->hull_vert[v][0], (float)s->hull_vert[v][1], (float)s->hull_vert[v][2], 0.f};

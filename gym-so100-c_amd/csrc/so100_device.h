@@ -60,8 +60,9 @@ struct DevModel {
   float geom_pos[SO100_NGEOM][3];   // body frame (world for static)
   float geom_mat[SO100_NGEOM][9];
   float geom_size[SO100_NGEOM][3];
+  float geom_rbound[SO100_NGEOM];   // |half sizes| (box bounding sphere)
 
-  // pairs (0..13 box-box, 14..22 table-hull)
+  // pairs (0..13 box-box, 14..22 table-hull, 23..76 (cube | bin box, hull) through MPR)
   int pair_g1[SO100_NPAIR], pair_g2[SO100_NPAIR];
   int pair_b1[SO100_NPAIR], pair_b2[SO100_NPAIR];
   int pair_cond4[SO100_NPAIR];      // 1: condim 4 (torsion row), 0: condim 3 (J row 3 zero)
@@ -75,7 +76,8 @@ struct DevModel {
 
   // arm/jaw collision hulls vs the table top (body-frame vertices and bounding box: center, half extents)
   int hull_body[SO100_NHULL], hull_start[SO100_NHULL], hull_count[SO100_NHULL];
-  float4_t hull_center[SO100_NHULL], hull_half[SO100_NHULL];
+  float4_t hull_center[SO100_NHULL], hull_half[SO100_NHULL];   // hull_half.w = |half extents|
+  float4_t hull_centroid[SO100_NHULL];   // MPR portal centre (mesh volume centroid), body frame
   float4_t hull_vert[SO100_HULL_NVERT];
   float table_top, table_lo[2], table_hi[2];
 

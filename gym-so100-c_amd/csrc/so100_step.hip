@@ -29,9 +29,15 @@ struct __attribute__((aligned(16))) ConGeom {    // per-contact geometry (collis
 union ConSlot {
   ConGeom g;
 };
+struct __attribute__((aligned(16))) MprStage {   // a box-hull (MPR) contact staged during collision
+  float pos[4];        // world position, dist
+  float nrm[4];        // world normal (box -> hull), pair index (int bits)
+};
+struct __attribute__((aligned(16))) ConArea {
+  ConSlot con[kMaxCon];
+  MprStage mpr[kMaxCon];
+};
 struct __attribute__((aligned(16))) SerialScratch {   // per-body arrays of the 6-link chain
-  float xm[6][12];     // body rotation (row-major 3x3, padded)
-  float xp[6][4];
   float cin[6][16];    // spatial inertia about the Base origin: I(9), m*d(3), m
   float cdof[6][8];    // motion subspace (angular; linear)
   float cfrc[6][8];    // RNE body forces
@@ -41,7 +47,12 @@ struct __attribute__((aligned(16))) SerialScratch {   // per-body arrays of the 
   float X[6][8];       // M^-1 columns (X[c][i] = M^-1[i][c])
   float cdd[6][8];     // RNE: cdof_dot per body
   float tau[8];        // actuator force minus bias
+  // link frames last: collision still reads them (hull scans) while it fills the contact slots and the
+  // MPR staging area, which alias the dead dynamics scratch in front of them
+  float xm[6][12];     // body rotation (row-major 3x3, padded)
+  float xp[6][4];
 };
+static_assert(__builtin_offsetof(SerialScratch, xm) >= sizeof(ConArea), "link frames must outlive the contact area");
 struct __attribute__((aligned(16))) EnvShared {
   float qpos[16];
   float qvel[16];
@@ -67,8 +78,11 @@ struct __attribute__((aligned(16))) EnvShared {
   int con_pair[kMaxCon];
   float con_dist[kMaxCon];
   union {
-    ConSlot con[kMaxCon];        // geometry (collision -> Jacobian), then solver data (setup -> PGS)
-    SerialScratch ser;           // serial stage scratch (dead before collision writes contacts)
+    struct {
+      ConSlot con[kMaxCon];      // geometry (collision -> Jacobian)
+      MprStage mpr[kMaxCon];     // MPR contacts staged before the compaction
+    };
+    SerialScratch ser;           // dynamics scratch (dead before collision) + link frames (live through it)
   };
   // stride = 13.25 x 256 B: the 4 envs of a wave hit different LDS bank windows for the same field
   float bank_pad[16];
@@ -986,6 +1000,386 @@ DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lan
   return found;
 }
 
+// ------------------------------------------------------------------ box vs convex hull: MPR (oracle mpr_*)
+// MuJoCo mjc_Convex -> libccd ccdMPRPenetration, restated (oracle/so100_oracle.c):
+// obj1 = the box (cube or a bin box), obj2 = hull k, in hull k's body frame H.  Every lane of the env's
+// row runs the portal arithmetic redundantly; the hull support is lane-parallel (lanes split the
+// vertices, a 16-lane (score, index) max keeps the oracle's first maximal vertex), so all 16 lanes hold
+// bitwise-identical portals and take identical branches.  Portal slots are only ever addressed by
+// constant indices (no scratch).
+struct MprSup {
+  float v[3], v1[3], v2[3];
+};
+struct MprObj {
+  float c[3], ax[9], h[3], hc[3];   // box centre, axes (columns of ax), half sizes; hull centroid (all H)
+  int s0, n;                        // hull vertex range
+};
+constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
+constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
+constexpr int kMprIters = 50;               // MuJoCo ccd_iterations
+
+DEV bool ccd_zero(float x) { return fabsf(x) < kCcdEps; }
+DEV bool ccd_eq(float a, float b) {
+  const float ab = fabsf(a - b);
+  if (ab < kCcdEps) return true;
+  const float fa = fabsf(a), fb = fabsf(b);
+  return fb > fa ? ab < kCcdEps * fb : ab < kCcdEps * fa;
+}
+DEV void normalize3(float* v) {
+  const float k = 1.0f / sqrtf(dot3(v, v));
+  v[0] *= k; v[1] *= k; v[2] *= k;
+}
+DEV void sub3(float* r, const float* a, const float* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+// d = w ? s : d as unconditional selects: a conditional copy between portal slots would be folded into a
+// store through a selected pointer, which puts the portal in scratch memory
+DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    d.v[t] = w ? s.v[t] : d.v[t];
+    d.v1[t] = w ? s.v1[t] : d.v1[t];
+    d.v2[t] = w ? s.v2[t] : d.v2[t];
+  }
+}
+
+DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const float* d, MprSup& s, int lane) {
+#pragma unroll
+  for (int t = 0; t < 3; t++) s.v1[t] = o.c[t];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float l = o.ax[i] * d[0] + o.ax[3 + i] * d[1] + o.ax[6 + i] * d[2];
+    const float sz = l >= 0.f ? o.h[i] : -o.h[i];
+#pragma unroll
+    for (int t = 0; t < 3; t++) s.v1[t] += sz * o.ax[3 * t + i];
+  }
+  const float n0 = -d[0], n1 = -d[1], n2 = -d[2];
+  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + o.s0;
+  float best = -__builtin_inff(), bx = 0.f, by = 0.f, bz = 0.f;
+  int bi = 0x7fffffff;
+  for (int i = lane; i < o.n; i += kLanes) {
+    const float4 v = verts[i];
+    const float sc = n0 * v.x + n1 * v.y + n2 * v.z;
+    if (sc > best) { best = sc; bi = i; bx = v.x; by = v.y; bz = v.z; }
+  }
+#pragma unroll
+  for (int off = 1; off < kLanes; off <<= 1) {
+    const float os = __shfl_xor(best, off, kLanes), ox = __shfl_xor(bx, off, kLanes);
+    const float oy = __shfl_xor(by, off, kLanes), oz = __shfl_xor(bz, off, kLanes);
+    const int oi = __shfl_xor(bi, off, kLanes);
+    if (os > best || (os == best && oi < bi)) { best = os; bi = oi; bx = ox; by = oy; bz = oz; }
+  }
+  s.v2[0] = bx; s.v2[1] = by; s.v2[2] = bz;
+  sub3(s.v, s.v1, s.v2);
+}
+DEV void portal_dir(const MprSup* P, float* dir) {
+  float a[3], b[3];
+  sub3(a, P[2].v, P[1].v);
+  sub3(b, P[3].v, P[1].v);
+  cross3(dir, a, b);
+  normalize3(dir);
+}
+DEV bool portal_reach_tol(const MprSup* P, const MprSup& v4, const float* dir) {
+  const float d4 = dot3(v4.v, dir);
+  float d1 = d4 - dot3(P[1].v, dir);
+  const float d2 = d4 - dot3(P[2].v, dir), d3 = d4 - dot3(P[3].v, dir);
+  d1 = d1 < d2 ? d1 : d2;
+  d1 = d1 < d3 ? d1 : d3;
+  return ccd_eq(d1, kMprTol) || d1 < kMprTol;
+}
+DEV void portal_expand(MprSup* P, const MprSup& v4) {
+  float v4v0[3];
+  cross3(v4v0, v4.v, P[0].v);
+  const bool a = dot3(P[1].v, v4v0) > 0.f, b = dot3(P[2].v, v4v0) > 0.f, c = dot3(P[3].v, v4v0) > 0.f;
+  sup_sel(P[1], v4, a ? b : !c);
+  sup_sel(P[2], v4, !a && c);
+  sup_sel(P[3], v4, a && !b);
+}
+// -1: no intersection, 0: portal, 1: touching on v1, 2: origin on the segment v0-v1
+DEV int mpr_discover(const DevModel* __restrict__ m, const MprObj& o, MprSup* P, int lane) {
+#pragma unroll
+  for (int t = 0; t < 3; t++) { P[0].v1[t] = o.c[t]; P[0].v2[t] = o.hc[t]; }
+  sub3(P[0].v, P[0].v1, P[0].v2);
+  if (ccd_zero(P[0].v[0]) && ccd_zero(P[0].v[1]) && ccd_zero(P[0].v[2])) P[0].v[0] += kCcdEps * 10.f;
+  float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]}, va[3], vb[3];
+  normalize3(dir);
+  mpr_support(m, o, dir, P[1], lane);
+  float dt = dot3(P[1].v, dir);
+  if (ccd_zero(dt) || dt < 0.f) return -1;
+  cross3(dir, P[0].v, P[1].v);
+  if (ccd_zero(dot3(dir, dir))) return (ccd_zero(P[1].v[0]) && ccd_zero(P[1].v[1]) && ccd_zero(P[1].v[2])) ? 1 : 2;
+  normalize3(dir);
+  mpr_support(m, o, dir, P[2], lane);
+  dt = dot3(P[2].v, dir);
+  if (ccd_zero(dt) || dt < 0.f) return -1;
+  sub3(va, P[1].v, P[0].v);
+  sub3(vb, P[2].v, P[0].v);
+  cross3(dir, va, vb);
+  normalize3(dir);
+  {
+    const bool sw = dot3(dir, P[0].v) > 0.f;
+    const MprSup t = P[1];
+    sup_sel(P[1], P[2], sw);
+    sup_sel(P[2], t, sw);
+    const float sg = sw ? -1.f : 1.f;
+    dir[0] *= sg; dir[1] *= sg; dir[2] *= sg;
+  }
+  for (int it = 0; it < kMprIters; it++) {
+    mpr_support(m, o, dir, P[3], lane);
+    dt = dot3(P[3].v, dir);
+    if (ccd_zero(dt) || dt < 0.f) return -1;
+    cross3(va, P[1].v, P[3].v);
+    dt = dot3(va, P[0].v);
+    const bool c1 = dt < 0.f && !ccd_zero(dt);
+    cross3(va, P[3].v, P[2].v);
+    dt = dot3(va, P[0].v);
+    const bool c2 = !c1 && dt < 0.f && !ccd_zero(dt);     // tested against the unchanged v2, as libccd
+    sup_sel(P[2], P[3], c1);
+    sup_sel(P[1], P[3], c2);
+    if (!c1 && !c2) return 0;
+    sub3(va, P[1].v, P[0].v);
+    sub3(vb, P[2].v, P[0].v);
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  return -1;
+}
+DEV float seg_dist2(const float* x0, const float* b, float* w) {
+  float dd[3];
+  sub3(dd, b, x0);
+  float t = -dot3(x0, dd);
+  t /= dot3(dd, dd);
+  if (t < 0.f || ccd_zero(t)) { w[0] = x0[0]; w[1] = x0[1]; w[2] = x0[2]; }
+  else if (t > 1.f || ccd_eq(t, 1.f)) { w[0] = b[0]; w[1] = b[1]; w[2] = b[2]; }
+  else {
+#pragma unroll
+    for (int k = 0; k < 3; k++) w[k] = dd[k] * t + x0[k];
+  }
+  return dot3(w, w);
+}
+// ccdVec3PointTriDist2 of the origin, with the witness point
+DEV float tri_dist2(const float* x0, const float* B, const float* C, float* w) {
+  float d1[3], d2[3];
+  sub3(d1, B, x0);
+  sub3(d2, C, x0);
+  const float v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(x0, d1), q = dot3(x0, d2), r = dot3(d1, d2);
+  const float det = ww * v - r * r;
+  float s, t;
+  if (ccd_zero(det)) { s = -1.f; t = -1.f; }
+  else { s = (q * r - ww * p) / det; t = (-s * r - q) / ww; }
+  if ((ccd_zero(s) || s > 0.f) && (ccd_eq(s, 1.f) || s < 1.f) && (ccd_zero(t) || t > 0.f) &&
+      (ccd_eq(t, 1.f) || t < 1.f) && (ccd_eq(t + s, 1.f) || t + s < 1.f)) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) w[k] = x0[k] + d1[k] * s + d2[k] * t;
+    return dot3(w, w);
+  }
+  float w2[3];
+  float dist = seg_dist2(x0, B, w);
+  float d2b = seg_dist2(x0, C, w2);
+  if (d2b < dist) { dist = d2b; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  d2b = seg_dist2(B, C, w2);
+  if (d2b < dist) { dist = d2b; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  return dist;
+}
+DEV void mpr_find_pos(const MprSup* P, float* pos) {
+  float dir[3], vec[3], b[4];
+  portal_dir(P, dir);
+  cross3(vec, P[1].v, P[2].v); b[0] = dot3(vec, P[3].v);
+  cross3(vec, P[3].v, P[2].v); b[1] = dot3(vec, P[0].v);
+  cross3(vec, P[0].v, P[1].v); b[2] = dot3(vec, P[3].v);
+  cross3(vec, P[2].v, P[1].v); b[3] = dot3(vec, P[0].v);
+  float sum = b[0] + b[1] + b[2] + b[3];
+  if (ccd_zero(sum) || sum < 0.f) {
+    b[0] = 0.f;
+    cross3(vec, P[2].v, P[3].v); b[1] = dot3(vec, dir);
+    cross3(vec, P[3].v, P[1].v); b[2] = dot3(vec, dir);
+    cross3(vec, P[1].v, P[2].v); b[3] = dot3(vec, dir);
+    sum = b[1] + b[2] + b[3];
+  }
+  const float inv = 1.f / sum;
+  float p1[3] = {0.f, 0.f, 0.f}, p2[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int t = 0; t < 3; t++) { p1[t] += P[i].v1[t] * b[i]; p2[t] += P[i].v2[t] * b[i]; }
+#pragma unroll
+  for (int t = 0; t < 3; t++) pos[t] = 0.5f * (p1[t] * inv + p2[t] * inv);
+}
+// ccdMPRPenetration: true and (depth, dir box -> hull, pos) on intersection with a defined normal
+DEV bool mpr_penetration(const DevModel* __restrict__ m, const MprObj& o, float& depth, float* dir, float* pos,
+                         int lane) {
+  MprSup P[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int t = 0; t < 3; t++) { P[i].v[t] = 0.f; P[i].v1[t] = 0.f; P[i].v2[t] = 0.f; }
+  const int res = mpr_discover(m, o, P, lane);
+  if (res < 0 || res == 1) return false;
+  if (res == 2) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) { pos[t] = 0.5f * (P[1].v1[t] + P[1].v2[t]); dir[t] = P[1].v[t]; }
+    depth = sqrtf(dot3(dir, dir));
+    if (ccd_zero(depth)) return false;
+    normalize3(dir);
+    return true;
+  }
+  // refine the portal until it holds the origin
+  for (int it = 0;; it++) {
+    if (it >= kMprIters) return false;
+    float pd[3];
+    portal_dir(P, pd);
+    float dt = dot3(pd, P[1].v);
+    if (ccd_zero(dt) || dt > 0.f) break;
+    MprSup v4;
+    mpr_support(m, o, pd, v4, lane);
+    dt = dot3(v4.v, pd);
+    if (!(ccd_zero(dt) || dt > 0.f) || portal_reach_tol(P, v4, pd)) return false;
+    portal_expand(P, v4);
+  }
+  // penetration: expand towards the boundary until the tolerance (or the iteration cap)
+  for (int it = 0;; it++) {
+    float pd[3];
+    portal_dir(P, pd);
+    MprSup v4;
+    mpr_support(m, o, pd, v4, lane);
+    if (portal_reach_tol(P, v4, pd) || it > kMprIters) break;
+    portal_expand(P, v4);
+  }
+  depth = sqrtf(tri_dist2(P[1].v, P[2].v, P[3].v, dir));
+  if (ccd_zero(depth)) return false;
+  normalize3(dir);
+  mpr_find_pos(P, pos);
+  return true;
+}
+
+// Box j (0 = the cube, 1..5 = bin boxes) in hull k's body frame H: centre, axes (columns), half sizes.
+DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int j, int k, MprObj& o) {
+  const int a = m->hull_body[k] - 2, g = SO100_CUBE_GEOM + j;
+  const float* RH = sh.ser.xm[a];
+  const float* pH = sh.ser.xp[a];
+  float pb[3], Rb[9];
+  if (j == 0) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) pb[t] = sh.cube_pos[t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) Rb[t] = sh.cube_mat[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < 3; t++) pb[t] = m->geom_pos[g][t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) Rb[t] = m->geom_mat[g][t];
+  }
+  float dp[3];
+  sub3(dp, pb, pH);
+  mulmtv3(o.c, RH, dp);
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int jj = 0; jj < 3; jj++) o.ax[3 * i + jj] = RH[i] * Rb[jj] + RH[3 + i] * Rb[3 + jj] + RH[6 + i] * Rb[6 + jj];
+#pragma unroll
+  for (int t = 0; t < 3; t++) o.h[t] = m->geom_size[g][t];
+  const float4 hc = reinterpret_cast<const float4*>(m->hull_centroid)[k];
+  o.hc[0] = hc.x; o.hc[1] = hc.y; o.hc[2] = hc.z;
+  o.s0 = m->hull_start[k];
+  o.n = m->hull_count[k];
+}
+// conservative broadphase, stage 1 (oracle mpr_broadphase): bounding spheres, tested in the world frame
+// (the box centre against hull k's box centre; radii precomputed: hull_half.w, |half sizes| of the box)
+DEV bool mpr_sphere(const DevModel* __restrict__ m, const EnvShared& sh, int j, int k) {
+  const int a = m->hull_body[k] - 2, g = SO100_CUBE_GEOM + j;
+  const float4 hb4 = reinterpret_cast<const float4*>(m->hull_center)[k];
+  const float* RH = sh.ser.xm[a];
+  const float hb[3] = {hb4.x, hb4.y, hb4.z};
+  float w[3];
+  mulmv3(w, RH, hb);
+  float T[3];
+#pragma unroll
+  for (int t = 0; t < 3; t++) T[t] = (j == 0 ? sh.cube_pos[t] : m->geom_pos[g][t]) - (w[t] + sh.ser.xp[a][t]);
+  const float rs = reinterpret_cast<const float4*>(m->hull_half)[k].w + m->geom_rbound[g];
+  return dot3(T, T) <= rs * rs;
+}
+// stage 2: OBB-OBB separating axes in H (hull k's box vs the box)
+DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) {
+  const float4 hb4 = reinterpret_cast<const float4*>(m->hull_center)[k];
+  const float4 hh4 = reinterpret_cast<const float4*>(m->hull_half)[k];
+  const float hb[3] = {hb4.x, hb4.y, hb4.z}, hh[3] = {hh4.x, hh4.y, hh4.z};
+  float T[3];
+  sub3(T, o.c, hb);
+  float A[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) A[i] = fabsf(o.ax[i]) + 1e-5f;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+    if (fabsf(T[i]) > hh[i] + o.h[0] * A[3 * i] + o.h[1] * A[3 * i + 1] + o.h[2] * A[3 * i + 2]) return false;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const float s = T[0] * o.ax[j] + T[1] * o.ax[3 + j] + T[2] * o.ax[6 + j];
+    if (fabsf(s) > hh[0] * A[j] + hh[1] * A[3 + j] + hh[2] * A[6 + j] + o.h[j]) return false;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const float ra = hh[i1] * A[3 * i2 + j] + hh[i2] * A[3 * i1 + j];
+      const float rb = o.h[j1] * A[3 * i + j2] + o.h[j2] * A[3 * i + j1];
+      const float s = T[i2] * o.ax[3 * i1 + j] - T[i1] * o.ax[3 * i2 + j];
+      if (fabsf(s) > ra + rb) return false;
+    }
+  }
+  return true;
+}
+
+// The (cube | bin box, hull) pairs 23..76 of one substep, contacts staged in sh.mpr in pair order.
+//  * broadphase, lane-parallel: lane l of the env's row tests pairs l, l+16, l+32, l+48 (< 54);
+//  * narrowphase: the wave walks the union of its 4 envs' candidate pairs in ascending order; each env
+//    holding the pair runs MPR on its whole row.
+// Returns the env's number of staged contacts (uniform across its row, capped at kMaxCon).
+DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, int grp, bool valid) {
+#ifdef SO100_EXPERIMENT_NO_MPR
+  return 0;   // timing experiment only: box-hull contacts off
+#endif
+  uint64_t env_cand = 0, wave_cand = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int q = lane + kLanes * r;
+    bool cand = false;
+    if (valid && q < SO100_NPAIR_MPR && mpr_sphere(m, sh, q / SO100_NHULL, q % SO100_NHULL)) {
+      MprObj o;
+      mpr_obj_setup(m, sh, q / SO100_NHULL, q % SO100_NHULL, o);
+      cand = mpr_broadphase(m, o, q % SO100_NHULL);
+    }
+    const uint64_t b = __ballot(cand);
+    env_cand |= ((b >> (grp * 16)) & 0xFFFFull) << (16 * r);
+    wave_cand |= ((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFull) << (16 * r);
+  }
+  int ns = 0;
+  while (wave_cand) {
+    const int q = __builtin_ctzll(wave_cand);
+    wave_cand &= wave_cand - 1ull;
+    if ((env_cand >> q) & 1ull) {
+      const int j = q / SO100_NHULL, k = q % SO100_NHULL;
+      MprObj o;
+      mpr_obj_setup(m, sh, j, k, o);
+      float depth, dir[3], pos[3];
+      if (mpr_penetration(m, o, depth, dir, pos, lane)) {
+        if (ns < kMaxCon && lane == 0) {
+          const int a = m->hull_body[k] - 2;
+          float wn[3], wp[3];
+          mulmv3(wn, sh.ser.xm[a], dir);
+          mulmv3(wp, sh.ser.xm[a], pos);
+          MprStage& st = sh.mpr[ns];
+          st.pos[0] = wp[0] + sh.ser.xp[a][0]; st.pos[1] = wp[1] + sh.ser.xp[a][1];
+          st.pos[2] = wp[2] + sh.ser.xp[a][2]; st.pos[3] = -depth;
+          st.nrm[0] = wn[0]; st.nrm[1] = wn[1]; st.nrm[2] = wn[2];
+          st.nrm[3] = __int_as_float(SO100_PAIR_MPR0 + q);
+        }
+        ns++;
+      }
+    }
+  }
+  return ns < kMaxCon ? ns : kMaxCon;
+}
+
 DEV void make_frame(float* f) {
   float* n = f;
   float* t1 = f + 3;
@@ -1277,11 +1671,13 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     dynamics_par(m, sh, lane, mscale);
     __syncthreads();
     SSTAMP(1);
-    // ---------------- S3: collision: hulls vs the table (lane k = hull k), one box pair per lane;
-    // compaction in pair order (box pairs, then hull pairs)
+    // ---------------- S3: collision: hulls vs the table (lane k = hull k), box-hull pairs by MPR
+    // (staged in LDS), one box pair per lane; compaction in pair order (box pairs, table-hull pairs,
+    // box-hull pairs)
     float hx, hy, hz;
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
+    const int nmpr = mpr_contacts(m, sh, lane, grp, valid);
     PairContacts pc;
     pc.n = 0;
     if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
@@ -1318,6 +1714,19 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
         sh.con_pair[hslot] = SO100_NPAIR_BOX + lane;
       }
       tot += __popc(hrow);
+      const int mslot = tot + lane;
+      if (lane < nmpr && mslot < kMaxCon) {
+        const MprStage st = sh.mpr[lane];
+        float fr[9] = {st.nrm[0], st.nrm[1], st.nrm[2], 0, 0, 0, 0, 0, 0};
+        make_frame(fr);
+#pragma unroll
+        for (int t = 0; t < 9; t++) sh.con[mslot].g.frame[t] = fr[t];
+#pragma unroll
+        for (int t = 0; t < 4; t++) sh.con[mslot].g.pos[t] = st.pos[t];
+        sh.con_dist[mslot] = st.pos[3];
+        sh.con_pair[mslot] = __float_as_int(st.nrm[3]);
+      }
+      tot += nmpr;
       if (lane == 0) sh.ncon = tot < kMaxCon ? tot : kMaxCon;
     }
     __syncthreads();

@@ -16,8 +16,10 @@ from . import constants as C
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so100_model.json")
 
 NBODY, NHINGE, NQ, NV, NU, NGEOM = 9, 6, 13, 12, 6, 15
-NPAIR_BOX, NHULL, HULL_NVERT = 14, 9, 2560
-NPAIR = NPAIR_BOX + NHULL
+NPAIR_BOX, NHULL, HULL_NVERT, NBINBOX = 14, 9, 2560, 5
+PAIR_MPR0 = NPAIR_BOX + NHULL                  # (box, hull) pairs of the MPR convex collider start here
+NPAIR = PAIR_MPR0 + (1 + NBINBOX) * NHULL      # 77
+NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
 MAXCON, CONDIM, NOBS = 16, 4, 15
 NEFC_MAX = NV + NHINGE + MAXCON * CONDIM
 
@@ -53,6 +55,7 @@ class SO100Model(ctypes.Structure):
         ("pair_solimp", _arr(_d, NPAIR, 5)), ("pair_margin", _arr(_d, NPAIR)),
         ("hull_body", _arr(_i, NHULL)), ("hull_start", _arr(_i, NHULL)), ("hull_count", _arr(_i, NHULL)),
         ("hull_center", _arr(_d, NHULL, 3)), ("hull_half", _arr(_d, NHULL, 3)),
+        ("hull_centroid", _arr(_d, NHULL, 3)),
         ("hull_vert", _arr(_d, HULL_NVERT, 3)),
         ("table_top", _d), ("table_lo", _arr(_d, 2)), ("table_hi", _arr(_d, 2)),
         ("site_cube_body", _i), ("site_cube_pos", _arr(_d, 3)), ("site_ee_body", _i), ("site_ee_pos", _arr(_d, 3)),
@@ -134,6 +137,7 @@ def build_model(path=ASSET, iterations=None, nsubstep=None):
     _set(m, "hull_count", np.asarray(counts, dtype=np.int64))
     _set(m, "hull_center", np.asarray([x["center"] for x in h]))
     _set(m, "hull_half", np.asarray([x["half"] for x in h]))
+    _set(m, "hull_centroid", np.asarray([x["centroid"] for x in h]))
     _set(m, "hull_vert", verts)
     tp = d["table_plane"]
     m.table_top = tp["top"]

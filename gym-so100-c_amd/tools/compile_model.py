@@ -15,8 +15,10 @@ reference.  It restates what MuJoCo's compiler does for the parts of
   bin walls/floor (transfer_cube.xml:18-22), table = 8-vertex box hull of tabletop.stl
   (scene_so100.xml:3,20) emitted as an exact box
 * arm/jaw collision hulls: qhull convex hulls (scipy) of the class="collision" meshes on the moving arm
-  bodies (so_arm100.xml:79,87,95,103,111-112,136-138), vertices in the body frame, for the
-  hull-vs-table contacts; pair parameters mixed like the box pairs
+  bodies (so_arm100.xml:79,87,95,103,111-112,136-138), vertices in the body frame, mesh volume
+  centroid (the mesh geom's frame origin), for the hull-vs-table contacts and the box-vs-hull pairs of
+  the convex collider (cube and bin boxes vs every hull); pair parameters mixed like
+  the box pairs
 * contact-pair parameter mixing (MuJoCo mj_contactParam semantics, restated): condim=max,
   friction=elementwise max, solref/solimp = solmix-weighted mean (solmix defaults 1 -> mean)
 * setConst quantities at qpos0 (MuJoCo mj_setConst, restated): dof_M0 (diag of M incl. armature),
@@ -360,7 +362,14 @@ def compile_model():
             hv = v[ConvexHull(v).vertices] + pos
             lo, hi = hv.min(0), hv.max(0)
             c = (lo + hi) / 2
+            # volume centroid of the (closed) mesh: MuJoCo re-centres a mesh geom on its inertial frame,
+            # so geom_xpos -- the centre mjc_Convex's MPR starts its portal from -- is this point
+            tri = v.reshape(-1, 3, 3)
+            vol6 = np.einsum("ij,ij->i", tri[:, 0], np.cross(tri[:, 1], tri[:, 2]))
+            assert vol6.sum() > 0, g["mesh"]
+            centroid = (vol6[:, None] * tri.sum(1)).sum(0) / (4 * vol6.sum()) + pos
             hulls.append(dict(name=g["mesh"], body=bid[bname], verts=hv.tolist(), center=c.tolist(),
+                              centroid=centroid.tolist(),
                               half=((hi - lo) / 2).tolist(),
                               condim=int(g.get("condim", MJ_CONDIM)),
                               friction=(vec(g["friction"]).tolist() if "friction" in g else MJ_FRICTION),
@@ -395,6 +404,16 @@ def compile_model():
     for k, h in enumerate(hulls):
         pairs.append(dict(g1=gid["table"], g2=-1 - k, body1=0, body2=h["body"], name1="table", name2=h["name"],
                           hull=k, **mixed(tbl, h)))
+    # (box, hull k) through the general convex collider (MPR): geom1 = the box (MuJoCo orders a pair by
+    # geom type, box < mesh), normal from the box to the hull.  Pairs 23..31: the cube against every
+    # arm/jaw hull; pairs 32..76: bin box j (walls, floor) against hull k at 32 + 9 j + k.  Not in scope:
+    # the static Base hull (far from every spawn), hull-hull self-collision, pads vs table/bin.
+    boxes = ["red_box"] + ["bin_wall", "bin_wall2", "bin_wall3", "bin_wall4", "bin_floor"]
+    for n1 in boxes:
+        g1 = geoms[gid[n1]]
+        for k, h in enumerate(hulls):
+            pairs.append(dict(g1=gid[n1], g2=-1 - k, body1=g1["body"], body2=h["body"], name1=n1,
+                              name2=h["name"], hull=k, **mixed(g1, h)))
 
     # ---- sites ----
     cube_site = vec(bodies["box"]["sites"][0]["pos"], 3)

@@ -14,6 +14,8 @@
  *   geoms  0 table | 1..4 fixed_jaw_pad_1..4 | 5..8 moving_jaw_pad_1..4 | 9 red_box | 10..14 bin walls+floor
  *   pairs  0..7 pad-vs-red_box | 8 (red_box, table) | 9..13 (red_box, bin_*)   (box-box)
  *          14..22 (table, hull k): arm/jaw collision hulls vs the table top
+ *          23..31 (red_box, hull k) | 32..76 (bin box j, hull k) at 32 + 9 j + k, j = bin_wall,
+ *          bin_wall2..4, bin_floor: box vs convex hull through the MPR convex collider
  *   hulls  0 Rotation_Pitch | 1 Upper_Arm | 2 Lower_Arm | 3 Wrist_Pitch_Roll |
  *          4..5 Fixed_Jaw_Collision_1..2 | 6..8 Moving_Jaw_Collision_1..3
  */
@@ -28,7 +30,11 @@
 #define SO100_NGEOM 15
 #define SO100_NPAIR_BOX 14         /* box-box pairs 0..13 */
 #define SO100_NHULL 9               /* arm/jaw collision hulls */
-#define SO100_NPAIR (SO100_NPAIR_BOX + SO100_NHULL)   /* + (table, hull k) pairs 14..22 */
+#define SO100_NBINBOX 5             /* bin walls + floor (geoms 10..14) */
+#define SO100_PAIR_MPR0 (SO100_NPAIR_BOX + SO100_NHULL)     /* 23: first (box, hull) MPR pair */
+#define SO100_NPAIR_MPR ((1 + SO100_NBINBOX) * SO100_NHULL) /* 54: (cube | bin box j, hull k) */
+#define SO100_NPAIR (SO100_PAIR_MPR0 + SO100_NPAIR_MPR)    /* 77 */
+#define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_CUBE_BODY 8
 #define SO100_CUBE_GEOM 9
@@ -36,7 +42,7 @@
 #define SO100_NPAIR_GRIPPER 8       /* pairs 0..7 — single_arm.py:348-352 touch_gripper   */
 #define SO100_MAXCONPAIR 4          /* contacts kept per box-box pair (deepest + spread)  */
 #define SO100_MAXCON 16             /* contacts kept per env per position stage           */
-#define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, hull-table pairs are 3 */
+#define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, table/bin-hull pairs are 3 */
 #define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_MAXCON * SO100_CONDIM)
 #define SO100_NOBS 15               /* box(3) bin(3) ee(3) qpos(6) — env.py:137-145      */
 
@@ -109,6 +115,7 @@ typedef struct so100_model {
   int    hull_count[SO100_NHULL];
   double hull_center[SO100_NHULL][3];
   double hull_half[SO100_NHULL][3];
+  double hull_centroid[SO100_NHULL][3];   /* mesh volume centroid = the mesh geom's frame origin */
   double hull_vert[SO100_HULL_NVERT][3];
   double table_top;
   double table_lo[2];

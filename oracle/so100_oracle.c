@@ -621,6 +621,257 @@ static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
   make_frame(con->frame);
 }
 
+/* ---------------------------------------------------------------- box vs convex hull (MPR)
+ * [3P] MuJoCo mjc_Convex -> libccd ccdMPRPenetration (libccd mpr.c: discoverPortal, refinePortal,
+ * findPenetr, findPenetrTouch, findPenetrSegment, findPos, expandPortal, portalDir,
+ * portalEncapsulesOrigin, portalReachTolerance, portalCanEncapsuleOrigin; vec3.c
+ * ccdVec3PointTriDist2), restated.  MuJoCo 3.3.3 defaults to its native GJK/EPA; this is the libccd
+ * path it keeps behind mjDSBL_NATIVECCD (deviation 7).  One contact per pair (no
+ * multiccd).  obj1 = the box (geom1), obj2 = hull k (geom2): Minkowski difference obj1 - obj2, centres
+ * = geom_xpos (box centre; the mesh's volume centroid).  Supports as mjccd_support: box corner by the
+ * sign (>= 0 -> +size) of the direction in the box frame; hull = first vertex of maximal (-d).v.
+ * Everything runs in hull k's body frame H, where the vertices are stored; the contact is rotated to
+ * the world at the end.  ccd_tolerance 1e-6, ccd_iterations 50 (MuJoCo defaults).  The loops libccd
+ * leaves unbounded (discoverPortal's, refinePortal's) stop after the same 50 iterations: no contact. */
+#define MPR_TOL ((real)1e-6)
+#define MPR_ITERS 50
+/* libccd's zero/equality tests use MuJoCo's double-precision CCD_EPS (DBL_EPSILON) in both builds: the
+ * tests are absolute, and FLT_EPSILON would misclassify mm-scale geometry (e.g. |v0 x v1|^2 ~ 1e-10 read
+ * as collinear), sending the fp32 build down different branches than MuJoCo's double libccd */
+#define CCD_EPS ((real)2.220446049250313e-16)
+typedef struct { real v[3], v1[3], v2[3]; } mpr_sup;
+typedef struct {
+  real c[3], ax[9], h[3];        /* box centre, axes (columns of ax), half sizes, all in H */
+  const double (*vert)[3];       /* hull vertices (H) */
+  int nvert;
+  real hc[3];                    /* hull centroid (H) */
+} mpr_obj;
+
+static int ccd_zero(real x) { return (real)fabs((double)x) < CCD_EPS; }
+static int ccd_eq(real a, real b) {
+  real ab = (real)fabs((double)(a - b));
+  if (ab < CCD_EPS) return 1;
+  real fa = (real)fabs((double)a), fb = (real)fabs((double)b);
+  return fb > fa ? ab < CCD_EPS * fb : ab < CCD_EPS * fa;
+}
+static void sub3(real r[3], const real a[3], const real b[3]) { for (int t = 0; t < 3; t++) r[t] = a[t] - b[t]; }
+static void normalize3(real v[3]) {
+  real k = 1 / (real)sqrt((double)dot3(v, v));
+  for (int t = 0; t < 3; t++) v[t] *= k;
+}
+static void mpr_support(const mpr_obj* o, const real d[3], mpr_sup* s) {
+  for (int t = 0; t < 3; t++) s->v1[t] = o->c[t];
+  for (int i = 0; i < 3; i++) {
+    real l = o->ax[i] * d[0] + o->ax[3 + i] * d[1] + o->ax[6 + i] * d[2];
+    real sz = l >= 0 ? o->h[i] : -o->h[i];
+    for (int t = 0; t < 3; t++) s->v1[t] += sz * o->ax[3 * t + i];
+  }
+  real nd[3] = {-d[0], -d[1], -d[2]}, best = 0;
+  int bi = -1;
+  for (int v = 0; v < o->nvert; v++) {
+    real hv[3];
+    load3(hv, o->vert[v]);
+    real sc = dot3(nd, hv);
+    if (bi < 0 || sc > best) { best = sc; bi = v; }
+  }
+  load3(s->v2, o->vert[bi]);
+  sub3(s->v, s->v1, s->v2);
+}
+static void portal_dir(const mpr_sup P[4], real dir[3]) {
+  real a[3], b[3];
+  sub3(a, P[2].v, P[1].v);
+  sub3(b, P[3].v, P[1].v);
+  cross3(dir, a, b);
+  normalize3(dir);
+}
+static int portal_reach_tol(const mpr_sup P[4], const mpr_sup* v4, const real dir[3]) {
+  real d4 = dot3(v4->v, dir);
+  real d1 = d4 - dot3(P[1].v, dir), d2 = d4 - dot3(P[2].v, dir), d3 = d4 - dot3(P[3].v, dir);
+  d1 = d1 < d2 ? d1 : d2;
+  d1 = d1 < d3 ? d1 : d3;
+  return ccd_eq(d1, MPR_TOL) || d1 < MPR_TOL;
+}
+static void portal_expand(mpr_sup P[4], const mpr_sup* v4) {
+  real v4v0[3];
+  cross3(v4v0, v4->v, P[0].v);
+  if (dot3(P[1].v, v4v0) > 0) {
+    if (dot3(P[2].v, v4v0) > 0) P[1] = *v4; else P[3] = *v4;
+  } else {
+    if (dot3(P[3].v, v4v0) > 0) P[2] = *v4; else P[1] = *v4;
+  }
+}
+/* -1: no intersection, 0: portal, 1: touching on v1, 2: origin on the segment v0-v1 */
+static int mpr_discover(const mpr_obj* o, mpr_sup P[4]) {
+  for (int t = 0; t < 3; t++) { P[0].v1[t] = o->c[t]; P[0].v2[t] = o->hc[t]; }
+  sub3(P[0].v, P[0].v1, P[0].v2);
+  if (ccd_zero(P[0].v[0]) && ccd_zero(P[0].v[1]) && ccd_zero(P[0].v[2])) P[0].v[0] += CCD_EPS * 10;
+  real dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]}, va[3], vb[3];
+  normalize3(dir);
+  mpr_support(o, dir, &P[1]);
+  real dt = dot3(P[1].v, dir);
+  if (ccd_zero(dt) || dt < 0) return -1;
+  cross3(dir, P[0].v, P[1].v);
+  if (ccd_zero(dot3(dir, dir))) return (ccd_zero(P[1].v[0]) && ccd_zero(P[1].v[1]) && ccd_zero(P[1].v[2])) ? 1 : 2;
+  normalize3(dir);
+  mpr_support(o, dir, &P[2]);
+  dt = dot3(P[2].v, dir);
+  if (ccd_zero(dt) || dt < 0) return -1;
+  sub3(va, P[1].v, P[0].v);
+  sub3(vb, P[2].v, P[0].v);
+  cross3(dir, va, vb);
+  normalize3(dir);
+  if (dot3(dir, P[0].v) > 0) {
+    mpr_sup t = P[1]; P[1] = P[2]; P[2] = t;
+    for (int k = 0; k < 3; k++) dir[k] = -dir[k];
+  }
+  for (int it = 0; it < MPR_ITERS; it++) {
+    mpr_support(o, dir, &P[3]);
+    dt = dot3(P[3].v, dir);
+    if (ccd_zero(dt) || dt < 0) return -1;
+    int cont = 0;
+    cross3(va, P[1].v, P[3].v);
+    dt = dot3(va, P[0].v);
+    if (dt < 0 && !ccd_zero(dt)) { P[2] = P[3]; cont = 1; }
+    if (!cont) {
+      cross3(va, P[3].v, P[2].v);
+      dt = dot3(va, P[0].v);
+      if (dt < 0 && !ccd_zero(dt)) { P[1] = P[3]; cont = 1; }
+    }
+    if (!cont) return 0;
+    sub3(va, P[1].v, P[0].v);
+    sub3(vb, P[2].v, P[0].v);
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  return -1;
+}
+static int mpr_refine(const mpr_obj* o, mpr_sup P[4]) {
+  for (int it = 0; it < MPR_ITERS; it++) {
+    real dir[3];
+    portal_dir(P, dir);
+    real dt = dot3(dir, P[1].v);
+    if (ccd_zero(dt) || dt > 0) return 0;                  /* portal encapsulates the origin */
+    mpr_sup v4;
+    mpr_support(o, dir, &v4);
+    dt = dot3(v4.v, dir);
+    if (!(ccd_zero(dt) || dt > 0) || portal_reach_tol(P, &v4, dir)) return -1;
+    portal_expand(P, &v4);
+  }
+  return -1;
+}
+/* ccdVec3PointTriDist2 / __ccdVec3PointSegmentDist2 with P = origin and a witness point */
+static real seg_dist2(const real x0[3], const real b[3], real w[3]) {
+  real dd[3], a[3];
+  sub3(dd, b, x0);
+  for (int t = 0; t < 3; t++) a[t] = x0[t];
+  real t = -dot3(a, dd);
+  t /= dot3(dd, dd);
+  if (t < 0 || ccd_zero(t)) { for (int k = 0; k < 3; k++) w[k] = x0[k]; }
+  else if (t > 1 || ccd_eq(t, 1)) { for (int k = 0; k < 3; k++) w[k] = b[k]; }
+  else { for (int k = 0; k < 3; k++) w[k] = dd[k] * t + x0[k]; }
+  return dot3(w, w);
+}
+static real tri_dist2(const real x0[3], const real B[3], const real C[3], real w[3]) {
+  real d1[3], d2[3], a[3];
+  sub3(d1, B, x0);
+  sub3(d2, C, x0);
+  for (int t = 0; t < 3; t++) a[t] = x0[t];
+  real v = dot3(d1, d1), ww = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  real det = ww * v - r * r, s, t;
+  if (ccd_zero(det)) { s = -1; t = -1; }
+  else { s = (q * r - ww * p) / det; t = (-s * r - q) / ww; }
+  if ((ccd_zero(s) || s > 0) && (ccd_eq(s, 1) || s < 1) && (ccd_zero(t) || t > 0) && (ccd_eq(t, 1) || t < 1) &&
+      (ccd_eq(t + s, 1) || t + s < 1)) {
+    for (int k = 0; k < 3; k++) w[k] = x0[k] + d1[k] * s + d2[k] * t;
+    return dot3(w, w);
+  }
+  real w2[3];
+  real dist = seg_dist2(x0, B, w);
+  real d2b = seg_dist2(x0, C, w2);
+  if (d2b < dist) { dist = d2b; memcpy(w, w2, sizeof(w2)); }
+  d2b = seg_dist2(B, C, w2);
+  if (d2b < dist) { dist = d2b; memcpy(w, w2, sizeof(w2)); }
+  return dist;
+}
+static void mpr_find_pos(const mpr_sup P[4], real pos[3]) {
+  real dir[3], vec[3], b[4];
+  portal_dir(P, dir);
+  cross3(vec, P[1].v, P[2].v); b[0] = dot3(vec, P[3].v);
+  cross3(vec, P[3].v, P[2].v); b[1] = dot3(vec, P[0].v);
+  cross3(vec, P[0].v, P[1].v); b[2] = dot3(vec, P[3].v);
+  cross3(vec, P[2].v, P[1].v); b[3] = dot3(vec, P[0].v);
+  real sum = b[0] + b[1] + b[2] + b[3];
+  if (ccd_zero(sum) || sum < 0) {
+    b[0] = 0;
+    cross3(vec, P[2].v, P[3].v); b[1] = dot3(vec, dir);
+    cross3(vec, P[3].v, P[1].v); b[2] = dot3(vec, dir);
+    cross3(vec, P[1].v, P[2].v); b[3] = dot3(vec, dir);
+    sum = b[1] + b[2] + b[3];
+  }
+  real inv = 1 / sum, p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  for (int i = 0; i < 4; i++)
+    for (int t = 0; t < 3; t++) { p1[t] += P[i].v1[t] * b[i]; p2[t] += P[i].v2[t] * b[i]; }
+  for (int t = 0; t < 3; t++) pos[t] = (real)0.5 * (p1[t] * inv + p2[t] * inv);
+}
+/* ccdMPRPenetration: 1 and (depth, dir obj1 -> obj2, pos) on intersection with a defined normal */
+static int mpr_penetration(const mpr_obj* o, real* depth, real dir[3], real pos[3]) {
+  mpr_sup P[4];
+  memset(P, 0, sizeof(P));
+  int res = mpr_discover(o, P);
+  if (res < 0) return 0;
+  if (res == 1) return 0;                                   /* touching: zero depth, no normal */
+  if (res == 2) {                                           /* origin on the segment v0-v1 */
+    for (int t = 0; t < 3; t++) { pos[t] = (real)0.5 * (P[1].v1[t] + P[1].v2[t]); dir[t] = P[1].v[t]; }
+    *depth = (real)sqrt((double)dot3(dir, dir));
+    if (ccd_zero(*depth)) return 0;
+    normalize3(dir);
+    return 1;
+  }
+  if (mpr_refine(o, P) < 0) return 0;
+  for (int it = 0;; it++) {
+    real pd[3];
+    portal_dir(P, pd);
+    mpr_sup v4;
+    mpr_support(o, pd, &v4);
+    if (portal_reach_tol(P, &v4, pd) || it > MPR_ITERS) {
+      *depth = (real)sqrt((double)tri_dist2(P[1].v, P[2].v, P[3].v, dir));
+      if (ccd_zero(*depth)) return 0;                       /* MuJoCo drops a contact without a normal */
+      normalize3(dir);
+      mpr_find_pos(P, pos);
+      return 1;
+    }
+    portal_expand(P, &v4);
+  }
+}
+/* conservative broadphase for (box, hull k) in H: bounding spheres, then OBB-OBB separating axes
+ * (the hull's H-aligned bounding box vs the box; |R| padded by 1e-5) */
+static int mpr_broadphase(const mpr_obj* o, const real hb[3], const real hh[3]) {
+  real T[3];
+  sub3(T, o->c, hb);
+  real rs = (real)sqrt((double)dot3(hh, hh)) + (real)sqrt((double)dot3(o->h, o->h));
+  if (dot3(T, T) > rs * rs) return 0;
+  real R[3][3], A[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) { R[i][j] = o->ax[3 * i + j]; A[i][j] = (real)fabs((double)R[i][j]) + (real)1e-5; }
+  for (int i = 0; i < 3; i++)
+    if ((real)fabs((double)T[i]) > hh[i] + o->h[0] * A[i][0] + o->h[1] * A[i][1] + o->h[2] * A[i][2]) return 0;
+  for (int j = 0; j < 3; j++) {
+    real s = T[0] * R[0][j] + T[1] * R[1][j] + T[2] * R[2][j];
+    if ((real)fabs((double)s) > hh[0] * A[0][j] + hh[1] * A[1][j] + hh[2] * A[2][j] + o->h[j]) return 0;
+  }
+  for (int i = 0; i < 3; i++) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    for (int j = 0; j < 3; j++) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      real ra = hh[i1] * A[i2][j] + hh[i2] * A[i1][j];
+      real rb = o->h[j1] * A[i][j2] + o->h[j2] * A[i][j1];
+      real s = T[i2] * R[i1][j] - T[i1] * R[i2][j];
+      if ((real)fabs((double)s) > ra + rb) return 0;
+    }
+  }
+  return 1;
+}
+
 static void collision(const so100_model* m, so100o_data* d) {
   d->ncon = 0;
   d->ncon_dropped = 0;
@@ -669,11 +920,40 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = best - top;
     add_contact(d, &con, p);
   }
+  /* pairs 23..76: (cube | bin box, hull k) through the MPR convex collider, in H = hull k's body frame */
+  for (int p = SO100_PAIR_MPR0; p < SO100_NPAIR; p++) {
+    const int k = (p - SO100_PAIR_MPR0) % SO100_NHULL, g = m->pair_geom1[p], b = m->hull_body[k];
+    const real* RH = d->xmat[b];
+    mpr_obj o;
+    real dp[3], hb[3], hh[3];
+    sub3(dp, d->geom_xpos[g], d->xpos[b]);
+    mulmtv3(o.c, RH, dp);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        o.ax[3 * i + j] = RH[i] * d->geom_xmat[g][j] + RH[3 + i] * d->geom_xmat[g][3 + j] + RH[6 + i] * d->geom_xmat[g][6 + j];
+    load3(o.h, m->geom_size[g]);
+    o.vert = (const double (*)[3])m->hull_vert[m->hull_start[k]];
+    o.nvert = m->hull_count[k];
+    load3(o.hc, m->hull_centroid[k]);
+    load3(hb, m->hull_center[k]);
+    load3(hh, m->hull_half[k]);
+    if (!mpr_broadphase(&o, hb, hh)) continue;
+    real depth, dir[3], pos[3];
+    if (!mpr_penetration(&o, &depth, dir, pos)) continue;
+    so100o_contact con;
+    memset(&con, 0, sizeof(con));
+    mulmv3(con.frame, RH, dir);
+    mulmv3(con.pos, RH, pos);
+    for (int t = 0; t < 3; t++) con.pos[t] += d->xpos[b][t];
+    con.dist = -depth;
+    add_contact(d, &con, p);
+  }
 }
 
 uint32_t so100o_contact_bits(const so100o_data* d) {
   uint32_t bits = 0;
-  for (int c = 0; c < d->ncon; c++) bits |= 1u << d->con[c].pair;
+  for (int c = 0; c < d->ncon; c++)
+    if (d->con[c].pair < SO100_NPAIR_BITS) bits |= 1u << d->con[c].pair;
   return bits;
 }
 

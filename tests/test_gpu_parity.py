@@ -405,3 +405,64 @@ def test_hull_table_parity(model, oracle64, oracle32):
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     assert bit_bad <= max(2, 0.05 * len(qv_err))
     env.close()
+
+
+def test_mpr_contact_parity(model, oracle64, oracle32):
+    """Box-hull contacts through the MPR collider (pairs 23..76: the cube and the bin boxes against the
+    arm/jaw hulls): states from fp64-oracle random-action rollouts that hold such
+    contacts, then teacher-forced GPU steps against the oracle at the fp32 floor."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import PAIR_MPR0, NHULL
+    rng = np.random.default_rng(21)
+    d = oracle64.new_data()
+    states, kinds = [], set()
+    for e in range(64):
+        oracle64.reset(model, d, oracle64.spawn_pose(2000 + e))
+        for _ in range(200):
+            oracle64.env_step(model, d, 0, rng.uniform(-1, 1, 6).astype(np.float32))
+            pairs = [d.con[i].pair for i in range(d.ncon)]
+            mp = [p for p in pairs if p >= PAIR_MPR0]
+            if mp and not d.ncon_dropped:
+                q, v, w, _ = oracle64.get_state(d)
+                states.append((q, v, w))
+                kinds.update(p < PAIR_MPR0 + NHULL for p in mp)
+                break
+        if len(states) >= 32:
+            break
+    n = len(states)
+    assert n >= 16 and kinds == {True, False}, (n, kinds)     # both cube-hull and bin-hull contacts
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True)
+    env.reset(seed=3)
+    env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
+                  np.array([s[2] for s in states], np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, mpr_con = [], [], []
+    for step in range(3):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = rng.uniform(-1, 1, (n, 6)).astype(np.float32)
+        env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        dbg = env.debug.cpu().numpy()
+        for i in range(n):
+            pairs = dbg[i, 48:48 + int(dbg[i, 0])]
+            mpr_con.append(int((pairs >= PAIR_MPR0).sum()))
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(model, d64, 0, act[i])
+            oracle32.env_step(model, d32, 0, act[i])
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+    qv_err, qv_floor, mpr_con = np.array(qv_err), np.array(qv_floor), np.array(mpr_con)
+    print(f"\nbox-hull (MPR): {n} envs, GPU MPR contacts per env mean {mpr_con.mean():.2f} (envs with any: "
+          f"{(mpr_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
+          f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
+          f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
+    assert (mpr_con[:n] > 0).mean() > 0.3              # the GPU collider sees the contacts too
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    env.close()

@@ -6,7 +6,7 @@ import copy
 
 import numpy as np
 
-from gym_so100.model import NPAIR_BOX, NHULL
+from gym_so100.model import NPAIR_BOX, NHULL, PAIR_MPR0
 
 NV = 12
 
@@ -66,7 +66,7 @@ def test_hull_table_contacts_match_independent_geometry(model, oracle64):
         d = _state(oracle64, model, arm)
         want = _expected(model, d, hulls)
         got = [(d.con[i].pair, np.array(d.con[i].pos[:]), d.con[i].dist, np.array(d.con[i].frame[:]))
-               for i in range(d.ncon) if d.con[i].pair >= NPAIR_BOX]
+               for i in range(d.ncon) if NPAIR_BOX <= d.con[i].pair < PAIR_MPR0]
         assert [g[0] for g in got] == [w[0] for w in want]          # hull order, one contact per hull
         for (p, pos, dist, fr), (_, wpos, wdist) in zip(got, want):
             np.testing.assert_allclose(pos, wpos, atol=1e-12)
@@ -82,7 +82,7 @@ def test_hull_contacts_are_condim3_rows_on_arm_dofs(model, oracle64):
     d = _state(oracle64, model, arm)
     oracle64.call("so100o_fwd_acceleration", model, d)
     rows = [i for i in range(d.nefc) if d.efc_type[i] == 2 and d.efc_dim[i] > 0]
-    hull_rows = [i for i in rows if d.con[d.efc_id[i]].pair >= NPAIR_BOX]
+    hull_rows = [i for i in rows if NPAIR_BOX <= d.con[d.efc_id[i]].pair < PAIR_MPR0]
     assert hull_rows
     for i in hull_rows:
         assert d.efc_dim[i] == 3
