@@ -1055,10 +1055,20 @@ DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const floa
   const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + o.s0;
   float best = -__builtin_inff(), bx = 0.f, by = 0.f, bz = 0.f;
   int bi = 0x7fffffff;
-  for (int i = lane; i < o.n; i += kLanes) {
-    const float4 v = verts[i];
-    const float sc = n0 * v.x + n1 * v.y + n2 * v.z;
-    if (sc > best) { best = sc; bi = i; bx = v.x; by = v.y; bz = v.z; }
+  // batches of 8 vertices per lane, all 8 loads issued before any use (clamped indices, masked scores,
+  // selects instead of branches): the scan is load-latency bound, not VALU bound
+  for (int base = lane; base < o.n; base += 8 * kLanes) {
+    float4 vb[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) vb[u] = verts[min(base + u * kLanes, o.n - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = base + u * kLanes;
+      const float sc = n0 * vb[u].x + n1 * vb[u].y + n2 * vb[u].z;
+      const bool t = i < o.n && sc > best;
+      best = t ? sc : best; bi = t ? i : bi;
+      bx = t ? vb[u].x : bx; by = t ? vb[u].y : by; bz = t ? vb[u].z : bz;
+    }
   }
 #pragma unroll
   for (int off = 1; off < kLanes; off <<= 1) {
@@ -1353,6 +1363,9 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
     wave_cand |= ((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFull) << (16 * r);
   }
   int ns = 0;
+#ifdef SO100_EXPERIMENT_MPR_BROAD_ONLY
+  wave_cand = 0;   // timing experiment only: broadphase without the narrowphase
+#endif
   while (wave_cand) {
     const int q = __builtin_ctzll(wave_cand);
     wave_cand &= wave_cand - 1ull;
