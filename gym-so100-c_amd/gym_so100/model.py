@@ -36,7 +36,8 @@ def _arr(t, *dims):
 class SO100Model(ctypes.Structure):
     """Mirror of ``so100_model`` (include/so100_model.h) — field order must match exactly."""
     _fields_ = [
-        ("timestep", _d), ("nsubstep", _i), ("iterations", _i), ("tolerance", _d), ("impratio", _d),
+        ("timestep", _d), ("nsubstep", _i), ("iterations", _i), ("solver", _i), ("tolerance", _d),
+        ("impratio", _d),
         ("gravity", _arr(_d, 3)), ("meaninertia", _d),
         ("body_parent", _arr(_i, NBODY)), ("body_pos", _arr(_d, NBODY, 3)), ("body_quat", _arr(_d, NBODY, 4)),
         ("body_ipos", _arr(_d, NBODY, 3)), ("body_iquat", _arr(_d, NBODY, 4)), ("body_mass", _arr(_d, NBODY)),
@@ -90,14 +91,21 @@ def load_model_dict(path=ASSET):
         return json.load(f)
 
 
-def build_model(path=ASSET, iterations=None, nsubstep=None):
-    """Return an ``SO100Model`` ctypes struct filled from the derived model table."""
+SOLVERS = {"pgs": 0, "newton": 1}      # SO100_SOLVER_* (include/so100_model.h)
+
+
+def build_model(path=ASSET, iterations=None, nsubstep=None, solver="pgs"):
+    """Return an ``SO100Model`` ctypes struct filled from the derived model table.
+
+    solver: "pgs" (north_star's projected Gauss-Seidel) or "newton" (MuJoCo's default solver, which the
+    reference's model uses: so_arm100.xml:4 sets no solver)."""
     d = load_model_dict(path)
     m = SO100Model()
     o = d["opt"]
     m.timestep = o["timestep"]
     m.nsubstep = int(round(C.DT / o["timestep"])) if nsubstep is None else int(nsubstep)   # env.py:120-127
     m.iterations = int(o["iterations"] if iterations is None else iterations)
+    m.solver = SOLVERS[solver]
     m.tolerance = o["tolerance"]
     m.impratio = o["impratio"]
     _set(m, "gravity", o["gravity"])

@@ -44,6 +44,8 @@
 #define SO100_MAXCON 16             /* contacts kept per env per position stage           */
 #define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, table/bin-hull pairs are 3 */
 #define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_MAXCON * SO100_CONDIM)
+#define SO100_SOLVER_PGS 0          /* projected Gauss-Seidel on the dual (mj_solPGS)               */
+#define SO100_SOLVER_NEWTON 1       /* primal Newton with exact line search (mj_solNewton)          */
 #define SO100_NOBS 15               /* box(3) bin(3) ee(3) qpos(6) — env.py:137-145      */
 
 #ifdef __cplusplus
@@ -54,7 +56,8 @@ typedef struct so100_model {
   /* options (MuJoCo defaults + so_arm100.xml:4) */
   double timestep;                  /* 0.002 */
   int    nsubstep;                  /* control_timestep / timestep = 10 (env.py:120-127) */
-  int    iterations;                /* PGS sweeps (MuJoCo default 100) */
+  int    iterations;                /* solver iterations: PGS sweeps / Newton steps (MuJoCo default 100) */
+  int    solver;                    /* SO100_SOLVER_PGS (north_star) or SO100_SOLVER_NEWTON (MuJoCo's default) */
   double tolerance;                 /* 1e-8 */
   double impratio;                  /* 10 */
   double gravity[3];

@@ -1315,6 +1315,233 @@ static void sol_pgs(const so100_model* m, so100o_data* d) {
   }
 }
 
+/* ---------------------------------------------------------------- primal Newton solver
+ * [3P] mj_solNewton (engine_solver.c mj_solPrimal with flg_Newton), restated: minimise the convex
+ *   c(a) = 1/2 (a - a_smooth)' M (a - a_smooth) + sum_b s_b(J_b a - aref_b)
+ * over qacc a, where s_b is the soft-constraint cost of block b (mj_constraintUpdate, primal): dof
+ * frictionloss (quadratic inside |jar| < R f, linear outside), joint limits (quadratic when jar < 0),
+ * elliptic contacts (top zone 0, bottom zone quadratic, middle zone 1/2 Dm (N - mu T)^2).  Newton
+ * direction from the Cholesky of H = M + sum_b J_b' H_b J_b (H_b: the block's cost Hessian in jar,
+ * including the middle-zone cone Hessian), exact line search, MuJoCo's termination: scale * (old cost -
+ * new cost) < tolerance or scale * |grad| < tolerance, scale = 1 / (meaninertia nv); alpha = 0 stops.
+ * The start is qacc_warmstart if its cost is below qacc_smooth's (mj_fwdConstraint).  The line search
+ * is ours (a safeguarded 1-D Newton on c'(alpha) to relative precision; MuJoCo brackets to ls_tolerance
+ * 0.01), so the iterates differ from MuJoCo's path but converge to the same unique minimiser. */
+#define LS_TOL (sizeof(real) == 8 ? (real)1e-12 : (real)1e-6)
+
+/* cost, force (= -d cost / d jar) and cost Hessian of the constraint block at row i; returns its rows */
+static int block_eval(const so100o_data* d, int i, const real* jar, real* cost, real f[4], real H[4][4]) {
+  memset(f, 0, sizeof(real) * 4);
+  memset(H, 0, sizeof(real) * 16);
+  *cost = 0;
+  const int t = d->efc_type[i];
+  if (t == SO100O_EFC_FRICTION) {
+    const real fl = d->efc_frictionloss[i], R = d->efc_R[i], D = d->efc_D[i], x = jar[0];
+    if (x >= R * fl) { f[0] = -fl; *cost = fl * x - (real)0.5 * R * fl * fl; }
+    else if (x <= -R * fl) { f[0] = fl; *cost = -fl * x - (real)0.5 * R * fl * fl; }
+    else { f[0] = -D * x; *cost = (real)0.5 * D * x * x; H[0][0] = D; }
+    return 1;
+  }
+  if (t == SO100O_EFC_LIMIT) {
+    const real D = d->efc_D[i], x = jar[0];
+    if (x < 0) { f[0] = -D * x; *cost = (real)0.5 * D * x * x; H[0][0] = D; }
+    return 1;
+  }
+  const int dim = d->efc_dim[i];
+  const real mu = d->efc_mu[i][0] * (real)sqrt((double)(d->efc_R[i + 1] / d->efc_R[i]));
+  real U[4], T = 0;
+  U[0] = jar[0] * mu;
+  for (int k = 1; k < dim; k++) { U[k] = jar[k] * d->efc_mu[i][k - 1]; T += U[k] * U[k]; }
+  T = (real)sqrt((double)T);
+  const real N = U[0];
+  if (N >= mu * T || (T <= 0 && N >= 0)) return dim;                       /* top zone */
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) {                              /* bottom zone */
+    for (int k = 0; k < dim; k++) {
+      const real D = d->efc_D[i + k];
+      f[k] = -D * jar[k];
+      *cost += (real)0.5 * D * jar[k] * jar[k];
+      H[k][k] = D;
+    }
+    return dim;
+  }
+  /* middle zone: c = 1/2 Dm (N - mu T)^2 with g = d(N - mu T)/d jar */
+  const real Dm = d->efc_D[i] / (mu * mu * (1 + mu * mu)), NmT = N - mu * T;
+  real g[4];
+  g[0] = mu;
+  for (int k = 1; k < dim; k++) g[k] = -mu * U[k] * d->efc_mu[i][k - 1] / T;
+  *cost = (real)0.5 * Dm * NmT * NmT;
+  for (int k = 0; k < dim; k++) f[k] = -Dm * NmT * g[k];
+  for (int k = 0; k < dim; k++)
+    for (int l = 0; l < dim; l++) H[k][l] = Dm * g[k] * g[l];
+  for (int k = 1; k < dim; k++)
+    for (int l = 1; l < dim; l++) {
+      const real fk = d->efc_mu[i][k - 1], fl = d->efc_mu[i][l - 1];
+      H[k][l] -= Dm * NmT * mu * fk * fl * ((k == l ? 1 / T : 0) - U[k] * U[l] / (T * T * T));
+    }
+  return dim;
+}
+
+/* total cost at jar (+ Gauss term given separately); forces into f (nefc) */
+static real constraint_cost(const so100o_data* d, const real* jar, real* f) {
+  real c = 0;
+  for (int i = 0; i < d->nefc;) {
+    real cb, fb[4], Hb[4][4];
+    const int n = block_eval(d, i, jar + i, &cb, fb, Hb);
+    for (int k = 0; k < n; k++) f[i + k] = fb[k];
+    c += cb;
+    i += n;
+  }
+  return c;
+}
+static real gauss_cost(const so100o_data* d, const real a[NV]) {
+  real e[NV], c = 0;
+  for (int k = 0; k < NV; k++) e[k] = a[k] - d->qacc_smooth[k];
+  for (int i = 0; i < NV; i++)
+    for (int j = 0; j < NV; j++) c += (real)0.5 * e[i] * d->qM[i][j] * e[j];
+  return c;
+}
+static void jar_at(const so100o_data* d, const real a[NV], real* jar) {
+  for (int i = 0; i < d->nefc; i++) {
+    real s = 0;
+    for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * a[k];
+    jar[i] = s - d->efc_aref[i];
+  }
+}
+/* dense Cholesky solve H x = b (H SPD); returns 0 if not positive definite */
+static int chol_solve(real H[NV][NV], const real b[NV], real x[NV]) {
+  real L[NV][NV];
+  memset(L, 0, sizeof(L));
+  for (int j = 0; j < NV; j++) {
+    real s = H[j][j];
+    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+    if (!(s > 0)) return 0;
+    L[j][j] = (real)sqrt((double)s);
+    for (int i = j + 1; i < NV; i++) {
+      real t = H[i][j];
+      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+      L[i][j] = t / L[j][j];
+    }
+  }
+  real y[NV];
+  for (int i = 0; i < NV; i++) {
+    real s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = NV - 1; i >= 0; i--) {
+    real s = y[i];
+    for (int k = i + 1; k < NV; k++) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  return 1;
+}
+/* c'(alpha), c''(alpha) along a + alpha s (e = a - a_smooth, Js = J s precomputed) */
+static void line_derivs(const so100o_data* d, const real e[NV], const real s[NV], const real* jar0, const real* Js,
+                        real alpha, real* d1, real* d2) {
+  real Ms[NV], g1 = 0, g2 = 0;
+  for (int i = 0; i < NV; i++) {
+    real t = 0;
+    for (int j = 0; j < NV; j++) t += d->qM[i][j] * s[j];
+    Ms[i] = t;
+  }
+  for (int i = 0; i < NV; i++) { g1 += Ms[i] * (e[i] + alpha * s[i]); g2 += Ms[i] * s[i]; }
+  for (int i = 0; i < d->nefc;) {
+    real jar[4], cb, fb[4], Hb[4][4];
+    const int dim = d->efc_type[i] == SO100O_EFC_CONTACT ? d->efc_dim[i] : 1;
+    for (int k = 0; k < dim; k++) jar[k] = jar0[i + k] + alpha * Js[i + k];
+    block_eval(d, i, jar, &cb, fb, Hb);
+    for (int k = 0; k < dim; k++) {
+      g1 -= fb[k] * Js[i + k];
+      for (int l = 0; l < dim; l++) g2 += Js[i + k] * Hb[k][l] * Js[i + l];
+    }
+    i += dim;
+  }
+  *d1 = g1;
+  *d2 = g2;
+}
+static real line_search(const so100o_data* d, const real a[NV], const real s[NV], const real* jar0) {
+  real e[NV], Js[NEFC];
+  for (int k = 0; k < NV; k++) e[k] = a[k] - d->qacc_smooth[k];
+  for (int i = 0; i < d->nefc; i++) {
+    real t = 0;
+    for (int k = 0; k < NV; k++) t += d->efc_J[i][k] * s[k];
+    Js[i] = t;
+  }
+  real d10, d20;
+  line_derivs(d, e, s, jar0, Js, 0, &d10, &d20);
+  if (!(d10 < 0)) return 0;
+  const real tol = LS_TOL * -d10;
+  real lo = 0, hi = -1, alpha = 1;                  /* hi < 0: no upper bracket yet */
+  for (int it = 0; it < 50; it++) {
+    real d1, d2;
+    line_derivs(d, e, s, jar0, Js, alpha, &d1, &d2);
+    if ((real)fabs((double)d1) <= tol) break;
+    if (d1 < 0) lo = alpha; else hi = alpha;
+    real nxt = d2 > 0 ? alpha - d1 / d2 : -1;
+    if (hi >= 0) { if (!(nxt > lo && nxt < hi)) nxt = (real)0.5 * (lo + hi); }
+    else if (!(nxt > lo)) nxt = 2 * alpha;
+    if (nxt == alpha) break;
+    alpha = nxt;
+  }
+  return alpha;
+}
+
+static void sol_newton(const so100_model* m, so100o_data* d) {
+  const int nefc = d->nefc;
+  const real scale = 1 / ((real)m->meaninertia * (real)NV);
+  real a[NV], jar[NEFC], f[NEFC];
+  /* start: the warmstart if it is cheaper than the unconstrained acceleration */
+  jar_at(d, d->qacc_warmstart, jar);
+  const real cw = gauss_cost(d, d->qacc_warmstart) + constraint_cost(d, jar, f);
+  jar_at(d, d->qacc_smooth, jar);
+  const real cs = constraint_cost(d, jar, f);
+  memcpy(a, cw < cs ? d->qacc_warmstart : d->qacc_smooth, sizeof(a));
+  jar_at(d, a, jar);
+  real cost = gauss_cost(d, a) + constraint_cost(d, jar, f);
+  d->solver_iter = 0;
+  d->solver_improvement = 0;
+  for (int it = 0; it < m->iterations; it++) {
+    /* gradient and Hessian at a */
+    real grad[NV], H[NV][NV];
+    for (int i = 0; i < NV; i++) {
+      real t = 0;
+      for (int j = 0; j < NV; j++) { t += d->qM[i][j] * (a[j] - d->qacc_smooth[j]); H[i][j] = d->qM[i][j]; }
+      grad[i] = t;
+    }
+    for (int i = 0; i < nefc;) {
+      real cb, fb[4], Hb[4][4];
+      const int dim = block_eval(d, i, jar + i, &cb, fb, Hb);
+      for (int k = 0; k < dim; k++) {
+        for (int v = 0; v < NV; v++) grad[v] -= d->efc_J[i + k][v] * fb[k];
+        for (int l = 0; l < dim; l++) {
+          if (Hb[k][l] == 0) continue;
+          for (int p = 0; p < NV; p++)
+            for (int q = 0; q < NV; q++) H[p][q] += d->efc_J[i + k][p] * Hb[k][l] * d->efc_J[i + l][q];
+        }
+      }
+      i += dim;
+    }
+    real gn = 0;
+    for (int k = 0; k < NV; k++) gn += grad[k] * grad[k];
+    if (scale * (real)sqrt((double)gn) < (real)m->tolerance) break;
+    real s[NV], mg[NV];
+    for (int k = 0; k < NV; k++) mg[k] = -grad[k];
+    if (!chol_solve(H, mg, s)) break;
+    const real alpha = line_search(d, a, s, jar);
+    d->solver_iter = it + 1;
+    if (alpha == 0) break;
+    for (int k = 0; k < NV; k++) a[k] += alpha * s[k];
+    jar_at(d, a, jar);
+    const real nc = gauss_cost(d, a) + constraint_cost(d, jar, f);
+    const real improvement = scale * (cost - nc);
+    cost = nc;
+    d->solver_improvement = improvement;
+    if (improvement < (real)m->tolerance) break;
+  }
+  constraint_cost(d, jar, d->efc_force);
+  memcpy(d->qacc, a, sizeof(a));
+}
+
 void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   /* [3P] mj_fwdActuation: position actuator, ctrl clamped to ctrlrange, force clamped to forcerange */
   memset(d->qfrc_actuator, 0, sizeof(d->qfrc_actuator));
@@ -1335,10 +1562,13 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   solve_m(d, d->qacc_smooth, rhs);
   const int nefc = d->nefc;
   if (nefc == 0) { memcpy(d->qacc, d->qacc_smooth, sizeof(d->qacc)); d->solver_iter = 0; return; }
-  /* [3P] mj_referenceConstraint + mj_projectConstraint: aref, b, AR = J M^-1 J' + R */
+  /* [3P] mj_referenceConstraint: aref */
+  for (int i = 0; i < nefc; i++)
+    d->efc_aref[i] = -d->efc_B[i] * d->efc_vel[i] - d->efc_K[i] * d->efc_imp[i] * (d->efc_pos[i] - d->efc_margin[i]);
+  if (m->solver == SO100_SOLVER_NEWTON) { sol_newton(m, d); return; }
+  /* [3P] mj_projectConstraint: b, AR = J M^-1 J' + R */
   static __thread real MJT[NEFC][NV];
   for (int i = 0; i < nefc; i++) {
-    d->efc_aref[i] = -d->efc_B[i] * d->efc_vel[i] - d->efc_K[i] * d->efc_imp[i] * (d->efc_pos[i] - d->efc_margin[i]);
     real s = 0;
     for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * d->qacc_smooth[k];
     d->efc_b[i] = s - d->efc_aref[i];

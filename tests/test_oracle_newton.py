@@ -1,0 +1,143 @@
+"""The primal Newton solver (MuJoCo's default, mj_solNewton; the reference's model sets no solver,
+so_arm100.xml:4) in the oracle.
+
+MuJoCo is not in this container; the checks are restated optimality conditions of the same convex
+problem, not MuJoCo's own numbers:
+  * an independent numpy evaluation of the primal cost (Gauss term + frictionloss, limit and elliptic
+    cone costs) has no descent direction at Newton's qacc (gradient ~ 0, no random probe is cheaper);
+  * the dual solver on the same problem (PGS run far past its 100 sweeps) converges to the same qacc;
+  * Newton converges in a handful of iterations where PGS exhausts its 100 sweeps.
+"""
+import numpy as np
+import pytest
+
+from gym_so100.model import build_model
+
+NV = 12
+
+
+def _rollout_states(o, m, n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for e in range(n):
+        d = o.new_data()
+        o.reset(m, d, o.spawn_pose(3000 + e))
+        for _ in range(int(rng.integers(20, 120))):
+            o.env_step(m, d, 0, rng.uniform(-1, 1, 6).astype(np.float32))
+        out.append(o.get_state(d))
+    return out
+
+
+def _solve(o, m, st):
+    d = o.new_data()
+    o.set_state(d, *st)
+    o.call("so100o_fwd_position", m, d)
+    o.call("so100o_fwd_velocity", m, d)
+    o.call("so100o_fwd_acceleration", m, d)
+    return d
+
+
+def _np_problem(d):
+    n = d.nefc
+    J = np.array([[d.efc_J[i][k] for k in range(NV)] for i in range(n)])
+    M = np.array([[d.qM[i][k] for k in range(NV)] for i in range(NV)])
+    return dict(n=n, J=J, M=M, a0=np.array(d.qacc_smooth[:]), aref=np.array(d.efc_aref[:n]),
+                R=np.array(d.efc_R[:n]), fl=np.array(d.efc_frictionloss[:n]), typ=np.array(d.efc_type[:n]),
+                dim=np.array(d.efc_dim[:n]), mu=np.array([d.efc_mu[i][:] for i in range(n)]))
+
+
+def _np_cost(P, a):
+    """Primal cost, restated independently of the oracle (MuJoCo mj_constraintUpdate semantics)."""
+    e = a - P["a0"]
+    c = 0.5 * e @ P["M"] @ e
+    jar = P["J"] @ a - P["aref"]
+    i = 0
+    while i < P["n"]:
+        t, R = P["typ"][i], P["R"][i]
+        D = 1 / R
+        if t == 0:
+            f, x = P["fl"][i], jar[i]
+            c += f * abs(x) - 0.5 * R * f * f if abs(x) >= R * f else 0.5 * D * x * x
+            i += 1
+        elif t == 1:
+            c += 0.5 * D * min(jar[i], 0.0) ** 2
+            i += 1
+        else:
+            dim = P["dim"][i]
+            mu = P["mu"][i][0] * np.sqrt(P["R"][i + 1] / R)
+            U = jar[i:i + dim] * np.concatenate([[mu], P["mu"][i][:dim - 1]])
+            N, T = U[0], np.linalg.norm(U[1:])
+            if N >= mu * T:
+                pass
+            elif mu * N + T <= 0:
+                c += 0.5 * np.sum(jar[i:i + dim] ** 2 / P["R"][i:i + dim])
+            else:
+                Dm = D / (mu * mu * (1 + mu * mu))
+                c += 0.5 * Dm * (N - mu * T) ** 2
+            i += dim
+    return c
+
+
+@pytest.fixture(scope="module")
+def models():
+    return build_model(), build_model(solver="newton"), build_model(solver="newton", iterations=100)
+
+
+def test_newton_is_the_minimiser(models, oracle64):
+    _, mn, _ = models
+    rng = np.random.default_rng(1)
+    nc = 0
+    for st in _rollout_states(oracle64, mn, 24, seed=2):
+        d = _solve(oracle64, mn, st)
+        if d.nefc == 0:
+            continue
+        nc += d.ncon > 0
+        P = _np_problem(d)
+        a = np.array(d.qacc[:])
+        c0 = _np_cost(P, a)
+        # central-difference gradient of the independent cost: ~0 at the minimiser
+        h = 1e-6 * (1 + np.abs(a))
+        g = np.array([(_np_cost(P, a + h[k] * np.eye(NV)[k]) - _np_cost(P, a - h[k] * np.eye(NV)[k])) / (2 * h[k])
+                      for k in range(NV)])
+        gscale = np.abs(P["M"] @ (a - P["a0"])).max() + 1e-3
+        assert np.abs(g).max() < 1e-4 * gscale, (np.abs(g).max(), gscale)
+        for _ in range(20):                                    # no probe direction is cheaper
+            da = rng.normal(size=NV) * 1e-3 * (1 + np.abs(a))
+            assert _np_cost(P, a + da) >= c0 - 1e-12 * (1 + abs(c0))
+    assert nc >= 12
+
+
+def test_newton_matches_converged_dual_solver(models, oracle64):
+    """PGS (dual, 4000 sweeps, tolerance 0) and Newton (primal) solve the same convex problem."""
+    mp, mn, _ = models
+    mp_long = build_model(iterations=4000)
+    mp_long.tolerance = 0.0
+    errs, iters_n, iters_p = [], [], []
+    for st in _rollout_states(oracle64, mn, 16, seed=3):
+        dn = _solve(oracle64, mn, st)
+        dl = _solve(oracle64, mp_long, st)
+        dp = _solve(oracle64, mp, st)
+        an, al = np.array(dn.qacc[:]), np.array(dl.qacc[:])
+        errs.append(np.abs(an - al).max() / (1 + np.abs(an).max()))
+        iters_n.append(dn.solver_iter)
+        iters_p.append(dp.solver_iter)
+    errs = np.array(errs)
+    assert np.median(errs) < 1e-4 and errs.max() < 5e-3, errs
+    assert np.mean(iters_n) < 8 and max(iters_n) <= 30, iters_n
+    assert np.mean(iters_p) > 3 * np.mean(iters_n)
+
+
+def test_newton_free_flight_is_exact(models, oracle64):
+    """No contact (cube in the air, arm away): the problem is the 12 frictionloss rows only, whose
+    minimiser Newton reaches exactly (the fp64 solution does not depend on the start)."""
+    _, mn, _ = models
+    d = oracle64.new_data()
+    oracle64.reset(mn, d, np.array([0.4, 0.95, 0.6, 1, 0, 0, 0]))
+    for _ in range(3):                                         # 60 ms: the cube is still falling
+        oracle64.env_step(mn, d, 0, np.zeros(6, np.float32))
+    st = oracle64.get_state(d)
+    d1 = _solve(oracle64, mn, st)
+    assert d1.ncon == 0
+    st2 = (st[0], st[1], st[2] + 0.3, st[3])                   # another warmstart
+    d2 = _solve(oracle64, mn, st2)
+    np.testing.assert_allclose(np.array(d1.qacc[:]), np.array(d2.qacc[:]), rtol=1e-9, atol=1e-9)
