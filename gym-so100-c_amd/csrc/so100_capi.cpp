@@ -16,7 +16,7 @@
 #include "so100_device.h"
 
 namespace so100 {
-hipError_t launch_step(const DevModel*, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
+hipError_t launch_step(const DevModel*, int, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
                        hipStream_t, hipEvent_t*);
 hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
 hipError_t alloc_workspace(int, Workspace*);
@@ -47,6 +47,7 @@ struct so100_env {
   int n;
   DevModel* d_model;
   int nsubstep;
+  int solver;                   // SO100_SOLVER_* of the model
   std::vector<Chunk> chunks;
   hipEvent_t fork = nullptr;
   int task;
@@ -242,6 +243,8 @@ int build_device_model(const so100_model* s, DevModel* d) {
   d->timestep = (float)s->timestep;
   d->nsubstep = s->nsubstep;
   d->iterations = s->iterations;
+  if (s->solver != SO100_SOLVER_PGS && s->solver != SO100_SOLVER_NEWTON) return fail("model: unknown solver");
+  d->solver = s->solver;
   d->tolerance = (float)s->tolerance;
   d->impratio = (float)s->impratio;
   for (int k = 0; k < 3; k++) d->gravity[k] = (float)s->gravity[k];
@@ -392,7 +395,7 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (e != hipSuccess) { fail_hip("so100_create: hipMalloc", e); return nullptr; }
   e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
-  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
+  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, h.solver, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
   e = make_chunks(env, default_chunks(n_envs));
   if (e != hipSuccess) {
     (void)free_chunks(env);
@@ -458,7 +461,7 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
   const hipStream_t s = (hipStream_t)stream;
   if (env->chunks.size() == 1) {
     Chunk& c = env->chunks[0];
-    hipError_t e = so100::launch_step(env->d_model, env->nsubstep, c.ws, *b, c.count, env->task, flags, env->max_steps,
+    hipError_t e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c.ws, *b, c.count, env->task, flags, env->max_steps,
                                       env->base_seed, env->env_offset, s, ev);
     return e == hipSuccess ? 0 : fail_hip("so100_step", e);
   }
@@ -469,13 +472,13 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
     Chunk& c = env->chunks[k];
     e = hipStreamWaitEvent(c.s, env->fork, 0);
     if (e == hipSuccess)
-      e = so100::launch_step(env->d_model, env->nsubstep, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
+      e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
                              env->max_steps, env->base_seed, env->env_offset + c.start, c.s, nullptr);
     if (e == hipSuccess) e = hipEventRecord(c.done, c.s);
   }
   Chunk& c0 = env->chunks[0];
   if (e == hipSuccess)
-    e = so100::launch_step(env->d_model, env->nsubstep, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
+    e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
                            env->base_seed, env->env_offset, s, ev);
   for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) e = hipStreamWaitEvent(s, env->chunks[k].done, 0);
   return e == hipSuccess ? 0 : fail_hip("so100_step", e);

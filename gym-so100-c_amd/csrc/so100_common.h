@@ -41,6 +41,33 @@ DEV float rowsum16(float v) {
   v += dpp<0x140>(v);  // row_mirror
   return v;
 }
+// ------------------------------------------------------------------ row broadcast (DPP row_newbcast, gfx90a+)
+template <int L>
+DEV float bcast_row_c(float v) { return dpp<0x150 + L>(v); }
+// j must fold to a constant after unrolling; every lane of each 16-lane row receives lane j of that row
+DEV float bcast_row(float v, int j) {
+  switch (j) {
+    case 0: return bcast_row_c<0>(v);
+    case 1: return bcast_row_c<1>(v);
+    case 2: return bcast_row_c<2>(v);
+    case 3: return bcast_row_c<3>(v);
+    case 4: return bcast_row_c<4>(v);
+    case 5: return bcast_row_c<5>(v);
+    case 6: return bcast_row_c<6>(v);
+    case 7: return bcast_row_c<7>(v);
+    case 8: return bcast_row_c<8>(v);
+    case 9: return bcast_row_c<9>(v);
+    case 10: return bcast_row_c<10>(v);
+    case 11: return bcast_row_c<11>(v);
+    case 12: return bcast_row_c<12>(v);
+    case 13: return bcast_row_c<13>(v);
+    case 14: return bcast_row_c<14>(v);
+    default: return bcast_row_c<15>(v);
+  }
+}
+DEV float4 bcast_row4(float4 v, int j) {
+  return make_float4(bcast_row(v.x, j), bcast_row(v.y, j), bcast_row(v.z, j), bcast_row(v.w, j));
+}
 DEV float bcast16(float v, int src) { return __shfl(v, src, kLanes); }
 DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 

@@ -18,6 +18,7 @@ struct DevModel {
   float timestep;
   int nsubstep;
   int iterations;
+  int solver;                       // SO100_SOLVER_PGS | SO100_SOLVER_NEWTON
   float tolerance;
   float impratio;
   float gravity[3];
@@ -129,6 +130,21 @@ enum HdrField : int {
   H_NCON = 39,      // contact count (int bits)
 };
 static_assert(H_NCON + 1 == kHdrLane && kHdrLane % 4 == 0 && kConRec % 4 == 0, "workspace record layout");
+// Newton solver record (model.solver = SO100_SOLVER_NEWTON): the same buffers, one 160-float header per
+// env (H_NCON kept at its PGS offset for the contact counter) and per contact the block
+//   0-3 aref, 4-7 R (normal, t1, t2, torsion), 8 cone mu (= friction0 sqrt(R1/R0)), 9 friction0,
+//   10 friction1 (torsion), then J at kJOff as for PGS.
+enum NewtonHdr : int {
+  N_QS = 0,         // qacc_smooth [12]
+  N_WARM = 12,      // qacc_warmstart [12]
+  N_FRAREF = 24,    // frictionloss rows: aref = -B vel [12]
+  N_LIMS = 40,      // joint-limit rows: side +-1, 0 = inactive [6]
+  N_LIMAREF = 46,   // [6]
+  N_LIMR = 52,      // [6]
+  N_M = 58,         // arm M (incl. armature), row-major 6x6
+  N_MC = 94,        // cube diagonal masses (m, m, m, I0, I1, I2)
+};
+static_assert(N_FRAREF + 12 <= H_NCON && N_MC + 6 <= kHdrEnv, "Newton header layout");
 constexpr int kPgsEnvs = 16;      // solver: envs per wave64 (4 lanes each) = one "group"
 constexpr int kResident = 4;      // solver: contacts per env held on-chip across the sweeps
 constexpr int kHeavyCap = 512;    // solver: groups with > kResident contacts dispatched first (cap)

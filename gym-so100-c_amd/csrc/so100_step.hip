@@ -1407,34 +1407,6 @@ DEV void make_frame(float* f) {
   cross3(f + 6, n, t1);
 }
 
-// ------------------------------------------------------------------ row broadcast (DPP row_newbcast, gfx90a+)
-template <int L>
-DEV float bcast_row_c(float v) { return dpp<0x150 + L>(v); }
-// j must fold to a constant after unrolling; every lane of each 16-lane row receives lane j of that row
-DEV float bcast_row(float v, int j) {
-  switch (j) {
-    case 0: return bcast_row_c<0>(v);
-    case 1: return bcast_row_c<1>(v);
-    case 2: return bcast_row_c<2>(v);
-    case 3: return bcast_row_c<3>(v);
-    case 4: return bcast_row_c<4>(v);
-    case 5: return bcast_row_c<5>(v);
-    case 6: return bcast_row_c<6>(v);
-    case 7: return bcast_row_c<7>(v);
-    case 8: return bcast_row_c<8>(v);
-    case 9: return bcast_row_c<9>(v);
-    case 10: return bcast_row_c<10>(v);
-    case 11: return bcast_row_c<11>(v);
-    case 12: return bcast_row_c<12>(v);
-    case 13: return bcast_row_c<13>(v);
-    case 14: return bcast_row_c<14>(v);
-    default: return bcast_row_c<15>(v);
-  }
-}
-DEV float4 bcast_row4(float4 v, int j) {
-  return make_float4(bcast_row(v.x, j), bcast_row(v.y, j), bcast_row(v.z, j), bcast_row(v.w, j));
-}
-
 // (M^-1 J')[dof] for the 4 rows of a contact: arm dofs use the dense 6x6 M^-1 row (row broadcasts of
 // the other arm lanes' J), cube dofs the diagonal inverse mass.
 DEV float4 minv_times(float4 J, const float* minv_row, float invmc, int lane) {
@@ -1630,7 +1602,7 @@ DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_
 //   kMode 1: Euler with the previous substep's solver output, then the same assembly;
 //   kMode 2: Euler, then the mj_step1 position stage and the task epilogue (reward, obs, autoreset).
 // Assembly writes the solver's per-env record (Workspace) that so100_pgs_kernel consumes.
-template <int kMode>
+template <int kMode, int kSolver>
 #ifndef SO100_STAGE_WAVES
 #define SO100_STAGE_WAVES 3      // waves per SIMD the stage kernel's register budget is sized for
 #endif
@@ -1683,6 +1655,19 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     __syncthreads();
     dynamics_par(m, sh, lane, mscale);
     __syncthreads();
+    if (kSolver == SO100_SOLVER_NEWTON && valid) {
+      // the Newton solver works with M itself: arm rows from the CRBA scratch (which collision reuses),
+      // the cube's diagonal masses
+      float* hd = args.w.hdr + (size_t)e * kHdrEnv;
+      if (lane < 6) {
+#pragma unroll
+        for (int j = 0; j < 6; j++) hd[N_M + 6 * lane + j] = sh.ser.M[lane][j];
+      } else if (lane < 9) {
+        hd[N_MC + lane - 6] = m->cube_mass * mscale;
+      } else if (lane < SO100_NV) {
+        hd[N_MC + lane - 6] = m->cube_inertia[lane - 9] * mscale;
+      }
+    }
     SSTAMP(1);
     // ---------------- S3: collision: hulls vs the table (lane k = hull k), box-hull pairs by MPR
     // (staged in LDS), one box pair per lane; compaction in pair order (box pairs, table-hull pairs,
@@ -1746,7 +1731,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
     SSTAMP(2);
-    if (lane == 0 && ncon > kResident) {
+    if (kSolver == SO100_SOLVER_PGS && lane == 0 && ncon > kResident) {
       // this env's solver group is heavy: list it once for first dispatch (so100_pgs.hip)
       const int g = env / kPgsEnvs, ngroups = (args.n + kPgsEnvs - 1) / kPgsEnvs;
       uint32_t* fl = args.w.gflag + args.par * ngroups + g;
@@ -1800,6 +1785,67 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     if (has_fr) cost_part += 0.5f * fr_R * fr_f * fr_f + fr_f * (qs_r - fr_aref);
     if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
 
+    if constexpr (kSolver == SO100_SOLVER_NEWTON) {
+      // ---------------- Newton record (so100_newton.hip builds its gradients and Hessians from it):
+      // J rows (-> HBM) and J qvel (lane c keeps contact c's), per contact aref, R and the cone
+      // coefficients, the header with qacc_smooth, the warmstart, the frictionloss and limit rows
+      float cVn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < kMaxCon; c++) {
+        if (c < ncon_max) {
+          float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (c < ncon && lane < SO100_NV) {
+            J = contact_jac(m, sh, c, lane);
+            reinterpret_cast<float4*>(crec + c * kConRec + kJOff)[lane] = J;
+          }
+          const bool mine = lane == c;
+          const float v0 = rowsum16(J.x * qvel_r), v1 = rowsum16(J.y * qvel_r);
+          const float v2 = rowsum16(J.z * qvel_r), v3 = rowsum16(J.w * qvel_r);
+          cVn[0] = mine ? v0 : cVn[0]; cVn[1] = mine ? v1 : cVn[1];
+          cVn[2] = mine ? v2 : cVn[2]; cVn[3] = mine ? v3 : cVn[3];
+        }
+      }
+      if (lane < ncon) {
+        const int p = sh.con_pair[lane];
+        const float dist = sh.con_dist[lane];
+        const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
+        const float K = m->pair_K[p], Bd = m->pair_B[p];
+        const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
+        const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
+        float R[4];
+        R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
+        R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
+        R[2] = R[1];
+        R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
+        float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
+        cs[0] = make_float4(-Bd * cVn[0] - K * imp * (dist - m->pair_margin[p]), -Bd * cVn[1], -Bd * cVn[2], -Bd * cVn[3]);
+        cs[1] = make_float4(R[0], R[1], R[2], R[3]);
+        cs[2] = make_float4(mu0 * sqrtf(R[1] / R[0]), mu0, mu1, 0.f);
+      }
+      if (valid) {
+        float* hd = args.w.hdr + (size_t)e * kHdrEnv;
+        if (lane < SO100_NV) { hd[N_QS + lane] = qs_r; hd[N_WARM + lane] = warm_r; hd[N_FRAREF + lane] = fr_aref; }
+        if (lane < 6) { hd[N_LIMS + lane] = lim_on ? lim_s : 0.f; hd[N_LIMAREF + lane] = lim_aref; hd[N_LIMR + lane] = lim_R; }
+        if (lane == 0) hd[H_NCON] = __int_as_float(ncon);
+        if (kMode == 1) {
+          if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
+          if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
+        }
+        if (B.debug && args.sub == m->nsubstep - 1) {
+          float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
+          if (lane < kMaxCon) {
+            dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
+            dbg[48 + lane] = lane < ncon ? (float)sh.con_pair[lane] : -1.f;
+          }
+          if (lane < SO100_NV) dbg[64 + lane] = qs_r;
+          if (lane == 0) {
+            dbg[0] = (float)ncon;
+            dbg[3] = (float)(12 + __popcll(lim_mask & (0xFFFFull << (grp * 16))) + 4 * ncon);
+          }
+        }
+      }
+      return;
+    }
     // ---------------- S6a: per-contact Jacobian rows (-> HBM) and the row reductions (lane = dof, DPP).
     // Lane c keeps contact c's reductions: the scalar setup below then runs once per contact, in parallel
     // over the contacts, instead of redundantly on all 16 lanes for every contact.
@@ -2215,8 +2261,12 @@ hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, fl
 
 // One env step = nsubstep x (stage, solve) + the final stage: 2 * nsubstep + 1 launches on one stream.
 // ev (optional, profiling): 2 nsubstep + 2 events, recorded before the first launch and after each.
-hipError_t launch_step(const DevModel* m, int nsubstep, Workspace& w, const so100_buffers& b, int n, int task,
-                       int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s, hipEvent_t* ev) {
+hipError_t launch_newton(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
+                         hipStream_t s);
+
+hipError_t launch_step(const DevModel* m, int nsubstep, int solver, Workspace& w, const so100_buffers& b, int n,
+                       int task, int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s,
+                       hipEvent_t* ev) {
   StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0, 0};
   const dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
   int k = 0;
@@ -2224,14 +2274,21 @@ hipError_t launch_step(const DevModel* m, int nsubstep, Workspace& w, const so10
   for (int sub = 0; sub <= nsubstep; sub++) {
     a.sub = sub;
     a.par = (int)(w.sub_count & 1u);
-    if (sub == 0) hipLaunchKernelGGL(so100_stage_kernel<0>, grid, dim3(kThreads), 0, s, a);
-    else if (sub < nsubstep) hipLaunchKernelGGL(so100_stage_kernel<1>, grid, dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(so100_stage_kernel<2>, grid, dim3(kThreads), 0, s, a);
+    if (solver == SO100_SOLVER_NEWTON) {
+      if (sub == 0) hipLaunchKernelGGL((so100_stage_kernel<0, SO100_SOLVER_NEWTON>), grid, dim3(kThreads), 0, s, a);
+      else if (sub < nsubstep) hipLaunchKernelGGL((so100_stage_kernel<1, SO100_SOLVER_NEWTON>), grid, dim3(kThreads), 0, s, a);
+      else hipLaunchKernelGGL((so100_stage_kernel<2, SO100_SOLVER_NEWTON>), grid, dim3(kThreads), 0, s, a);
+    } else {
+      if (sub == 0) hipLaunchKernelGGL((so100_stage_kernel<0, SO100_SOLVER_PGS>), grid, dim3(kThreads), 0, s, a);
+      else if (sub < nsubstep) hipLaunchKernelGGL((so100_stage_kernel<1, SO100_SOLVER_PGS>), grid, dim3(kThreads), 0, s, a);
+      else hipLaunchKernelGGL((so100_stage_kernel<2, SO100_SOLVER_PGS>), grid, dim3(kThreads), 0, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[k++], s);
     if (sub < nsubstep) {
-      e = launch_pgs(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, a.par, s);
+      e = solver == SO100_SOLVER_NEWTON ? launch_newton(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, s)
+                                        : launch_pgs(m, w, b.qacc_warmstart, b.debug, n, sub == nsubstep - 1, a.par, s);
       if (e != hipSuccess) return e;
       if (ev) (void)hipEventRecord(ev[k++], s);
       w.sub_count++;

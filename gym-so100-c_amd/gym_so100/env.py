@@ -29,7 +29,7 @@ class SO100Env(_Base):
 
     def __init__(self, task, obs_type="so100_state", render_mode="rgb_array", observation_width=640,
                  observation_height=480, visualization_width=640, visualization_height=480, device="cuda:0",
-                 max_episode_steps=0):
+                 max_episode_steps=0, solver="pgs"):
         super().__init__()
         self.task = task
         self.obs_type = obs_type
@@ -38,7 +38,7 @@ class SO100Env(_Base):
         self.visualization_width, self.visualization_height = visualization_width, visualization_height
         # TimeLimit is applied by the gymnasium registry wrapper (as in the reference); 0 = none here
         self._venv = SO100VecEnv(1, task=task, obs_type=obs_type, device=device, autoreset=False,
-                                 max_episode_steps=max_episode_steps)
+                                 max_episode_steps=max_episode_steps, solver=solver)
         self.observation_space = spaces.Box(low=-100.0, high=100.0, shape=(len(SO100_JOINTS) + 3 * 3,),
                                             dtype=np.float32)           # env.py:67-73
         self.action_space = spaces.Box(low=-1, high=1, shape=(len(SO100_ACTIONS),), dtype=np.float32)
@@ -67,12 +67,12 @@ class SO100GoalEnv(_Base):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
 
     def __init__(self, render_mode="rgb_array", observation_width=640, observation_height=480,
-                 visualization_width=640, visualization_height=480, device="cuda:0"):
+                 visualization_width=640, visualization_height=480, device="cuda:0", solver="pgs"):
         super().__init__()
         self.max_episode_steps = 300                                     # env.py:200
         self.current_step = 0
         self.render_mode = render_mode
-        self._venv = SO100VecEnv(1, task="so100_goal", device=device, autoreset=False)
+        self._venv = SO100VecEnv(1, task="so100_goal", device=device, autoreset=False, solver=solver)
         self.distance_threshold = GOAL_DISTANCE_THRESHOLD                # env.py:252
         obs_space = spaces.Box(low=-np.inf, high=np.inf, shape=(15,), dtype=np.float32)
         self.observation_space = spaces.Dict({

@@ -52,13 +52,16 @@ class SO100VecEnv:
             per-env cube mass / friction scales (fixed per env) + Gaussian action noise.
         env_offset: global index of this shard's first env (multi-GPU sharding); in-kernel seeds use
             the global env id so trajectories do not depend on the number of GPUs.
-        iterations: PGS sweeps per substep (default: model's 100, MuJoCo's default).
+        iterations: solver iterations per substep, PGS sweeps or Newton steps (default: the model's 100,
+            MuJoCo's default).
+        solver: "pgs" (north_star's projected Gauss-Seidel, the default) or "newton" (MuJoCo's default
+            solver, which the reference's model runs: the unique minimiser of the constraint problem).
         debug: allocate the [N, 96] diagnostics buffer (contacts, forces, solver iterations).
     """
 
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
-                 iterations=None, debug=False):
+                 iterations=None, debug=False, solver="pgs"):
         torch = _torch()
         if obs_type != "so100_state":
             raise NotImplementedError(
@@ -77,7 +80,8 @@ class SO100VecEnv:
         self.max_episode_steps = _MAX_STEPS[task] if max_episode_steps is None else int(max_episode_steps)
         self.base_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.env_offset = int(env_offset)
-        self.model = build_model(iterations=iterations)
+        self.solver = solver
+        self.model = build_model(iterations=iterations, solver=solver)
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._handle = self.lib.so100_create(ctypes.byref(self.model), self.num_envs, dev_index)
         if not self._handle:

@@ -466,3 +466,57 @@ def test_mpr_contact_parity(model, oracle64, oracle32):
     assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     env.close()
+
+
+def test_newton_solver_parity(oracle64, oracle32):
+    """MuJoCo's default solver (primal Newton, solver="newton"): teacher-forced GPU steps against the fp64
+    oracle's Newton from random-action rollout states (contacts on the table, bin, gripper and hulls),
+    at the fp32 floor (the fp32 oracle's Newton on the same states); 2-6 Newton steps per substep."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import build_model
+    mn = build_model(solver="newton")
+    n = 48
+    rng = np.random.default_rng(31)
+    d = oracle64.new_data()
+    states = []
+    for e in range(n):
+        oracle64.reset(mn, d, oracle64.spawn_pose(4000 + e))
+        for _ in range(int(rng.integers(10, 160))):
+            oracle64.env_step(mn, d, 0, rng.uniform(-1, 1, 6).astype(np.float32))
+        states.append(oracle64.get_state(d)[:3])
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver="newton")
+    env.reset(seed=3)
+    env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
+                  np.array([s[2] for s in states], np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, iters, ncon = [], [], [], []
+    for step in range(3):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = rng.uniform(-1, 1, (n, 6)).astype(np.float32)
+        env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        dbg = env.debug.cpu().numpy()
+        iters += list(dbg[:, 1])
+        ncon += list(dbg[:, 0])
+        for i in range(n):
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(mn, d64, 0, act[i])
+            oracle32.env_step(mn, d32, 0, act[i])
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+    qv_err, qv_floor, iters, ncon = np.array(qv_err), np.array(qv_floor), np.array(iters), np.array(ncon)
+    print(f"\nnewton: contacts/env {ncon.mean():.2f}, GPU Newton steps per substep mean {iters.mean():.2f} max "
+          f"{iters.max():.0f} | qvel rel GPU median {np.median(qv_err):.2e} p90 {np.quantile(qv_err, .9):.2e} max "
+          f"{qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} p90 {np.quantile(qv_floor, .9):.2e} "
+          f"max {qv_floor.max():.2e}")
+    assert ncon.mean() > 1.0
+    assert iters.max() <= 30 and iters.mean() < 10
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    env.close()
