@@ -32,6 +32,10 @@ BYTES_PER_ENV_STEP = 408
 # (160 B) + J rows (192 B) read once.
 SOLVER_BYTES_PER_ENV = 640 + 48
 SOLVER_BYTES_PER_CONTACT = 160 + 192
+# Newton record (so100_device.h NewtonHdr): header 100 floats read + qacc write; per contact 12 floats of
+# block + 48 of J read
+NEWTON_BYTES_PER_ENV = 4 * 100 + 48
+NEWTON_BYTES_PER_CONTACT = 4 * (12 + 48)
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 CLOCK_HZ = 2.4e9             # MI355X peak engine clock (valu_busy uses it: a lower real clock only raises the share)
 SIMDS = 1024                 # 256 CUs x 4 SIMDs
@@ -59,6 +63,8 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the per-launch HIP events")
     p.add_argument("--contact-steps", type=int, default=10, help="untimed steps sampling contacts/env")
+    p.add_argument("--solver", default="pgs", choices=["pgs", "newton"],
+                   help="constraint solver: pgs (north_star, default) or newton (MuJoCo's default)")
     return p.parse_args(argv)
 
 
@@ -90,10 +96,11 @@ def cpu_baseline(seconds):
                       f"{t_used:.1f}s)"}
 
 
-def load_traffic(n_envs):
+def load_traffic(n_envs, solver="pgs"):
     """(HBM bytes per solver launch of n_envs envs, VALU wave-instructions per env step) from the
-    committed rocprofv3 PMC passes (profiles/pmc_traffic.json, tests/_pmc_traffic.py), or (None, None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    committed rocprofv3 PMC passes (profiles/pmc_traffic[_newton].json, tests/_pmc_traffic.py), or
+    (None, None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if solver == "pgs" else f"pmc_traffic_{solver}.json")
     if not os.path.exists(path):
         return None, None
     try:
@@ -132,7 +139,7 @@ def main(argv=None):
         scaling = "strong"
 
     from gym_so100 import SO100VecEnv
-    env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset)
+    env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset, solver=args.solver)
     env.reset(seed=1000 + offset)   # env i <- RandomState(1000 + global id)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed * 1000003 + rank)
@@ -187,9 +194,11 @@ def main(argv=None):
         value = env_steps / elapsed
         # the timed launches are chunk 0's (n0 envs), concurrent with the other chunks' (so100_chunk_info)
         nchunks, n0 = env.chunk_info()
-        solver_bytes = n0 * (SOLVER_BYTES_PER_ENV + SOLVER_BYTES_PER_CONTACT * contacts_per_env)
+        per_env, per_con = ((SOLVER_BYTES_PER_ENV, SOLVER_BYTES_PER_CONTACT) if args.solver == "pgs" else
+                            (NEWTON_BYTES_PER_ENV, NEWTON_BYTES_PER_CONTACT))
+        solver_bytes = n0 * (per_env + per_con * contacts_per_env)
         achieved = solver_bytes / (solver_ms * 1e-3)
-        traffic, valu_insts = load_traffic(n0)
+        traffic, valu_insts = load_traffic(n0, args.solver)
         # VALU issue share of the timed run: insts x 2 cyc (wave64 on SIMD-32) / (step x 2.4 GHz x 1024 SIMDs)
         valu_busy = valu_insts * 2.0 / (step_ms * 1e-3 * CLOCK_HZ * SIMDS) if valu_insts else None
         line = {
@@ -200,11 +209,11 @@ def main(argv=None):
                                     f"({count} per GPU), joint-space ctrl, fp32 state, CubeToBin reward, "
                                     "auto-reset"),
                        "envs_total": total, "envs_per_gpu": count, "task": args.task, "substeps": 10,
-                       "pgs_iterations": env.model.iterations, "parallelism": f"env-sharded x{world}, no collectives",
+                       "solver": args.solver, "solver_iterations": env.model.iterations, "parallelism": f"env-sharded x{world}, no collectives",
                        "actions": "U[-1,1]^6 pool resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic, "valu_busy": valu_busy,
-                         "kernel": "so100_pgs_kernel", "kernel_ms": solver_ms,
+                         "kernel": f"so100_{args.solver}_kernel", "kernel_ms": solver_ms,
                          "bytes_per_launch": solver_bytes, "envs_per_launch": n0, "concurrent_chunks": nchunks,
                          "contacts_per_env": contacts_per_env,
                          "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
