@@ -6,7 +6,8 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One "step" = one batched env step of every env on every GPU: action prologue, 10 physics substeps
-(kinematics, CRBA/RNE, box-box contacts, PGS, semi-implicit Euler), the final position stage,
+(kinematics, CRBA/RNE, box-box / hull / MPR contacts, the constraint solve -- primal Newton, MuJoCo's
+default and so the reference's, or --solver pgs -- and semi-implicit Euler), the final position stage,
 reward/obs epilogue, TimeLimit + in-kernel auto-reset — 21 HIP launches per GPU per step (per substep a
 stage kernel and a solver kernel, then the final stage kernel).
 Envs are sharded contiguously (global ids drive the seeds); there is no collective on the data path:
@@ -27,7 +28,7 @@ METRIC = "env steps/sec (whole node), 65k parallel bin-a-cube envs at 1/2/4/8 MI
 # + warmstart 48 + elapsed 4 + episode 4 = 180; writes qpos 52 + qvel 48 + warmstart 48 + obs 60 + reward 4
 # + terminated/truncated/success/diverged 4 + contact_bits 4 + elapsed 4 + episode 4 = 228.
 BYTES_PER_ENV_STEP = 408
-# dominant kernel = the PGS solver (so100_pgs.hip).  Algorithmic bytes per launch: per env the solver
+# dominant kernel = the solver (so100_newton.hip / so100_pgs.hip).  PGS algorithmic bytes per launch: per env the solver
 # record header (4 lanes x 40 floats = 640 B) read + qacc (48 B) written; per contact the solver block
 # (160 B) + J rows (192 B) read once.
 SOLVER_BYTES_PER_ENV = 640 + 48
@@ -63,12 +64,12 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the per-launch HIP events")
     p.add_argument("--contact-steps", type=int, default=10, help="untimed steps sampling contacts/env")
-    p.add_argument("--solver", default="pgs", choices=["pgs", "newton"],
-                   help="constraint solver: pgs (north_star, default) or newton (MuJoCo's default)")
+    p.add_argument("--solver", default="newton", choices=["newton", "pgs"],
+                   help="constraint solver: newton (MuJoCo's default, which the reference runs; default) or pgs")
     return p.parse_args(argv)
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, solver="newton"):
     """Time the oracle (fp64 C restatement, OpenMP over envs) on this host's cores — a reported,
     non-target baseline (the reference's MuJoCo is not installed here)."""
     import ctypes
@@ -77,7 +78,7 @@ def cpu_baseline(seconds):
     from oracle.oracle import Oracle
     from gym_so100.model import build_model
     o = Oracle(64)
-    m = build_model()
+    m = build_model(solver=solver)
     cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     nenv = 4 * cores
     datas = (o.Data * nenv)()
@@ -92,8 +93,8 @@ def cpu_baseline(seconds):
         done += o.batch_run(m, datas, nenv, steps_per_call, 0, acts, nthreads=cores)
         t_used += time.perf_counter() - t0
     return {"value": done / t_used, "unit": "env_steps/s", "cores": cores, "kind": "port",
-            "sample": f"{nenv} CubeToBin envs x {done // nenv} steps (fp64 oracle, OpenMP {cores} threads, "
-                      f"{t_used:.1f}s)"}
+            "sample": f"{nenv} CubeToBin envs x {done // nenv} steps (fp64 oracle, {solver} solver, OpenMP "
+                      f"{cores} threads, {t_used:.1f}s)"}
 
 
 def load_traffic(n_envs, solver="pgs"):
@@ -226,7 +227,7 @@ def main(argv=None):
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+                line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.solver)
             except Exception as e:   # baseline is reported, never required for the GPU number
                 line["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
         print(json.dumps(line), flush=True)

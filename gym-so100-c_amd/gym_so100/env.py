@@ -29,7 +29,7 @@ class SO100Env(_Base):
 
     def __init__(self, task, obs_type="so100_state", render_mode="rgb_array", observation_width=640,
                  observation_height=480, visualization_width=640, visualization_height=480, device="cuda:0",
-                 max_episode_steps=0, solver="pgs"):
+                 max_episode_steps=0, solver="newton"):
         super().__init__()
         self.task = task
         self.obs_type = obs_type
@@ -67,7 +67,7 @@ class SO100GoalEnv(_Base):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
 
     def __init__(self, render_mode="rgb_array", observation_width=640, observation_height=480,
-                 visualization_width=640, visualization_height=480, device="cuda:0", solver="pgs"):
+                 visualization_width=640, visualization_height=480, device="cuda:0", solver="newton"):
         super().__init__()
         self.max_episode_steps = 300                                     # env.py:200
         self.current_step = 0

@@ -94,11 +94,11 @@ def load_model_dict(path=ASSET):
 SOLVERS = {"pgs": 0, "newton": 1}      # SO100_SOLVER_* (include/so100_model.h)
 
 
-def build_model(path=ASSET, iterations=None, nsubstep=None, solver="pgs"):
+def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton"):
     """Return an ``SO100Model`` ctypes struct filled from the derived model table.
 
-    solver: "pgs" (north_star's projected Gauss-Seidel) or "newton" (MuJoCo's default solver, which the
-    reference's model uses: so_arm100.xml:4 sets no solver)."""
+    solver: "newton" (default: MuJoCo's default solver, which the reference's model uses --
+    so_arm100.xml:4 sets no solver) or "pgs" (north_star's projected Gauss-Seidel)."""
     d = load_model_dict(path)
     m = SO100Model()
     o = d["opt"]

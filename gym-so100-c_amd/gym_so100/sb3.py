@@ -40,7 +40,7 @@ class SO100SB3VecEnv(_VecEnvBase):
     metadata = {"render_modes": []}
 
     def __init__(self, num_envs, task="so100_cube_to_bin", device="cuda:0", seed=0, max_episode_steps=None,
-                 domain_randomization=None, env_offset=0, iterations=None, solver="pgs"):
+                 domain_randomization=None, env_offset=0, iterations=None, solver="newton"):
         self.venv = SO100VecEnv(num_envs, task=task, device=device, seed=seed, max_episode_steps=max_episode_steps,
                                 autoreset=True, domain_randomization=domain_randomization, env_offset=env_offset,
                                 iterations=iterations, solver=solver)

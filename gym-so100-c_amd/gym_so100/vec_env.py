@@ -54,14 +54,14 @@ class SO100VecEnv:
             the global env id so trajectories do not depend on the number of GPUs.
         iterations: solver iterations per substep, PGS sweeps or Newton steps (default: the model's 100,
             MuJoCo's default).
-        solver: "pgs" (north_star's projected Gauss-Seidel, the default) or "newton" (MuJoCo's default
-            solver, which the reference's model runs: the unique minimiser of the constraint problem).
+        solver: "newton" (default: MuJoCo's default solver, which the reference's model runs; the
+            unique minimiser of the constraint problem) or "pgs" (north_star's projected Gauss-Seidel).
         debug: allocate the [N, 96] diagnostics buffer (contacts, forces, solver iterations).
     """
 
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
-                 iterations=None, debug=False, solver="pgs"):
+                 iterations=None, debug=False, solver="newton"):
         torch = _torch()
         if obs_type != "so100_state":
             raise NotImplementedError(

@@ -116,11 +116,17 @@ def _oracle_precision_floor(model, o64, o32, states):
     return np.array(qp), np.array(qv)
 
 
-def test_step_parity_teacher_forced(venv, model, oracle64, oracle32):
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_step_parity_teacher_forced(solver, oracle64, oracle32):
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import build_model
+    model = build_model(solver=solver)
+    venv = SO100VecEnv(64, device="cuda:0", autoreset=False, debug=True, max_episode_steps=0, solver=solver)
     qp, qv, rew_bad, bit_bad, states = _teacher_forced(venv, model, oracle64, steps=40, seed=1000)
+    venv.close()
     fqp, fqv = _oracle_precision_floor(model, oracle64, oracle32, states)
     n = len(qv)
-    print(f"\nGPU vs fp64 oracle over {n} env-steps: qpos abs median {np.median(qp):.2e} p99 {np.quantile(qp, .99):.2e}"
+    print(f"\n[{solver}] GPU vs fp64 oracle over {n} env-steps: qpos abs median {np.median(qp):.2e} p99 {np.quantile(qp, .99):.2e}"
           f" | qvel rel median {np.median(qv):.2e} p99 {np.quantile(qv, .99):.2e} max {qv.max():.2e}"
           f" | within 1e-4: {np.mean(qv < 1e-4):.3f}")
     print(f"fp32 oracle vs fp64 oracle (precision floor): qvel rel median {np.median(fqv):.2e} "
@@ -134,10 +140,13 @@ def test_step_parity_teacher_forced(venv, model, oracle64, oracle32):
     assert bit_bad <= max(4, 0.01 * n)
 
 
-def test_free_flight_bit_close(model, oracle64):
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_free_flight_bit_close(solver, oracle64):
     """No contacts at all (cube in the air, arm high): GPU equals the fp64 oracle to fp32 rounding."""
     from gym_so100 import SO100VecEnv
-    env = SO100VecEnv(8, device="cuda:0", autoreset=False, max_episode_steps=0)
+    from gym_so100.model import build_model
+    model = build_model(solver=solver)
+    env = SO100VecEnv(8, device="cuda:0", autoreset=False, max_episode_steps=0, solver=solver)
     env.reset(seed=7)
     qpos = env.qpos.clone()
     qpos[:, 8] = 0.6
@@ -297,12 +306,15 @@ def test_single_env_api():
     assert rb.dtype == np.float32 and (rb == 0).all()
 
 
-def test_heavy_contact_parity(model, oracle64, oracle32):
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_heavy_contact_parity(solver, oracle64, oracle32):
     """Cube pressed into a bin corner: floor + two walls give up to 12 contacts, beyond the solver's 4
     on-chip slots — exercises the streamed-overflow contacts and the heavy-group first dispatch."""
     from gym_so100 import SO100VecEnv
+    from gym_so100.model import build_model
+    model = build_model(solver=solver)
     n = 32
-    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True)
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
     env.reset(seed=5)
     rng = np.random.default_rng(7)
     qpos = env.qpos.cpu().numpy().astype(np.float64)
@@ -336,7 +348,7 @@ def test_heavy_contact_parity(model, oracle64, oracle32):
             qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
             qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
     qv_err, qv_floor, ncon = np.array(qv_err), np.array(qv_floor), np.concatenate(ncon)
-    print(f"\nheavy contacts: GPU ncon mean {ncon.mean():.1f} max {ncon.max():.0f} | qvel rel GPU median "
+    print(f"\n[{solver}] heavy contacts: GPU ncon mean {ncon.mean():.1f} max {ncon.max():.0f} | qvel rel GPU median "
           f"{np.median(qv_err):.2e} p90 {np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median "
           f"{np.median(qv_floor):.2e} p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
     assert (ncon > 4).mean() > 0.5                      # the overflow path is really exercised
@@ -346,11 +358,13 @@ def test_heavy_contact_parity(model, oracle64, oracle32):
     env.close()
 
 
-def test_hull_table_parity(model, oracle64, oracle32):
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_hull_table_parity(solver, oracle64, oracle32):
     """Arm/jaw hulls resting on the table (pairs 14..22, condim 3): states made by the
     fp64 oracle driving the arm down onto the table, then teacher-forced GPU steps against it."""
     from gym_so100 import SO100VecEnv
-    from gym_so100.model import NPAIR_BOX
+    from gym_so100.model import NPAIR_BOX, build_model
+    model = build_model(solver=solver)
     n = 24
     rng = np.random.default_rng(11)
     d = oracle64.new_data()
@@ -367,7 +381,7 @@ def test_hull_table_parity(model, oracle64, oracle32):
         q, v, w, _ = oracle64.get_state(d)
         states.append((q, v, w))
         targets.append((target - lo) / (hi - lo) * 2 - 1)      # keep pressing: the same targets as actions
-    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True)
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
     env.reset(seed=3)
     env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
                   np.array([s[2] for s in states], np.float32))
@@ -395,7 +409,7 @@ def test_hull_table_parity(model, oracle64, oracle32):
             qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
             bit_bad += oracle64.contact_bits(d64) != gb[i]
     qv_err, qv_floor, hull_con = np.array(qv_err), np.array(qv_floor), np.array(hull_con)
-    print(f"\nhull-table: GPU hull contacts per env mean {hull_con.mean():.2f} (envs with any: "
+    print(f"\n[{solver}] hull-table: GPU hull contacts per env mean {hull_con.mean():.2f} (envs with any: "
           f"{(hull_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
           f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
           f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e} | contact-bit mismatches {bit_bad}")
@@ -407,12 +421,14 @@ def test_hull_table_parity(model, oracle64, oracle32):
     env.close()
 
 
-def test_mpr_contact_parity(model, oracle64, oracle32):
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_mpr_contact_parity(solver, oracle64, oracle32):
     """Box-hull contacts through the MPR collider (pairs 23..76: the cube and the bin boxes against the
     arm/jaw hulls): states from fp64-oracle random-action rollouts that hold such
     contacts, then teacher-forced GPU steps against the oracle at the fp32 floor."""
     from gym_so100 import SO100VecEnv
-    from gym_so100.model import PAIR_MPR0, NHULL
+    from gym_so100.model import PAIR_MPR0, NHULL, build_model
+    model = build_model(solver=solver)
     rng = np.random.default_rng(21)
     d = oracle64.new_data()
     states, kinds = [], set()
@@ -431,7 +447,7 @@ def test_mpr_contact_parity(model, oracle64, oracle32):
             break
     n = len(states)
     assert n >= 16 and kinds == {True, False}, (n, kinds)     # both cube-hull and bin-hull contacts
-    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True)
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
     env.reset(seed=3)
     env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
                   np.array([s[2] for s in states], np.float32))
@@ -457,7 +473,7 @@ def test_mpr_contact_parity(model, oracle64, oracle32):
             qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
             qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
     qv_err, qv_floor, mpr_con = np.array(qv_err), np.array(qv_floor), np.array(mpr_con)
-    print(f"\nbox-hull (MPR): {n} envs, GPU MPR contacts per env mean {mpr_con.mean():.2f} (envs with any: "
+    print(f"\n[{solver}] box-hull (MPR): {n} envs, GPU MPR contacts per env mean {mpr_con.mean():.2f} (envs with any: "
           f"{(mpr_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
           f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
           f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")

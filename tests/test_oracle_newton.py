@@ -80,7 +80,7 @@ def _np_cost(P, a):
 
 @pytest.fixture(scope="module")
 def models():
-    return build_model(), build_model(solver="newton"), build_model(solver="newton", iterations=100)
+    return build_model(solver="pgs"), build_model(solver="newton"), build_model(solver="newton", iterations=100)
 
 
 def test_newton_is_the_minimiser(models, oracle64):
@@ -110,7 +110,7 @@ def test_newton_is_the_minimiser(models, oracle64):
 def test_newton_matches_converged_dual_solver(models, oracle64):
     """PGS (dual, 4000 sweeps, tolerance 0) and Newton (primal) solve the same convex problem."""
     mp, mn, _ = models
-    mp_long = build_model(iterations=4000)
+    mp_long = build_model(iterations=4000, solver="pgs")
     mp_long.tolerance = 0.0
     errs, iters_n, iters_p = [], [], []
     for st in _rollout_states(oracle64, mn, 16, seed=3):

@@ -179,8 +179,11 @@ def test_separated_boxes_no_contact(model, oracle64):
     assert d.ncon == 0
 
 
-def test_pgs_frictionloss_kkt(model, oracle64):
-    """Arm moving, no contacts: every frictionloss row satisfies the box-constrained optimality."""
+def test_pgs_frictionloss_kkt(oracle64):
+    """Arm moving, no contacts: every frictionloss row satisfies the box-constrained optimality (PGS, the
+    dual solver: efc_AR / efc_b are its data)."""
+    from gym_so100.model import build_model
+    model = build_model(solver="pgs")
     d = fresh(oracle64, model, box=(-0.2, 0.45, 0.5, 1, 0, 0, 0))
     rng = np.random.default_rng(4)
     for k in range(6):
