@@ -219,10 +219,13 @@ def main(argv=None):
                          "contacts_per_env": contacts_per_env,
                          "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
                          "boundary_bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "note": ("solver = serial Gauss-Seidel chains per env: issue/latency-bound, not HBM-bound "
-                                  "(DESIGN.md §3.5); traffic = measured PMC bytes per solver launch; valu_busy = PMC SQ_INSTS_VALU "
-                                  "per step x 2 cyc / (step time x 2.4 GHz x 1024 SIMDs): VALU issue share beside the HBM share "
-                                  "(SURVEY §8d)")},
+                         "note": ((f"solver = primal Newton ({args.solver}): per env a 12x12 Hessian, its Cholesky "
+                                   "factor and an exact line search on 16 lanes, 2-3 Newton steps per substep; "
+                                   if args.solver == "newton" else
+                                   "solver = serial Gauss-Seidel chains per env, 100 sweeps; ") +
+                                  "issue/latency-bound, not HBM-bound (DESIGN.md §3.5); traffic = measured PMC bytes per "
+                                  "solver launch; valu_busy = PMC SQ_INSTS_VALU per step x 2 cyc / (step time x 2.4 GHz x "
+                                  "1024 SIMDs): VALU issue share beside the HBM share (SURVEY §8d)")},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

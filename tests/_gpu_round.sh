@@ -1,9 +1,9 @@
-# round-end measurement set (writes gpurun_out/r01/*): parity tests, smoke, bench line, kernel trace,
-# PMC traffic of the solver kernel, SQ counters.
+# round-end measurement set (writes gpurun_out/r01/*): parity tests, smoke, bench line (default solver:
+# Newton), kernel trace, PMC traffic of the solver kernel, SQ counters; then the PGS bench line and trace.
 export TMPDIR=/tmp
 O=gpurun_out/r01
 rm -rf $O; mkdir -p $O
-timeout -k 10 600 python -m pytest tests -m gpu -q -rA > $O/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -rA --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc" >> $O/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
@@ -14,8 +14,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc -o fetch --output-format 
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc -o write --output-format csv -- $B > $O/pmc_write.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $O/pmc -o sq --output-format csv -- $B > $O/pmc_sq.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $O/pmc -o misc --output-format csv -- $B > $O/pmc_misc.log 2>&1 || exit $?
-python tests/_pmc_traffic.py $O/pmc 16384 $O/pmc_traffic.json 4 > $O/pmc_traffic.log 2>&1 || exit $?
+python tests/_pmc_traffic.py $O/pmc 16384 $O/pmc_traffic_newton.json 4 newton > $O/pmc_traffic.log 2>&1 || exit $?
 python tests/_pmc_report.py $O/pmc > $O/pmc_report.txt 2>&1 || exit $?
 python tests/_trace_report.py $O/trace > $O/trace_report.txt 2>&1 || exit $?
 lscpu > $O/lscpu.txt 2>&1; nproc > $O/nproc.txt; echo "OMP_NUM_THREADS=$OMP_NUM_THREADS" >> $O/nproc.txt
+timeout -k 10 300 python bench.py --solver pgs --no-cpu-baseline > $O/bench_pgs.json 2> $O/bench_pgs.err || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_pgs -o bench_pgs --output-format csv -- python bench.py --solver pgs --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace_pgs.log 2>&1 || exit $?
 echo ROUNDDONE

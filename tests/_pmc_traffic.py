@@ -14,14 +14,21 @@ MI355X_MICROARCH.md) / (step time x 2.4 GHz x 1024 SIMDs).  Counter passes seria
 per-dispatch busy figure from GRBM_GUI_ACTIVE would miss the chunks' overlap; it is recorded as
 valu_issue_frac_serialised for reference only.
 
-usage: python tests/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json> [chunks]
+usage: python tests/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json> [chunks] [solver]
+solver: newton (so100_newton_kernel) or pgs (so100_pgs_kernel; default for old profiles).  The Newton
+kernel's reads mix 16-B J rows with 4-B header loads; the same x2 correction is applied (the J rows
+dominate) and it is marked uncalibrated in the JSON.
 """
 import csv, glob, json, sys
+
+SOLVER = sys.argv[5] if len(sys.argv) > 5 else "pgs"
+KERNEL = f"so100_{SOLVER}_kernel"
+
 
 def per_launch(pattern, counter):
     vals = []
     for f in glob.glob(pattern):
-        rows = [r for r in csv.DictReader(open(f)) if "pgs_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        rows = [r for r in csv.DictReader(open(f)) if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter]
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
         vals += [float(r["Counter_Value"]) for r in rows[-20:]]
     return sum(vals) / len(vals) if vals else None
@@ -42,12 +49,13 @@ def kernel_mean(pattern, counter, name):
 
 
 per_kernel = {k: kernel_mean(d + "/sq*counter_collection.csv", "SQ_INSTS_VALU", k)
-              for k in ("so100_pgs_kernel", "so100_stage_kernel<0>", "so100_stage_kernel<1>", "so100_stage_kernel<2>")}
-step_insts = chunks * (10 * per_kernel["so100_pgs_kernel"] + per_kernel["so100_stage_kernel<0>"] +
-                       9 * per_kernel["so100_stage_kernel<1>"] + per_kernel["so100_stage_kernel<2>"])
+              for k in (KERNEL, "so100_stage_kernel<0,", "so100_stage_kernel<1,", "so100_stage_kernel<2,")}
+step_insts = chunks * (10 * per_kernel[KERNEL] + per_kernel["so100_stage_kernel<0,"] +
+                       9 * per_kernel["so100_stage_kernel<1,"] + per_kernel["so100_stage_kernel<2,"])
 fetch = per_launch(d + "/fetch*counter_collection.csv", "FETCH_SIZE")
 write = per_launch(d + "/write*counter_collection.csv", "WRITE_SIZE")
-res = {"kernel": "so100_pgs_kernel", "n_envs": n,
+res = {"kernel": KERNEL, "n_envs": n, "fetch_correction": "x2 (16-B/lane reads)" if SOLVER == "pgs" else
+       "x2 (J rows 16-B/lane; 4-B header loads uncalibrated)",
        "fetch_kb_raw": fetch, "write_kb": write,
        "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
        "sq_insts_valu": insts, "grbm_gui_active": gui, "chunks": chunks,
