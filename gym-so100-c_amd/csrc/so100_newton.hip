@@ -303,7 +303,8 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
         derivs(0.f, d10, d20);
         float alpha = 0.f;
         if (d10 < 0.f) {
-          const float tol_ls = 1e-6f * -d10;
+          // fp32 stops (oracle LS_TOL / LS_STEP): MuJoCo's ls_tolerance 0.01 on |c'|, or a relative step 1e-4
+          const float tol_ls = 1e-2f * -d10;
           float lo = 0.f, hi = -1.f;
           alpha = 1.f;
           for (int ls = 0; ls < 50; ls++) {
@@ -315,6 +316,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
             if (hi >= 0.f) { if (!(nxt > lo && nxt < hi)) nxt = 0.5f * (lo + hi); }
             else if (!(nxt > lo)) nxt = 2.f * alpha;
             if (nxt == alpha) break;
+            if (fabsf(nxt - alpha) <= 1e-4f * fabsf(alpha)) { alpha = nxt; break; }
             alpha = nxt;
           }
         }
@@ -335,7 +337,8 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
           const float improvement = scale * (cost - nc);
           cost = nc;
           last_impr = improvement;
-          if (improvement < tolerance) done = true;
+          // MuJoCo's test, and the fp32 relative one (oracle NEWTON_RELTOL): 1e-8 is below fp32 resolution
+          if (improvement < tolerance || improvement < 1e-6f * scale * fabsf(cost)) done = true;
         }
       }
     }
