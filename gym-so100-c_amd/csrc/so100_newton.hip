@@ -124,6 +124,8 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
   const int e = valid ? env : 0;
   const bool dof = lane < SO100_NV;
   const float* __restrict__ hd = a.w.hdr + (size_t)e * kHdrEnv;
+  STAMP_DECL
+  STAMP(-1);
 
   // ---------------- record -> registers
   const float qs = dof ? hd[N_QS + lane] : 0.f;
@@ -165,6 +167,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
     c_mu = mu.x; c_fr0 = mu.y; c_fr1 = mu.z;
   }
 
+
   // cost of the rows this lane owns at (frictionloss / limit jar of its dof, contact jar)
   auto rows_cost = [&](float xfr, float xlim, const float* xc) {
     float cost = 0.f, f, h, cc, fc[4], hc[10];
@@ -175,6 +178,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
     return cost;
   };
 
+  STAMP(0);
   // ---------------- start: the warmstart if its cost is below qacc_smooth's (mj_fwdConstraint)
   float qacc, jc[4];
   {
@@ -196,6 +200,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
   float gauss = 0.5f * rowsum16(dof ? ev * Me : 0.f);
   float cost = gauss + rowsum16(rows_cost(jfr, jlim, jc));
   const float scale = m->pgs_scale, tolerance = m->tolerance;
+  STAMP(1);
 
   bool done = !valid;
   int iters = 0;
@@ -222,6 +227,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
       }
       grad = dof ? grad : 0.f;
       const float gn = sqrtf(rowsum16(grad * grad));
+      STAMP(2);
       if (scale * gn < tolerance) {
         done = true;
       } else {
@@ -234,6 +240,8 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
         }
 #pragma unroll
         for (int c = 0; c < kMaxCon; c++) {
+          // (skipping contacts whose Hessian is zero in every env of the wave, or zero J columns, measured
+          // 2% slower: the uniform branches cost more than the DPP/FMA they save)
           if (c < ncon_max) {
             float hb[10];
 #pragma unroll
@@ -243,6 +251,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
             for (int j = 0; j < SO100_NV; j++) H[j] += dot4(w, bcast_row4(J[c], j));
           }
         }
+        STAMP(3);
         // ---- Cholesky H = L L' (lane i: row i of L; lc: column i, gathered from the broadcasts)
         float lc[SO100_NV], dinv = 1.f;
 #pragma unroll
@@ -276,6 +285,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
           else if (lane < k) sv -= lc[k] * xk;
         }
         sv = dof ? sv : 0.f;
+        STAMP(4);
         // ---- exact line search on c(a + alpha s): safeguarded 1-D Newton on c'(alpha) (oracle line_search)
         const float Ms = mul_m(mrow, mcd, sv);
         const float A1 = rowsum16(dof ? Ms * ev : 0.f), A2 = rowsum16(dof ? Ms * sv : 0.f);
@@ -299,8 +309,15 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
           d1 = rowsum16(l1) + A1 + al * A2;
           d2 = rowsum16(l2) + A2;
         };
-        float d10, d20;
-        derivs(0.f, d10, d20);
+        // c'(0) from the forces already evaluated at the current point (= derivs(0)'s d1)
+        float d10;
+        {
+          float l1 = 0.f;
+          l1 -= f_fr * sfr;
+          l1 -= f_lim * slim;
+          l1 -= fc[0] * jsc[0] + fc[1] * jsc[1] + fc[2] * jsc[2] + fc[3] * jsc[3];
+          d10 = rowsum16(l1) + A1;
+        }
         float alpha = 0.f;
         if (d10 < 0.f) {
           // fp32 stops (oracle LS_TOL / LS_STEP): MuJoCo's ls_tolerance 0.01 on |c'|, or a relative step 1e-4
@@ -321,6 +338,7 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
           }
         }
         iters = it + 1;
+        STAMP(5);
         if (alpha == 0.f) {
           done = true;
         } else {
@@ -340,13 +358,21 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
           // MuJoCo's test, and the fp32 relative one (oracle NEWTON_RELTOL): 1e-8 is below fp32 resolution
           if (improvement < tolerance || improvement < 1e-6f * scale * fabsf(cost)) done = true;
         }
+        STAMP(6);
       }
     }
   }
 
+  STAMP(7);
   // ---------------- qacc -> HBM (the next stage's Euler input and the next substep's warmstart)
   if (valid) {
     if (dof) a.qacc_out[(size_t)env * SO100_NV + lane] = qacc;
+#ifdef SO100_STAMPS
+    if (a.last && a.debug && lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) a.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)st_acc_[k];
+    }
+#endif
     if (a.last && a.debug) {
       float* dbg = a.debug + (size_t)env * SO100_DBG_STRIDE;
       float cc, f_fr, h, fc[4], hc[10];

@@ -1675,7 +1675,9 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     float hx, hy, hz;
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
+    SSTAMP(6);
     const int nmpr = mpr_contacts(m, sh, lane, grp, valid);
+    SSTAMP(7);
     PairContacts pc;
     pc.n = 0;
     if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
@@ -1805,6 +1807,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
           cVn[2] = mine ? v2 : cVn[2]; cVn[3] = mine ? v3 : cVn[3];
         }
       }
+      SSTAMP(3);
       if (lane < ncon) {
         const int p = sh.con_pair[lane];
         const float dist = sh.con_dist[lane];
@@ -1822,6 +1825,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
         cs[1] = make_float4(R[0], R[1], R[2], R[3]);
         cs[2] = make_float4(mu0 * sqrtf(R[1] / R[0]), mu0, mu1, 0.f);
       }
+      SSTAMP(4);
       if (valid) {
         float* hd = args.w.hdr + (size_t)e * kHdrEnv;
         if (lane < SO100_NV) { hd[N_QS + lane] = qs_r; hd[N_WARM + lane] = warm_r; hd[N_FRAREF + lane] = fr_aref; }
@@ -1831,6 +1835,13 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
           if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
           if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
         }
+        SSTAMP(5);
+#ifdef SO100_STAGE_STAMPS
+        if (B.debug && args.sub == m->nsubstep - 1 && lane == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
+        }
+#endif
         if (B.debug && args.sub == m->nsubstep - 1) {
           float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
           if (lane < kMaxCon) {
@@ -2021,7 +2032,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 #ifdef SO100_STAGE_STAMPS
       if (B.debug && args.sub == m->nsubstep - 1 && lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
+        for (int k = 0; k < 8; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
       }
 #endif
       // debug: contact set of the last substep (forces / iterations come from the solver kernel)

@@ -1,4 +1,5 @@
-"""Diagnostic: per-phase cycles of the stage kernel (mode 1, last substep); stage-stamps build via SO100_LIB."""
+"""Diagnostic: per-phase cycles of the stage kernel (mode 1, last substep); stage-stamps build via SO100_LIB.
+usage: SO100_LIB=<stamps build> python tests/_stage_stamps_report.py [solver]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -6,17 +7,18 @@ sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv
 n = 65536
-env = SO100VecEnv(n, device="cuda:0", debug=True)
+env = SO100VecEnv(n, device="cuda:0", debug=True, solver=sys.argv[1] if len(sys.argv) > 1 else "newton")
 env.reset(seed=1000)
 g = torch.Generator(device="cuda").manual_seed(0)
 for i in range(60):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
-acc = np.zeros(6)
+acc = np.zeros(8)
 for i in range(3):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
-    acc += env.debug.cpu().numpy()[::4, 88:94].mean(0)
+    acc += env.debug.cpu().numpy()[::4, 88:96].mean(0)
 acc /= 3
-names = ["Euler", "S1-S2 serial chain", "S3 collision", "S6a J + reductions", "S6b per-contact setup", "S7 + record"]
+names = ["Euler", "S1-S2 FK + dynamics", "S3c box-box + compaction", "S6a J + reductions", "S6b per-contact setup",
+         "S7 + record", "S3a hulls vs table", "S3b box-hull MPR"]
 for k, v in zip(names, acc):
     print(f"{k:24s} {v / 1e3:8.1f} Kcyc  {100 * v / acc.sum():5.1f}%")
