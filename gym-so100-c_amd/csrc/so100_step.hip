@@ -296,6 +296,17 @@ DEV void cube_frame(const float* qp, float* pos, float* mat) {
   pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
 }
 
+// the 6 hinge half-angle sines/cosines, one per lane (lanes 0..5), staged in sh.vec for fk_stage: the
+// transcendentals leave the serial chain on lane 0.  A barrier must separate it from fk_stage.
+DEV void joint_sincos(EnvShared& sh, int lane, bool act = true) {
+  if (act && lane < 6) {
+    float sn, cs;
+    sincosf(0.5f * sh.qpos[lane], &sn, &cs);
+    sh.vec[2 * lane] = sn;
+    sh.vec[2 * lane + 1] = cs;
+  }
+}
+
 // full serial stage; writes frames, M^-1, qacc_smooth, sites into sh
 // Forward kinematics of the 6-link chain (lane 0 of the env's row): body frames, joint anchors/axes,
 // jaw frames, sites, cube frame.  dynamics_par continues from these.
@@ -314,8 +325,7 @@ DEV void fk_stage(const DevModel* __restrict__ m, EnvShared& sh) {
       float R2[9], ax[3];
       quat2mat(R2, quat);
       mulmv3(ax, R2, m->jnt_axis[a]);
-      float sn, cs;
-      sincosf(0.5f * sh.qpos[a], &sn, &cs);
+      const float sn = sh.vec[2 * a], cs = sh.vec[2 * a + 1];    // joint_sincos
       float qj[4] = {cs, m->jnt_axis[a][0] * sn, m->jnt_axis[a][1] * sn, m->jnt_axis[a][2] * sn};
       quat_mul(quat, quat, qj);
       quat_normalize(quat);
@@ -833,10 +843,17 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
 #pragma unroll
   for (int k = 4; k < 8; k++) { P.x[k] = 0.f; P.y[k] = 0.f; }
   const float src1 = sel3(SR, c1), src2 = sel3(SR, c2), srcN = sel3(SR, codeN);
-  clip_stage(P, Pq, 0, -1.f, src1);
-  clip_stage(Pq, P, 0, 1.f, src1);
-  clip_stage(P, Pq, 1, -1.f, src2);
-  clip_stage(Pq, P, 1, 1.f, src2);
+  // an incident face inside the reference face's rectangle (the cube resting on the table) passes the
+  // four clip stages unchanged, in order: skip them (bitwise the same polygon)
+  bool inside = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) inside = inside && -P.x[k] < src1 && P.x[k] < src1 && -P.y[k] < src2 && P.y[k] < src2;
+  if (!inside) {
+    clip_stage(P, Pq, 0, -1.f, src1);
+    clip_stage(Pq, P, 0, 1.f, src1);
+    clip_stage(P, Pq, 1, -1.f, src2);
+    clip_stage(Pq, P, 1, 1.f, src2);
+  }
   const int n = P.n;
   if (n < 1) return;
   float det = m11 * m22 - m12 * m21;
@@ -1651,6 +1668,8 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
     __syncthreads();
     // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
+    joint_sincos(sh, lane);
+    __syncthreads();
     if (lane == 0) fk_stage(m, sh);
     __syncthreads();
     dynamics_par(m, sh, lane, mscale);
@@ -2056,6 +2075,8 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
   __syncthreads();
+  joint_sincos(sh, lane);
+  __syncthreads();
   if (lane == 0) fk_stage(m, sh);
   __syncthreads();
   float hx, hy, hz;
@@ -2129,6 +2150,8 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     __syncthreads();
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
     __syncthreads();
+    joint_sincos(sh, lane, do_reset && valid);
+    __syncthreads();
     if (lane == 0 && do_reset && valid) fk_stage(m, sh);
     __syncthreads();
     const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
@@ -2198,6 +2221,8 @@ __global__ void __launch_bounds__(kThreads) so100_reset_kernel(ResetArgs args) {
     env_reset_state(m, sh, lane, seed, qpos_r, qvel_r, warm_r, nullptr);
   }
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
+  __syncthreads();
+  joint_sincos(sh, lane, act);
   __syncthreads();
   if (lane == 0 && act) fk_stage(m, sh);
   __syncthreads();
