@@ -37,6 +37,22 @@ def _torch():
     return torch
 
 
+def _splitmix64(x):
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def _hash_uniform(seed, ids, field):
+    """U[0,1) per global env id from a counter-based hash (splitmix64), independent of sharding."""
+    with np.errstate(over="ignore"):
+        key = _splitmix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ (ids * np.uint64(0x100000001B3)) ^
+                          np.uint64(field * 0xD1B54A32D192ED03 & 0xFFFFFFFFFFFFFFFF))
+    return (key >> np.uint64(40)).astype(np.float64) / float(1 << 24)
+
+
 class SO100VecEnv:
     """N parallel SO-ARM100 envs on one GPU.
 
@@ -132,16 +148,17 @@ class SO100VecEnv:
         return _native.stream_ptr(_torch(), self.device)
 
     def set_domain_randomization(self, mass=(0.8, 1.2), friction=(0.8, 1.2), action_noise=0.05, seed=None):
-        """Per-env cube mass scale, contact friction scale (fixed per env) and action-noise sigma."""
+        """Per-env cube mass scale, contact friction scale (fixed per env) and action-noise sigma.
+
+        The scales are a counter-based hash of (seed, global env id), so an env draws the same parameters
+        whatever the sharding (configs[4]: 32,768 envs over 4 GPUs)."""
         torch = _torch()
-        g = torch.Generator(device="cpu")
-        g.manual_seed(self.base_seed + 7919 * (self.env_offset + 1) if seed is None else int(seed))
-        n = self.num_envs
-        p = torch.empty(n, 4, dtype=torch.float32)
-        p[:, 0] = torch.empty(n).uniform_(mass[0], mass[1], generator=g)
-        p[:, 1] = torch.empty(n).uniform_(friction[0], friction[1], generator=g)
+        s = self.base_seed if seed is None else int(seed)
+        ids = np.arange(self.env_offset, self.env_offset + self.num_envs, dtype=np.uint64)
+        p = torch.zeros(self.num_envs, 4, dtype=torch.float32)
+        p[:, 0] = torch.from_numpy(mass[0] + (mass[1] - mass[0]) * _hash_uniform(s, ids, 1))
+        p[:, 1] = torch.from_numpy(friction[0] + (friction[1] - friction[0]) * _hash_uniform(s, ids, 2))
         p[:, 2] = float(action_noise)
-        p[:, 3] = 0.0
         self.dr_params = p.to(self.device)
         self._flags |= _native.SO100_FLAG_DR
         if hasattr(self, "_buf"):

@@ -536,3 +536,51 @@ def test_newton_solver_parity(oracle64, oracle32):
     assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     env.close()
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_goal_env_config3_size(solver):
+    """configs[3] size (GoalEnv, 16,384 envs, randomized cube spawn): 40 steps with auto-reset keep the
+    state finite and the dict-obs contract: achieved_goal = the cube site, sparse reward consistent with
+    the goal distance, the lifted-goal curriculum box around each spawn."""
+    from gym_so100 import SO100VecEnv
+    n = 16384
+    env = SO100VecEnv(n, task="so100_goal", device="cuda:0", seed=4, solver=solver)
+    obs, _ = env.reset(seed=7)
+    spawn = env.qpos[:, 6:8].clone()
+    dg0 = obs["desired_goal"].clone()
+    assert ((dg0[:, :2] - spawn).abs() <= 0.03 + 1e-6).all()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for _ in range(40):
+        o, r, term, trunc, info = env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
+        dist = (o["achieved_goal"] - o["desired_goal"]).norm(dim=1)
+        ok = ~info["_final_observation"] if "_final_observation" in info else torch.ones_like(term)
+        assert torch.equal(r[ok], torch.where(dist[ok] < 0.01, 0.0, -1.0))
+    torch.cuda.synchronize()
+    assert torch.isfinite(env.qpos).all() and torch.isfinite(env.qvel).all()
+    assert torch.allclose(o["observation"][:, :3], o["achieved_goal"])
+    assert (env.total_steps == 40).all()
+    env.close()
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_domain_randomization_config4_shard(solver):
+    """configs[4] shard (32,768 DR envs over 4 GPUs = 8,192 per GPU): the shard at env_offset 8,192 draws
+    the same per-env parameters and runs the same trajectories as those envs of a 16,384-env run."""
+    from gym_so100 import SO100VecEnv
+    dr = dict(mass=(0.8, 1.2), friction=(0.8, 1.2), action_noise=0.05)
+    full = SO100VecEnv(16384, device="cuda:0", seed=6, domain_randomization=dr, solver=solver)
+    shard = SO100VecEnv(8192, device="cuda:0", seed=6, domain_randomization=dr, env_offset=8192, solver=solver)
+    full.reset(seed=[5000 + i for i in range(16384)])
+    shard.reset(seed=[5000 + 8192 + i for i in range(8192)])
+    assert torch.equal(full.dr_params[8192:], shard.dr_params)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(10):
+        a = torch.rand(16384, 6, generator=g, device="cuda") * 2 - 1
+        full.step(a)
+        shard.step(a[8192:].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(full.qpos[8192:], shard.qpos)
+    assert torch.isfinite(full.qpos).all()
+    full.close()
+    shard.close()
