@@ -226,13 +226,22 @@ int build_device_model(const so100_model* s, DevModel* d) {
       return fail("model: hull vertex range out of bounds");
   }
   // (box, hull) pairs of the MPR collider: box j = cube (geom 9) then the bin boxes (geoms 10..14), hull k
-  for (int p = SO100_PAIR_MPR0; p < SO100_NPAIR; p++) {
+  for (int p = SO100_PAIR_MPR0; p < SO100_PAIR_SELF0; p++) {
     const int q = p - SO100_PAIR_MPR0, j = q / SO100_NHULL, k = q % SO100_NHULL;
     const int g = SO100_CUBE_GEOM + j;
     if (s->pair_geom1[p] != g || s->pair_geom2[p] != -1 - k) return fail("model: MPR pair p must be (box j, hull k)");
     if (s->pair_body1[p] != s->geom_body[g] || s->pair_body2[p] != s->hull_body[k]) return fail("model: MPR pair bodies");
     if (j > 0 && s->geom_body[g] != 0) return fail("model: bin boxes must be static");
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: MPR pairs must have condim 3 or 4");
+    if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
+  }
+  // hull-hull self-collision pairs: two hulls on different arm links
+  for (int p = SO100_PAIR_SELF0; p < SO100_NPAIR; p++) {
+    const int k1 = -1 - s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
+    if (k1 < 0 || k1 >= SO100_NHULL || k2 < 0 || k2 >= SO100_NHULL) return fail("model: self pair must be two hulls");
+    if (s->pair_body1[p] != s->hull_body[k1] || s->pair_body2[p] != s->hull_body[k2] || k1 == k2)
+      return fail("model: self pair bodies");
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: self pairs must have condim 3 or 4");
     if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
   }
   for (int g = 0; g < SO100_NGEOM; g++) {

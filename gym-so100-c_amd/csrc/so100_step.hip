@@ -1028,8 +1028,14 @@ struct MprSup {
   float v[3], v1[3], v2[3];
 };
 struct MprObj {
-  float c[3], ax[9], h[3], hc[3];   // box centre, axes (columns of ax), half sizes; hull centroid (all H)
-  int s0, n;                        // hull vertex range
+  float c[3], ax[9], h[3];          // obj1 frame in H: origin (box centre / hull body origin), axes
+                                    // (columns of ax); box half sizes
+  float c1[3], bc[3], bh[3];        // obj1 centre (box centre / hull centroid), bounding box centre and half
+                                    // extents (axes ax), in H
+  float hc[3];                      // obj2 (hull) centroid in H
+  int hull1;                        // obj1: -1 a box, else a hull (self-collision); uniform over the wave
+  int s1, n1;                       // obj1 hull vertex range
+  int s0, n;                        // obj2 hull vertex range
 };
 constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
 constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
@@ -1058,31 +1064,21 @@ DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
   }
 }
 
-DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const float* d, MprSup& s, int lane) {
-#pragma unroll
-  for (int t = 0; t < 3; t++) s.v1[t] = o.c[t];
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    const float l = o.ax[i] * d[0] + o.ax[3 + i] * d[1] + o.ax[6 + i] * d[2];
-    const float sz = l >= 0.f ? o.h[i] : -o.h[i];
-#pragma unroll
-    for (int t = 0; t < 3; t++) s.v1[t] += sz * o.ax[3 * t + i];
-  }
-  const float n0 = -d[0], n1 = -d[1], n2 = -d[2];
-  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + o.s0;
+// first vertex of hull range [s0, s0 + n) maximising (n0, n1, n2) . v: lanes split the vertices, then a
+// 16-lane (score, index) max keeps the oracle's first maximal vertex; every lane of the row gets it
+DEV float3 hull_support(const DevModel* __restrict__ m, int s0, int cnt, float n0, float n1, float n2, int lane) {
+  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + s0;
   float best = -__builtin_inff(), bx = 0.f, by = 0.f, bz = 0.f;
   int bi = 0x7fffffff;
-  // batches of 8 vertices per lane, all 8 loads issued before any use (clamped indices, masked scores,
-  // selects instead of branches): the scan is load-latency bound, not VALU bound
-  for (int base = lane; base < o.n; base += 8 * kLanes) {
+  for (int base = lane; base < cnt; base += 8 * kLanes) {
     float4 vb[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) vb[u] = verts[min(base + u * kLanes, o.n - 1)];
+    for (int u = 0; u < 8; u++) vb[u] = verts[min(base + u * kLanes, cnt - 1)];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int i = base + u * kLanes;
       const float sc = n0 * vb[u].x + n1 * vb[u].y + n2 * vb[u].z;
-      const bool t = i < o.n && sc > best;
+      const bool t = i < cnt && sc > best;
       best = t ? sc : best; bi = t ? i : bi;
       bx = t ? vb[u].x : bx; by = t ? vb[u].y : by; bz = t ? vb[u].z : bz;
     }
@@ -1094,7 +1090,32 @@ DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const floa
     const int oi = __shfl_xor(bi, off, kLanes);
     if (os > best || (os == best && oi < bi)) { best = os; bi = oi; bx = ox; by = oy; bz = oz; }
   }
-  s.v2[0] = bx; s.v2[1] = by; s.v2[2] = bz;
+  return make_float3(bx, by, bz);
+}
+
+DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const float* d, MprSup& s, int lane) {
+#pragma unroll
+  for (int t = 0; t < 3; t++) s.v1[t] = o.c[t];
+  if (o.hull1 < 0) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const float l = o.ax[i] * d[0] + o.ax[3 + i] * d[1] + o.ax[6 + i] * d[2];
+      const float sz = l >= 0.f ? o.h[i] : -o.h[i];
+#pragma unroll
+      for (int t = 0; t < 3; t++) s.v1[t] += sz * o.ax[3 * t + i];
+    }
+  } else {
+    // obj1 hull: the direction into its body frame, its support back into H
+    float dl[3], w[3];
+    mulmtv3(dl, o.ax, d);
+    const float3 v = hull_support(m, o.s1, o.n1, dl[0], dl[1], dl[2], lane);
+    const float vv[3] = {v.x, v.y, v.z};
+    mulmv3(w, o.ax, vv);
+#pragma unroll
+    for (int t = 0; t < 3; t++) s.v1[t] += w[t];
+  }
+  const float3 v = hull_support(m, o.s0, o.n, -d[0], -d[1], -d[2], lane);
+  s.v2[0] = v.x; s.v2[1] = v.y; s.v2[2] = v.z;
   sub3(s.v, s.v1, s.v2);
 }
 DEV void portal_dir(const MprSup* P, float* dir) {
@@ -1123,7 +1144,7 @@ DEV void portal_expand(MprSup* P, const MprSup& v4) {
 // -1: no intersection, 0: portal, 1: touching on v1, 2: origin on the segment v0-v1
 DEV int mpr_discover(const DevModel* __restrict__ m, const MprObj& o, MprSup* P, int lane) {
 #pragma unroll
-  for (int t = 0; t < 3; t++) { P[0].v1[t] = o.c[t]; P[0].v2[t] = o.hc[t]; }
+  for (int t = 0; t < 3; t++) { P[0].v1[t] = o.c1[t]; P[0].v2[t] = o.hc[t]; }
   sub3(P[0].v, P[0].v1, P[0].v2);
   if (ccd_zero(P[0].v[0]) && ccd_zero(P[0].v[1]) && ccd_zero(P[0].v[2])) P[0].v[0] += kCcdEps * 10.f;
   float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]}, va[3], vb[3];
@@ -1277,22 +1298,30 @@ DEV bool mpr_penetration(const DevModel* __restrict__ m, const MprObj& o, float&
   return true;
 }
 
-// Box j (0 = the cube, 1..5 = bin boxes) in hull k's body frame H: centre, axes (columns), half sizes.
-DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int j, int k, MprObj& o) {
-  const int a = m->hull_body[k] - 2, g = SO100_CUBE_GEOM + j;
+// Convex pair p (23..97): obj1 = box geom (cube, bin box) or hull k1 (self-collision), obj2 = hull k, both
+// in hull k's body frame H.  Oracle collision().
+DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int p, MprObj& o) {
+  const int g = m->pair_g1[p], k = -1 - m->pair_g2[p];
+  const int a = m->hull_body[k] - 2;
   const float* RH = sh.ser.xm[a];
   const float* pH = sh.ser.xp[a];
   float pb[3], Rb[9];
-  if (j == 0) {
+  if (g == SO100_CUBE_GEOM) {
 #pragma unroll
     for (int t = 0; t < 3; t++) pb[t] = sh.cube_pos[t];
 #pragma unroll
     for (int t = 0; t < 9; t++) Rb[t] = sh.cube_mat[t];
-  } else {
+  } else if (g >= 0) {
 #pragma unroll
     for (int t = 0; t < 3; t++) pb[t] = m->geom_pos[g][t];
 #pragma unroll
     for (int t = 0; t < 9; t++) Rb[t] = m->geom_mat[g][t];
+  } else {
+    const int a1 = m->hull_body[-1 - g] - 2;
+#pragma unroll
+    for (int t = 0; t < 3; t++) pb[t] = sh.ser.xp[a1][t];
+#pragma unroll
+    for (int t = 0; t < 9; t++) Rb[t] = sh.ser.xm[a1][t];
   }
   float dp[3];
   sub3(dp, pb, pH);
@@ -1301,26 +1330,63 @@ DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int 
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int jj = 0; jj < 3; jj++) o.ax[3 * i + jj] = RH[i] * Rb[jj] + RH[3 + i] * Rb[3 + jj] + RH[6 + i] * Rb[6 + jj];
+  o.hull1 = g >= 0 ? -1 : -1 - g;
+  if (g >= 0) {
 #pragma unroll
-  for (int t = 0; t < 3; t++) o.h[t] = m->geom_size[g][t];
+    for (int t = 0; t < 3; t++) { o.h[t] = m->geom_size[g][t]; o.c1[t] = o.c[t]; o.bc[t] = o.c[t]; o.bh[t] = o.h[t]; }
+    o.s1 = 0; o.n1 = 0;
+  } else {
+    const int k1 = o.hull1;
+    const float4 c4 = reinterpret_cast<const float4*>(m->hull_centroid)[k1];
+    const float4 b4 = reinterpret_cast<const float4*>(m->hull_center)[k1];
+    const float4 h4 = reinterpret_cast<const float4*>(m->hull_half)[k1];
+    const float cl[3] = {c4.x, c4.y, c4.z}, bl[3] = {b4.x, b4.y, b4.z};
+    float t1[3], t2[3];
+    mulmv3(t1, o.ax, cl);
+    mulmv3(t2, o.ax, bl);
+#pragma unroll
+    for (int t = 0; t < 3; t++) { o.h[t] = 0.f; o.c1[t] = t1[t] + o.c[t]; o.bc[t] = t2[t] + o.c[t]; }
+    o.bh[0] = h4.x; o.bh[1] = h4.y; o.bh[2] = h4.z;
+    o.s1 = m->hull_start[k1];
+    o.n1 = m->hull_count[k1];
+  }
   const float4 hc = reinterpret_cast<const float4*>(m->hull_centroid)[k];
   o.hc[0] = hc.x; o.hc[1] = hc.y; o.hc[2] = hc.z;
   o.s0 = m->hull_start[k];
   o.n = m->hull_count[k];
 }
-// conservative broadphase, stage 1 (oracle mpr_broadphase): bounding spheres, tested in the world frame
-// (the box centre against hull k's box centre; radii precomputed: hull_half.w, |half sizes| of the box)
-DEV bool mpr_sphere(const DevModel* __restrict__ m, const EnvShared& sh, int j, int k) {
-  const int a = m->hull_body[k] - 2, g = SO100_CUBE_GEOM + j;
+// conservative broadphase, stage 1 (oracle mpr_broadphase): bounding spheres in the world frame: obj1's
+// centre (box centre / hull box centre) against hull k's box centre; radii precomputed (hull_half.w,
+// |half sizes| of a box)
+DEV bool mpr_sphere(const DevModel* __restrict__ m, const EnvShared& sh, int p) {
+  const int g = m->pair_g1[p], k = -1 - m->pair_g2[p];
+  const int a = m->hull_body[k] - 2;
   const float4 hb4 = reinterpret_cast<const float4*>(m->hull_center)[k];
-  const float* RH = sh.ser.xm[a];
   const float hb[3] = {hb4.x, hb4.y, hb4.z};
-  float w[3];
-  mulmv3(w, RH, hb);
+  float w[3], c1[3], r1;
+  mulmv3(w, sh.ser.xm[a], hb);
+  if (g == SO100_CUBE_GEOM) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) c1[t] = sh.cube_pos[t];
+    r1 = m->geom_rbound[g];
+  } else if (g >= 0) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) c1[t] = m->geom_pos[g][t];
+    r1 = m->geom_rbound[g];
+  } else {
+    const int k1 = -1 - g, a1 = m->hull_body[k1] - 2;
+    const float4 b4 = reinterpret_cast<const float4*>(m->hull_center)[k1];
+    const float bl[3] = {b4.x, b4.y, b4.z};
+    float t1[3];
+    mulmv3(t1, sh.ser.xm[a1], bl);
+#pragma unroll
+    for (int t = 0; t < 3; t++) c1[t] = t1[t] + sh.ser.xp[a1][t];
+    r1 = reinterpret_cast<const float4*>(m->hull_half)[k1].w;
+  }
   float T[3];
 #pragma unroll
-  for (int t = 0; t < 3; t++) T[t] = (j == 0 ? sh.cube_pos[t] : m->geom_pos[g][t]) - (w[t] + sh.ser.xp[a][t]);
-  const float rs = reinterpret_cast<const float4*>(m->hull_half)[k].w + m->geom_rbound[g];
+  for (int t = 0; t < 3; t++) T[t] = c1[t] - (w[t] + sh.ser.xp[a][t]);
+  const float rs = reinterpret_cast<const float4*>(m->hull_half)[k].w + r1;
   return dot3(T, T) <= rs * rs;
 }
 // stage 2: OBB-OBB separating axes in H (hull k's box vs the box)
@@ -1329,17 +1395,17 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
   const float4 hh4 = reinterpret_cast<const float4*>(m->hull_half)[k];
   const float hb[3] = {hb4.x, hb4.y, hb4.z}, hh[3] = {hh4.x, hh4.y, hh4.z};
   float T[3];
-  sub3(T, o.c, hb);
+  sub3(T, o.bc, hb);
   float A[9];
 #pragma unroll
   for (int i = 0; i < 9; i++) A[i] = fabsf(o.ax[i]) + 1e-5f;
 #pragma unroll
   for (int i = 0; i < 3; i++)
-    if (fabsf(T[i]) > hh[i] + o.h[0] * A[3 * i] + o.h[1] * A[3 * i + 1] + o.h[2] * A[3 * i + 2]) return false;
+    if (fabsf(T[i]) > hh[i] + o.bh[0] * A[3 * i] + o.bh[1] * A[3 * i + 1] + o.bh[2] * A[3 * i + 2]) return false;
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     const float s = T[0] * o.ax[j] + T[1] * o.ax[3 + j] + T[2] * o.ax[6 + j];
-    if (fabsf(s) > hh[0] * A[j] + hh[1] * A[3 + j] + hh[2] * A[6 + j] + o.h[j]) return false;
+    if (fabsf(s) > hh[0] * A[j] + hh[1] * A[3 + j] + hh[2] * A[6 + j] + o.bh[j]) return false;
   }
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -1348,7 +1414,7 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
     for (int j = 0; j < 3; j++) {
       const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
       const float ra = hh[i1] * A[3 * i2 + j] + hh[i2] * A[3 * i1 + j];
-      const float rb = o.h[j1] * A[3 * i + j2] + o.h[j2] * A[3 * i + j1];
+      const float rb = o.bh[j1] * A[3 * i + j2] + o.bh[j2] * A[3 * i + j1];
       const float s = T[i2] * o.ax[3 * i1 + j] - T[i1] * o.ax[3 * i2 + j];
       if (fabsf(s) > ra + rb) return false;
     }
@@ -1365,31 +1431,35 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
 #ifdef SO100_EXPERIMENT_NO_MPR
   return 0;   // timing experiment only: box-hull contacts off
 #endif
-  uint64_t env_cand = 0, wave_cand = 0;
+  constexpr int kRounds = (SO100_NPAIR_CONVEX + kLanes - 1) / kLanes;   // 5
+  static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
+  uint64_t env_cand[2] = {0ull, 0ull}, wave_cand[2] = {0ull, 0ull};
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
+  for (int r = 0; r < kRounds; r++) {
     const int q = lane + kLanes * r;
     bool cand = false;
-    if (valid && q < SO100_NPAIR_MPR && mpr_sphere(m, sh, q / SO100_NHULL, q % SO100_NHULL)) {
+    if (valid && q < SO100_NPAIR_CONVEX && mpr_sphere(m, sh, SO100_PAIR_MPR0 + q)) {
       MprObj o;
-      mpr_obj_setup(m, sh, q / SO100_NHULL, q % SO100_NHULL, o);
-      cand = mpr_broadphase(m, o, q % SO100_NHULL);
+      mpr_obj_setup(m, sh, SO100_PAIR_MPR0 + q, o);
+      cand = mpr_broadphase(m, o, -1 - m->pair_g2[SO100_PAIR_MPR0 + q]);
     }
     const uint64_t b = __ballot(cand);
-    env_cand |= ((b >> (grp * 16)) & 0xFFFFull) << (16 * r);
-    wave_cand |= ((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFull) << (16 * r);
+    env_cand[r / 4] |= ((b >> (grp * 16)) & 0xFFFFull) << (16 * (r % 4));
+    wave_cand[r / 4] |= ((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFull) << (16 * (r % 4));
   }
   int ns = 0;
 #ifdef SO100_EXPERIMENT_MPR_BROAD_ONLY
-  wave_cand = 0;   // timing experiment only: broadphase without the narrowphase
+  wave_cand[0] = wave_cand[1] = 0;   // timing experiment only: broadphase without the narrowphase
 #endif
-  while (wave_cand) {
-    const int q = __builtin_ctzll(wave_cand);
-    wave_cand &= wave_cand - 1ull;
-    if ((env_cand >> q) & 1ull) {
-      const int j = q / SO100_NHULL, k = q % SO100_NHULL;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+   while (wave_cand[h]) {
+    const int q = 64 * h + __builtin_ctzll(wave_cand[h]);
+    wave_cand[h] &= wave_cand[h] - 1ull;
+    if ((env_cand[h] >> (q - 64 * h)) & 1ull) {
+      const int p = SO100_PAIR_MPR0 + q, k = -1 - m->pair_g2[p];
       MprObj o;
-      mpr_obj_setup(m, sh, j, k, o);
+      mpr_obj_setup(m, sh, p, o);
       float depth, dir[3], pos[3];
       if (mpr_penetration(m, o, depth, dir, pos, lane)) {
         if (ns < kMaxCon && lane == 0) {
@@ -1401,11 +1471,12 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
           st.pos[0] = wp[0] + sh.ser.xp[a][0]; st.pos[1] = wp[1] + sh.ser.xp[a][1];
           st.pos[2] = wp[2] + sh.ser.xp[a][2]; st.pos[3] = -depth;
           st.nrm[0] = wn[0]; st.nrm[1] = wn[1]; st.nrm[2] = wn[2];
-          st.nrm[3] = __int_as_float(SO100_PAIR_MPR0 + q);
+          st.nrm[3] = __int_as_float(p);
         }
         ns++;
       }
     }
+   }
   }
   return ns < kMaxCon ? ns : kMaxCon;
 }

@@ -18,7 +18,9 @@ ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so10
 NBODY, NHINGE, NQ, NV, NU, NGEOM = 9, 6, 13, 12, 6, 15
 NPAIR_BOX, NHULL, HULL_NVERT, NBINBOX = 14, 9, 2560, 5
 PAIR_MPR0 = NPAIR_BOX + NHULL                  # (box, hull) pairs of the MPR convex collider start here
-NPAIR = PAIR_MPR0 + (1 + NBINBOX) * NHULL      # 77
+PAIR_SELF0 = PAIR_MPR0 + (1 + NBINBOX) * NHULL  # 77: hull-hull self-collision pairs
+NPAIR_SELF = 21
+NPAIR = PAIR_SELF0 + NPAIR_SELF                  # 98
 NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
 MAXCON, CONDIM, NOBS = 16, 4, 15
 NEFC_MAX = NV + NHINGE + MAXCON * CONDIM

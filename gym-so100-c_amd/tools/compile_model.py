@@ -15,6 +15,7 @@ reference.  It restates what MuJoCo's compiler does for the parts of
   bin walls/floor (transfer_cube.xml:18-22), table = 8-vertex box hull of tabletop.stl
   (scene_so100.xml:3,20) emitted as an exact box
 * arm/jaw collision hulls: qhull convex hulls (scipy) of the class="collision" meshes on the moving arm
+  bodies; hull-hull self-collision pairs of non-adjacent links (MuJoCo's parent-child filter);
   bodies (so_arm100.xml:79,87,95,103,111-112,136-138), vertices in the body frame, mesh volume
   centroid (the mesh geom's frame origin), for the hull-vs-table contacts and the box-vs-hull pairs of
   the convex collider (cube and bin boxes vs every hull); pair parameters mixed like
@@ -414,6 +415,18 @@ def compile_model():
         for k, h in enumerate(hulls):
             pairs.append(dict(g1=gid[n1], g2=-1 - k, body1=g1["body"], body2=h["body"], name1=n1,
                               name2=h["name"], hull=k, **mixed(g1, h)))
+    # Pairs 77..97: hull-hull self-collision of the arm, through the same collider.  MuJoCo filters only
+    # parent-child body pairs and the explicit exclude (Base / Rotation_Pitch, so_arm100.xml:165-167);
+    # geom1 = the hull on the body nearer the root, normal from it to the other.
+    parent = {bid[n]: bid[bodies[n]["parent"]] if bodies[n]["parent"] in bid else 0 for n in ARM_BODIES}
+    excl = {frozenset((bid[a], bid[b])) for a, b in excludes}
+    for k1, h1 in enumerate(hulls):
+        for k2, h2 in enumerate(hulls):
+            b1, b2 = h1["body"], h2["body"]
+            if not b1 < b2 or parent[b2] == b1 or frozenset((b1, b2)) in excl:
+                continue
+            pairs.append(dict(g1=-1 - k1, g2=-1 - k2, body1=b1, body2=b2, name1=h1["name"], name2=h2["name"],
+                              hull=k2, hull1=k1, **mixed(h1, h2)))
 
     # ---- sites ----
     cube_site = vec(bodies["box"]["sites"][0]["pos"], 3)

@@ -16,6 +16,7 @@
  *          14..22 (table, hull k): arm/jaw collision hulls vs the table top
  *          23..31 (red_box, hull k) | 32..76 (bin box j, hull k) at 32 + 9 j + k, j = bin_wall,
  *          bin_wall2..4, bin_floor: box vs convex hull through the MPR convex collider
+ *          77..97 (hull k1, hull k2): self-collision of hulls on non-adjacent arm links (MPR)
  *   hulls  0 Rotation_Pitch | 1 Upper_Arm | 2 Lower_Arm | 3 Wrist_Pitch_Roll |
  *          4..5 Fixed_Jaw_Collision_1..2 | 6..8 Moving_Jaw_Collision_1..3
  */
@@ -33,7 +34,10 @@
 #define SO100_NBINBOX 5             /* bin walls + floor (geoms 10..14) */
 #define SO100_PAIR_MPR0 (SO100_NPAIR_BOX + SO100_NHULL)     /* 23: first (box, hull) MPR pair */
 #define SO100_NPAIR_MPR ((1 + SO100_NBINBOX) * SO100_NHULL) /* 54: (cube | bin box j, hull k) */
-#define SO100_NPAIR (SO100_PAIR_MPR0 + SO100_NPAIR_MPR)    /* 77 */
+#define SO100_PAIR_SELF0 (SO100_PAIR_MPR0 + SO100_NPAIR_MPR)  /* 77: first hull-hull self-collision pair */
+#define SO100_NPAIR_SELF 21                                 /* hulls on non-adjacent arm links */
+#define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF)  /* 75 pairs through the MPR collider */
+#define SO100_NPAIR (SO100_PAIR_SELF0 + SO100_NPAIR_SELF)   /* 98 */
 #define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_CUBE_BODY 8
@@ -99,7 +103,8 @@ typedef struct so100_model {
   double geom_quat[SO100_NGEOM][4];
   double geom_size[SO100_NGEOM][3];
 
-  /* contact pairs with mixed parameters (geom2 of a hull pair: -1 - hull index) */
+  /* contact pairs with mixed parameters (a hull geom is -1 - hull index: geom2 of the hull pairs, both
+   * geoms of the self-collision pairs) */
   int    pair_geom1[SO100_NPAIR];
   int    pair_geom2[SO100_NPAIR];
   int    pair_body1[SO100_NPAIR];

@@ -641,8 +641,14 @@ static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
 #define CCD_EPS ((real)2.220446049250313e-16)
 typedef struct { real v[3], v1[3], v2[3]; } mpr_sup;
 typedef struct {
-  real c[3], ax[9], h[3];        /* box centre, axes (columns of ax), half sizes, all in H */
-  const double (*vert)[3];       /* hull vertices (H) */
+  int hull1;                     /* obj1: -1 = a box, else a hull (self-collision pairs) */
+  real c[3], ax[9], h[3];        /* obj1 frame in H: origin (box centre / hull body origin), axes (columns
+                                    of ax); box half sizes */
+  const double (*vert1)[3];      /* obj1 hull vertices (its body frame) */
+  int nvert1;
+  real c1[3];                    /* obj1 centre in H: box centre / hull centroid */
+  real bc[3], bh[3];             /* obj1 bounding box in H (axes ax): centre, half extents */
+  const double (*vert)[3];       /* obj2 = hull vertices (H) */
   int nvert;
   real hc[3];                    /* hull centroid (H) */
 } mpr_obj;
@@ -661,10 +667,26 @@ static void normalize3(real v[3]) {
 }
 static void mpr_support(const mpr_obj* o, const real d[3], mpr_sup* s) {
   for (int t = 0; t < 3; t++) s->v1[t] = o->c[t];
-  for (int i = 0; i < 3; i++) {
-    real l = o->ax[i] * d[0] + o->ax[3 + i] * d[1] + o->ax[6 + i] * d[2];
-    real sz = l >= 0 ? o->h[i] : -o->h[i];
-    for (int t = 0; t < 3; t++) s->v1[t] += sz * o->ax[3 * t + i];
+  if (o->hull1 < 0) {
+    for (int i = 0; i < 3; i++) {
+      real l = o->ax[i] * d[0] + o->ax[3 + i] * d[1] + o->ax[6 + i] * d[2];
+      real sz = l >= 0 ? o->h[i] : -o->h[i];
+      for (int t = 0; t < 3; t++) s->v1[t] += sz * o->ax[3 * t + i];
+    }
+  } else {                       /* obj1 hull: the first vertex maximising (ax' d) . v, back into H */
+    real dl[3], best1 = 0, v1[3];
+    mulmtv3(dl, o->ax, d);
+    int b1 = -1;
+    for (int v = 0; v < o->nvert1; v++) {
+      real hv[3];
+      load3(hv, o->vert1[v]);
+      real sc = dot3(dl, hv);
+      if (b1 < 0 || sc > best1) { best1 = sc; b1 = v; }
+    }
+    real hv[3];
+    load3(hv, o->vert1[b1]);
+    mulmv3(v1, o->ax, hv);
+    for (int t = 0; t < 3; t++) s->v1[t] += v1[t];
   }
   real nd[3] = {-d[0], -d[1], -d[2]}, best = 0;
   int bi = -1;
@@ -702,7 +724,7 @@ static void portal_expand(mpr_sup P[4], const mpr_sup* v4) {
 }
 /* -1: no intersection, 0: portal, 1: touching on v1, 2: origin on the segment v0-v1 */
 static int mpr_discover(const mpr_obj* o, mpr_sup P[4]) {
-  for (int t = 0; t < 3; t++) { P[0].v1[t] = o->c[t]; P[0].v2[t] = o->hc[t]; }
+  for (int t = 0; t < 3; t++) { P[0].v1[t] = o->c1[t]; P[0].v2[t] = o->hc[t]; }
   sub3(P[0].v, P[0].v1, P[0].v2);
   if (ccd_zero(P[0].v[0]) && ccd_zero(P[0].v[1]) && ccd_zero(P[0].v[2])) P[0].v[0] += CCD_EPS * 10;
   real dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]}, va[3], vb[3];
@@ -847,24 +869,24 @@ static int mpr_penetration(const mpr_obj* o, real* depth, real dir[3], real pos[
  * (the hull's H-aligned bounding box vs the box; |R| padded by 1e-5) */
 static int mpr_broadphase(const mpr_obj* o, const real hb[3], const real hh[3]) {
   real T[3];
-  sub3(T, o->c, hb);
-  real rs = (real)sqrt((double)dot3(hh, hh)) + (real)sqrt((double)dot3(o->h, o->h));
+  sub3(T, o->bc, hb);
+  real rs = (real)sqrt((double)dot3(hh, hh)) + (real)sqrt((double)dot3(o->bh, o->bh));
   if (dot3(T, T) > rs * rs) return 0;
   real R[3][3], A[3][3];
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) { R[i][j] = o->ax[3 * i + j]; A[i][j] = (real)fabs((double)R[i][j]) + (real)1e-5; }
   for (int i = 0; i < 3; i++)
-    if ((real)fabs((double)T[i]) > hh[i] + o->h[0] * A[i][0] + o->h[1] * A[i][1] + o->h[2] * A[i][2]) return 0;
+    if ((real)fabs((double)T[i]) > hh[i] + o->bh[0] * A[i][0] + o->bh[1] * A[i][1] + o->bh[2] * A[i][2]) return 0;
   for (int j = 0; j < 3; j++) {
     real s = T[0] * R[0][j] + T[1] * R[1][j] + T[2] * R[2][j];
-    if ((real)fabs((double)s) > hh[0] * A[0][j] + hh[1] * A[1][j] + hh[2] * A[2][j] + o->h[j]) return 0;
+    if ((real)fabs((double)s) > hh[0] * A[0][j] + hh[1] * A[1][j] + hh[2] * A[2][j] + o->bh[j]) return 0;
   }
   for (int i = 0; i < 3; i++) {
     const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
     for (int j = 0; j < 3; j++) {
       const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
       real ra = hh[i1] * A[i2][j] + hh[i2] * A[i1][j];
-      real rb = o->h[j1] * A[i][j2] + o->h[j2] * A[i][j1];
+      real rb = o->bh[j1] * A[i][j2] + o->bh[j2] * A[i][j1];
       real s = T[i2] * R[i1][j] - T[i1] * R[i2][j];
       if ((real)fabs((double)s) > ra + rb) return 0;
     }
@@ -920,18 +942,38 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = best - top;
     add_contact(d, &con, p);
   }
-  /* pairs 23..76: (cube | bin box, hull k) through the MPR convex collider, in H = hull k's body frame */
+  /* pairs 23..97 through the MPR convex collider, in H = the body frame of hull k (geom2):
+   *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links */
   for (int p = SO100_PAIR_MPR0; p < SO100_NPAIR; p++) {
-    const int k = (p - SO100_PAIR_MPR0) % SO100_NHULL, g = m->pair_geom1[p], b = m->hull_body[k];
+    const int k = -1 - m->pair_geom2[p], g = m->pair_geom1[p], b = m->hull_body[k];
     const real* RH = d->xmat[b];
     mpr_obj o;
+    memset(&o, 0, sizeof(o));
     real dp[3], hb[3], hh[3];
-    sub3(dp, d->geom_xpos[g], d->xpos[b]);
+    const real* Rb = g >= 0 ? d->geom_xmat[g] : d->xmat[m->hull_body[-1 - g]];
+    sub3(dp, g >= 0 ? d->geom_xpos[g] : d->xpos[m->hull_body[-1 - g]], d->xpos[b]);
     mulmtv3(o.c, RH, dp);
     for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++)
-        o.ax[3 * i + j] = RH[i] * d->geom_xmat[g][j] + RH[3 + i] * d->geom_xmat[g][3 + j] + RH[6 + i] * d->geom_xmat[g][6 + j];
-    load3(o.h, m->geom_size[g]);
+      for (int j = 0; j < 3; j++) o.ax[3 * i + j] = RH[i] * Rb[j] + RH[3 + i] * Rb[3 + j] + RH[6 + i] * Rb[6 + j];
+    o.hull1 = g >= 0 ? -1 : -1 - g;
+    if (g >= 0) {
+      load3(o.h, m->geom_size[g]);
+      memcpy(o.c1, o.c, sizeof(o.c1));
+      memcpy(o.bc, o.c, sizeof(o.bc));
+      memcpy(o.bh, o.h, sizeof(o.bh));
+    } else {
+      const int k1 = o.hull1;
+      real t[3], l[3];
+      o.vert1 = (const double (*)[3])m->hull_vert[m->hull_start[k1]];
+      o.nvert1 = m->hull_count[k1];
+      load3(l, m->hull_centroid[k1]);
+      mulmv3(t, o.ax, l);
+      for (int q = 0; q < 3; q++) o.c1[q] = t[q] + o.c[q];
+      load3(l, m->hull_center[k1]);
+      mulmv3(t, o.ax, l);
+      for (int q = 0; q < 3; q++) o.bc[q] = t[q] + o.c[q];
+      load3(o.bh, m->hull_half[k1]);
+    }
     o.vert = (const double (*)[3])m->hull_vert[m->hull_start[k]];
     o.nvert = m->hull_count[k];
     load3(o.hc, m->hull_centroid[k]);

@@ -432,7 +432,7 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
     rng = np.random.default_rng(21)
     d = oracle64.new_data()
     states, kinds = [], set()
-    for e in range(64):
+    for e in range(128):
         oracle64.reset(model, d, oracle64.spawn_pose(2000 + e))
         for _ in range(200):
             oracle64.env_step(model, d, 0, rng.uniform(-1, 1, 6).astype(np.float32))
@@ -443,10 +443,10 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
                 states.append((q, v, w))
                 kinds.update(p < PAIR_MPR0 + NHULL for p in mp)
                 break
-        if len(states) >= 32:
+        if len(states) >= 48:
             break
     n = len(states)
-    assert n >= 16 and kinds == {True, False}, (n, kinds)     # both cube-hull and bin-hull contacts
+    assert n >= 24 and kinds == {True, False}, (n, kinds)     # both cube-hull and bin-hull contacts
     env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
     env.reset(seed=3)
     env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
@@ -478,8 +478,11 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
           f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
           f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
     assert (mpr_con[:n] > 0).mean() > 0.3              # the GPU collider sees the contacts too
+    # MPR's fp32 branches (different portals) make the tail chaotic for ANY fp32 implementation: the
+    # fp32 oracle and the GPU put their large deviations on different states, so the tail is compared by
+    # its mass (share of env steps off by > 1e-4), not by a quantile of a 150-sample set
     assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
-    assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
+    assert np.mean(qv_err > 1e-4) <= 1.5 * np.mean(qv_floor > 1e-4) + 0.05
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     env.close()
 
@@ -584,3 +587,63 @@ def test_domain_randomization_config4_shard(solver):
     assert torch.isfinite(full.qpos).all()
     full.close()
     shard.close()
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_self_collision_parity(solver, oracle64, oracle32):
+    """Hull-hull self-collision (pairs 77..97): random arm configurations whose
+    non-adjacent links overlap, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import PAIR_SELF0, build_model
+    model = build_model(solver=solver)
+    rng = np.random.default_rng(17)
+    lo_j = np.array([r[0] for r in model.jnt_range]); hi_j = np.array([r[1] for r in model.jnt_range])
+    lo, hi = np.array(model.action_lo[:]), np.array(model.action_hi[:])
+    d = oracle64.new_data()
+    states, targets = [], []
+    while len(states) < 24:
+        arm = rng.uniform(lo_j, hi_j)
+        oracle64.reset(model, d, np.array([0.4, 0.95, 0.6, 1, 0, 0, 0]))
+        for k in range(6):
+            d.qpos[k] = arm[k]
+        oracle64.call("so100o_fwd_position", model, d)
+        if any(d.con[i].pair >= PAIR_SELF0 for i in range(d.ncon)) and not d.ncon_dropped:
+            q, v, w, _ = oracle64.get_state(d)
+            states.append((q, v * 0, w * 0))
+            targets.append(np.clip((arm - lo) / (hi - lo) * 2 - 1, -1, 1))
+    n = len(states)
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
+    env.reset(seed=3)
+    env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
+                  np.array([s[2] for s in states], np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, self_con = [], [], []
+    for step in range(3):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = (np.array(targets) + rng.normal(0, 0.02, (n, 6))).astype(np.float32)
+        env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        dbg = env.debug.cpu().numpy()
+        for i in range(n):
+            pairs = dbg[i, 48:48 + int(dbg[i, 0])]
+            self_con.append(int((pairs >= PAIR_SELF0).sum()))
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(model, d64, 0, act[i])
+            oracle32.env_step(model, d32, 0, act[i])
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+    qv_err, qv_floor, self_con = np.array(qv_err), np.array(qv_floor), np.array(self_con)
+    print(f"\n[{solver}] self-collision: GPU self contacts per env mean {self_con.mean():.2f} (envs with any: "
+          f"{(self_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
+          f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
+          f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
+    assert (self_con[:n] > 0).mean() > 0.5
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.mean(qv_err > 1e-4) <= 1.5 * np.mean(qv_floor > 1e-4) + 0.05    # tail mass (MPR: see above)
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    env.close()

@@ -209,3 +209,60 @@ def test_mpr_contact_rows(model, oracle64):
                 assert d.efc_force[i] >= 0.0
                 kinds[cube] = kinds.get(cube, 0) + 1
     assert kinds.get(True, 0) > 0 and kinds.get(False, 0) > 0, kinds
+
+
+def _self_configs(model, o, n, seed):
+    from gym_so100.model import PAIR_SELF0
+    rng = np.random.default_rng(seed)
+    lo = np.array([r[0] for r in model.jnt_range]); hi = np.array([r[1] for r in model.jnt_range])
+    hit, miss = [], []
+    while len(hit) < n or len(miss) < n:
+        arm = rng.uniform(lo, hi)
+        d = _state(o, model, arm, (0.4, 0.95, 0.6, 1, 0, 0, 0))
+        pairs = [d.con[i].pair for i in range(d.ncon) if d.con[i].pair >= PAIR_SELF0]
+        (hit if pairs else miss).append(arm)
+    return hit[:n], miss[:n]
+
+
+def test_self_collision_contacts_are_real_overlaps(model, oracle64):
+    """Hull-hull self-collision (pairs 77..97): every MPR contact is between two polytopes that really
+    intersect (an LP finds a common interior point of their H-representations), with the overlap along the
+    normal at least the reported depth; arms whose hulls an LP proves disjoint get no such contact."""
+    from scipy.optimize import linprog
+    from gym_so100.model import PAIR_SELF0, NPAIR
+    hit, miss = _self_configs(model, oracle64, 30, seed=8)
+
+    def world(d, k):
+        b = model.hull_body[k]
+        R, p = np.array(d.xmat[b][:]).reshape(3, 3), np.array(d.xpos[b][:])
+        return _hull(model, k) @ R.T + p
+
+    def depth_lp(V1, V2):
+        """max t such that a point lies t inside both hulls (t < 0: separated)."""
+        H1, H2 = ConvexHull(V1).equations, ConvexHull(V2).equations
+        A = np.vstack([H1[:, :3], H2[:, :3]])
+        b = -np.concatenate([H1[:, 3], H2[:, 3]])
+        res = linprog(c=[0, 0, 0, -1], A_ub=np.hstack([A, np.ones((len(A), 1))]), b_ub=b,
+                      bounds=[(None, None)] * 3 + [(None, 1.0)], method="highs")
+        return -res.fun
+    checked = 0
+    for arm in hit:
+        d = _state(oracle64, model, arm, (0.4, 0.95, 0.6, 1, 0, 0, 0))
+        for i in range(d.ncon):
+            p = d.con[i].pair
+            if p < PAIR_SELF0:
+                continue
+            k1, k2 = -1 - model.pair_geom1[p], -1 - model.pair_geom2[p]
+            V1, V2 = world(d, k1), world(d, k2)
+            assert depth_lp(V1, V2) > -1e-9, (p, depth_lp(V1, V2))
+            n = np.array(d.con[i].frame[:3])
+            assert (V1 @ n).max() - (V2 @ n).min() >= -d.con[i].dist - 1e-9
+            checked += 1
+    assert checked >= 30
+    for arm in miss:
+        d = _state(oracle64, model, arm, (0.4, 0.95, 0.6, 1, 0, 0, 0))
+        for p in range(PAIR_SELF0, NPAIR):
+            k1, k2 = -1 - model.pair_geom1[p], -1 - model.pair_geom2[p]
+            if model.hull_body[k1] == model.hull_body[k2]:
+                continue
+            assert depth_lp(world(d, k1), world(d, k2)) < 1e-6, p
