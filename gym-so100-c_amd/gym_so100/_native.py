@@ -32,7 +32,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 3          # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 4          # include/so100.h SO100_ABI_VERSION
 
 
 def load():
