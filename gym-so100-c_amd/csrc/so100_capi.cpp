@@ -19,6 +19,8 @@ namespace so100 {
 hipError_t launch_step(const DevModel*, int, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
                        hipStream_t, hipEvent_t*);
 hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
+hipError_t launch_render(const DevModel*, const float4*, const int*, const uint32_t*, int, const float*,
+                         const uint8_t*, const so100_camera&, int, int, int, uint8_t*, hipStream_t);
 hipError_t alloc_workspace(int, Workspace*);
 hipError_t free_workspace(Workspace*);
 hipError_t launch_reset(const DevModel*, const so100_buffers&, int, int, uint64_t, int, const uint8_t*, const uint32_t*,
@@ -54,6 +56,11 @@ struct so100_env {
   int max_steps;
   uint64_t base_seed;
   int env_offset;
+  // camera render mesh (so100_render_mesh)
+  float4* r_tri = nullptr;
+  int* r_body = nullptr;
+  uint32_t* r_rgb = nullptr;
+  int r_ntri = 0;
   // profiling (so100_profile_enable): events[step][2 nsubstep + 2]
   std::vector<hipEvent_t> prof_ev;
   int prof_cap = 0, prof_used = 0;
@@ -420,6 +427,9 @@ int so100_destroy(so100_env* env) {
   if (!env) return 0;
   DeviceGuard g(env->device);
   profile_free(env);
+  if (env->r_tri) (void)hipFree(env->r_tri);
+  if (env->r_body) (void)hipFree(env->r_body);
+  if (env->r_rgb) (void)hipFree(env->r_rgb);
   hipError_t e = hipFree(env->d_model);
   hipError_t e2 = free_chunks(env);
   if (e == hipSuccess) e = e2;
@@ -579,6 +589,54 @@ int so100_unnormalize(so100_env* env, int n, const float* action, float* ctrl, v
   DeviceGuard g(env->device);
   hipError_t e = so100::launch_unnormalize(env->d_model, n, action, ctrl, (hipStream_t)stream);
   return e == hipSuccess ? 0 : fail_hip("so100_unnormalize", e);
+}
+
+
+int so100_render_mesh(so100_env* env, const float* tri, const int* body, const float* rgb, int ntri) {
+  if (!env || !tri || !body || !rgb || ntri <= 0) return fail("so100_render_mesh: bad arguments");
+  std::vector<float4> t((size_t)ntri * 3);
+  std::vector<uint32_t> c((size_t)ntri);
+  for (int i = 0; i < ntri; i++) {
+    if (body[i] < 0 || body[i] >= SO100_NBODY) return fail("so100_render_mesh: body out of range");
+    for (int v = 0; v < 3; v++) {
+      const float* p = tri + (size_t)9 * i + 3 * v;
+      t[(size_t)3 * i + v] = make_float4(p[0], p[1], p[2], 0.f);
+    }
+    uint32_t col = 0;
+    for (int k = 0; k < 3; k++) {
+      const float x = rgb[(size_t)3 * i + k] < 0.f ? 0.f : (rgb[(size_t)3 * i + k] > 1.f ? 1.f : rgb[(size_t)3 * i + k]);
+      col |= (uint32_t)(x * 255.f + 0.5f) << (8 * k);
+    }
+    c[i] = col;
+  }
+  DeviceGuard g(env->device);
+  if (env->r_tri) (void)hipFree(env->r_tri);
+  if (env->r_body) (void)hipFree(env->r_body);
+  if (env->r_rgb) (void)hipFree(env->r_rgb);
+  env->r_tri = nullptr; env->r_body = nullptr; env->r_rgb = nullptr; env->r_ntri = 0;
+  hipError_t e = hipMalloc(&env->r_tri, t.size() * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&env->r_body, (size_t)ntri * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&env->r_rgb, (size_t)ntri * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(env->r_tri, t.data(), t.size() * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(env->r_body, body, (size_t)ntri * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(env->r_rgb, c.data(), (size_t)ntri * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail_hip("so100_render_mesh", e);
+  env->r_ntri = ntri;
+  return 0;
+}
+
+int so100_render(so100_env* env, const float* qpos, const uint8_t* mask, const so100_camera* cam, int width,
+                 int height, uint8_t* out, void* stream) {
+  if (!env || !qpos || !cam || !out) return fail("so100_render: bad arguments");
+  if (env->r_ntri <= 0) return fail("so100_render: no render mesh (so100_render_mesh)");
+  if (width <= 0 || height <= 0 || width > 4096 || (long)width * height > (1L << 22))
+    return fail("so100_render: bad image size (width <= 4096, width*height <= 2^22)");
+  if (cam->nlight < 0 || cam->nlight > SO100_MAX_LIGHTS || !(cam->fovy > 0.f && cam->fovy < 180.f))
+    return fail("so100_render: bad camera");
+  DeviceGuard g(env->device);
+  hipError_t e = so100::launch_render(env->d_model, env->r_tri, env->r_body, env->r_rgb, env->r_ntri, qpos, mask, *cam,
+                                      env->n, width, height, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail_hip("so100_render", e);
 }
 
 }  // extern "C"

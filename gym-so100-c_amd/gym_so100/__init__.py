@@ -18,6 +18,6 @@ try:  # gymnasium is an optional dependency here (absent in this image)
 
     for _id, _kw in ENV_IDS.items():
         _register(id=_id, entry_point="gym_so100.env:SO100Env", max_episode_steps=_kw["max_episode_steps"],
-                  nondeterministic=True, kwargs={"obs_type": "so100_state", "task": _kw["task"]})
+                  nondeterministic=True, kwargs={"obs_type": "so100_pixels_agent_pos", "task": _kw["task"]})
 except ImportError:
     pass

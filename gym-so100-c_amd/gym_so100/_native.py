@@ -25,6 +25,17 @@ class SO100Buffers(ctypes.Structure):
         "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug")]
 
 
+SO100_MAX_LIGHTS = 4
+
+
+class SO100Camera(ctypes.Structure):
+    """Mirror of ``so100_camera`` (include/so100.h): pose, fovy, headlight and directional lights."""
+    _fields_ = [("pos", ctypes.c_float * 3), ("mat", ctypes.c_float * 9), ("fovy", ctypes.c_float),
+                ("znear", ctypes.c_float), ("head_ambient", ctypes.c_float), ("head_diffuse", ctypes.c_float),
+                ("nlight", ctypes.c_int), ("light_dir", (ctypes.c_float * 3) * SO100_MAX_LIGHTS),
+                ("light_diffuse", ctypes.c_float * SO100_MAX_LIGHTS)]
+
+
 class NativeLibraryError(RuntimeError):
     pass
 
@@ -62,9 +73,12 @@ def load():
     lib.so100_profile_read.argtypes = [_P, _P, _P, _P, _P]
     lib.so100_contact_count.argtypes = [_P, _P, _P]
     lib.so100_chunk_info.argtypes = [_P, _P, _P]
+    lib.so100_render_mesh.argtypes = [_P, _P, _P, _P, ctypes.c_int]
+    lib.so100_render.argtypes = [_P, _P, _P, ctypes.POINTER(SO100Camera), ctypes.c_int, ctypes.c_int, _P, _P]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
-               "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info"):
+               "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info",
+               "so100_render_mesh", "so100_render"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
     lib.so100_struct_sizes.restype = ctypes.c_int
@@ -83,7 +97,7 @@ def load():
 EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
-                    "so100_contact_count", "so100_chunk_info")
+                    "so100_contact_count", "so100_chunk_info", "so100_render_mesh", "so100_render")
 
 
 def check(rc, what):

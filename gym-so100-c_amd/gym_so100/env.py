@@ -4,14 +4,17 @@
 ``SO100VecEnv`` on the GPU: numpy in, numpy out, like the reference.  For throughput use
 ``SO100VecEnv`` directly (thousands of envs per launch).
 
-Deviation: camera renders are out of scope, so ``obs_type`` must be "so100_state" and
-GoalEnv's "observation" is the 15-float state vector instead of flattened pixels + qpos.
+Observations: ``obs_type="so100_pixels_agent_pos"`` (the registered envs' and GoalEnv's form: the
+``top`` camera drawn by the GPU rasteriser, render.py) or ``"so100_state"``.  ``render()`` draws the
+same camera at the visualization size.  The images are the scene's geometry and colours, not MuJoCo's
+OpenGL pixels.
 """
 import numpy as np
 
 from . import spaces
 from .constants import SO100_ACTIONS, SO100_JOINTS, GOAL_DISTANCE_THRESHOLD, bin_max, bin_min
 from .vec_env import SO100VecEnv
+from .render import CameraRenderer
 
 try:
     import gymnasium as _gym
@@ -38,15 +41,28 @@ class SO100Env(_Base):
         self.visualization_width, self.visualization_height = visualization_width, visualization_height
         # TimeLimit is applied by the gymnasium registry wrapper (as in the reference); 0 = none here
         self._venv = SO100VecEnv(1, task=task, obs_type=obs_type, device=device, autoreset=False,
-                                 max_episode_steps=max_episode_steps, solver=solver)
-        self.observation_space = spaces.Box(low=-100.0, high=100.0, shape=(len(SO100_JOINTS) + 3 * 3,),
-                                            dtype=np.float32)           # env.py:67-73
+                                 max_episode_steps=max_episode_steps, solver=solver,
+                                 observation_width=observation_width, observation_height=observation_height)
+        self._vis = None
+        if obs_type == "so100_pixels_agent_pos":                          # env.py:50-66
+            self.observation_space = spaces.Dict({
+                "pixels": spaces.Box(low=0, high=255, shape=(observation_height, observation_width, 3),
+                                     dtype=np.uint8),
+                "agent_pos": spaces.Box(low=-10.0, high=10.0, shape=(len(SO100_JOINTS),), dtype=np.float32)})
+        else:
+            self.observation_space = spaces.Box(low=-100.0, high=100.0, shape=(len(SO100_JOINTS) + 3 * 3,),
+                                                dtype=np.float32)       # env.py:67-73
         self.action_space = spaces.Box(low=-1, high=1, shape=(len(SO100_ACTIONS),), dtype=np.float32)
 
     def reset(self, seed=None, options=None):
         super().reset(seed=seed)
         obs, _ = self._venv.reset(seed=None if seed is None else [int(seed)])
-        return obs[0].cpu().numpy(), {"is_success": False}              # env.py:169
+        return self._np_obs(obs), {"is_success": False}                 # env.py:169
+
+    def _np_obs(self, obs):
+        if isinstance(obs, dict):
+            return {k: v[0].cpu().numpy() for k, v in obs.items()}
+        return obs[0].cpu().numpy()
 
     def step(self, action):
         action = np.asarray(action, dtype=np.float32)
@@ -54,10 +70,14 @@ class SO100Env(_Base):
         obs, reward, terminated, truncated, info = self._venv.step(action[None, :6])
         r = float(reward[0].item())
         is_success = bool(info["is_success"][0].item())
-        return obs[0].cpu().numpy(), r, bool(terminated[0].item()), False, {"is_success": is_success}
+        return self._np_obs(obs), r, bool(terminated[0].item()), False, {"is_success": is_success}
 
     def render(self):
-        raise NotImplementedError("rendering is out of scope of the GPU hot path (DESIGN.md §7)")
+        """Top camera at the visualization size (env.py:79-90), uint8 [H, W, 3]."""
+        assert self.render_mode == "rgb_array"
+        if self._vis is None:
+            self._vis = CameraRenderer(self._venv, self.visualization_width, self.visualization_height)
+        return self._vis.render()[0].cpu().numpy()
 
     def close(self):
         self._venv.close()
@@ -67,14 +87,24 @@ class SO100GoalEnv(_Base):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
 
     def __init__(self, render_mode="rgb_array", observation_width=640, observation_height=480,
-                 visualization_width=640, visualization_height=480, device="cuda:0", solver="newton"):
+                 visualization_width=640, visualization_height=480, device="cuda:0", solver="newton",
+                 obs_type="so100_pixels_agent_pos"):
+        """obs_type "so100_pixels_agent_pos" (the reference's only form): "observation" = flattened
+        pixels / 255 + agent_pos (env.py:218-224, 267-270); "so100_state": the 15-float state vector."""
         super().__init__()
         self.max_episode_steps = 300                                     # env.py:200
         self.current_step = 0
         self.render_mode = render_mode
-        self._venv = SO100VecEnv(1, task="so100_goal", device=device, autoreset=False, solver=solver)
+        self.observation_width, self.observation_height = observation_width, observation_height
+        self.visualization_width, self.visualization_height = visualization_width, visualization_height
+        self._venv = SO100VecEnv(1, task="so100_goal", device=device, autoreset=False, solver=solver,
+                                 obs_type=obs_type, observation_width=observation_width,
+                                 observation_height=observation_height)
+        self._vis = None
         self.distance_threshold = GOAL_DISTANCE_THRESHOLD                # env.py:252
-        obs_space = spaces.Box(low=-np.inf, high=np.inf, shape=(15,), dtype=np.float32)
+        size = observation_height * observation_width * 3 + len(SO100_JOINTS) \
+            if obs_type == "so100_pixels_agent_pos" else 15
+        obs_space = spaces.Box(low=-np.inf, high=np.inf, shape=(size,), dtype=np.float32)
         self.observation_space = spaces.Dict({
             "observation": obs_space,
             "achieved_goal": spaces.Box(low=-np.inf, high=np.inf, shape=(3,), dtype=np.float32),
@@ -119,7 +149,11 @@ class SO100GoalEnv(_Base):
         return out, float(reward[0].item()), bool(terminated[0].item()), trunc, inf
 
     def render(self):
-        raise NotImplementedError("rendering is out of scope of the GPU hot path (DESIGN.md §7)")
+        """Top camera at the visualization size (env.py:256-265), uint8 [H, W, 3]."""
+        assert self.render_mode == "rgb_array"
+        if self._vis is None:
+            self._vis = CameraRenderer(self._venv, self.visualization_width, self.visualization_height)
+        return self._vis.render()[0].cpu().numpy()
 
     def close(self):
         self._venv.close()

@@ -9,6 +9,8 @@
 * reward ladders of the three tasks (single_arm.py), ``terminated = is_success = reward == 4``
   (env.py:175), TimeLimit truncation at 700 / 300 steps (gym_so100/__init__.py:7,17,27);
 * so100_state observation = [box, bin, ee, qpos[:6]] float32 (env.py:137-145);
+* so100_pixels_agent_pos observation = {"pixels": top camera uint8 [N,H,W,3], "agent_pos": qpos[:6]}
+  (env.py:130-136), rendered on the device by render.CameraRenderer (csrc/so100_render.hip);
 * GoalEnv: sparse reward 0/-1 at 0.01 m, terminated = success, own 300-step truncation, lifted-goal
   curriculum for the first 5000 steps (env.py:322-353, 372-406);
 * reset(seed=s) reproduces ``RandomState(s)`` cube spawns bit-for-bit (utils.py:18-29).
@@ -16,6 +18,10 @@
 Auto-reset follows the SB3/gymnasium-vector convention: when an env finishes, ``obs`` already holds
 the first observation of the next episode and ``info["final_observation"]`` the last one of the
 finished episode (mask in ``info["_final_observation"]``).
+
+With pixel observations an env that finishes is stepped, its terminal image drawn into
+``final_pixels``, then reset by the masked reset kernel (the same spawn and episode counter as the
+in-kernel auto-reset) and drawn again: ``info["final_observation"]`` is then {"pixels", "agent_pos"}.
 
 Output tensors are persistent device buffers overwritten by the next ``step``/``reset``; clone them if
 you keep them across calls.
@@ -59,7 +65,9 @@ class SO100VecEnv:
     Args:
         num_envs: number of envs on this device.
         task: "so100_cube_to_bin" | "so100_touch_cube" | "so100_touch_cube_sparse" | "so100_goal".
-        obs_type: "so100_state" (pixel observations are out of scope).
+        obs_type: "so100_state" (15 floats) or "so100_pixels_agent_pos" (the reference's registered
+            default: top-camera image + joint positions; GoalEnv: the flattened form of env.py:267-270).
+        observation_width, observation_height: image size for pixel observations (env.py:34-35).
         device: torch device string ("cuda:0").
         seed: base seed for in-kernel (auto-)reset spawns.
         max_episode_steps: TimeLimit; default per task as registered by the reference.
@@ -77,12 +85,10 @@ class SO100VecEnv:
 
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
-                 iterations=None, debug=False, solver="newton"):
+                 iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480):
         torch = _torch()
-        if obs_type != "so100_state":
-            raise NotImplementedError(
-                f"obs_type={obs_type!r}: camera renders are out of scope of the GPU hot path "
-                "(DESIGN.md §7); use obs_type='so100_state'")
+        if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
+            raise NotImplementedError(f"obs_type={obs_type!r}: 'so100_state' or 'so100_pixels_agent_pos'")
         if task not in _native.TASKS:
             raise NotImplementedError(task)    # env.py:117-118
         self.lib = _native.load()
@@ -133,6 +139,12 @@ class SO100VecEnv:
         self._fill_buffers()
         self._seeds = torch.zeros(n, dtype=i32, device=d)
         self._mask = torch.zeros(n, dtype=torch.uint8, device=d)
+        self.pixels = self.final_pixels = self.renderer = None
+        if obs_type == "so100_pixels_agent_pos":
+            from .render import CameraRenderer
+            self.renderer = CameraRenderer(self, observation_width, observation_height)
+            self.pixels = self.renderer.pixels
+            self.final_pixels = torch.zeros_like(self.pixels) if self.autoreset else None
 
     # ------------------------------------------------------------------ plumbing
     def _fill_buffers(self):
@@ -190,6 +202,8 @@ class SO100VecEnv:
             mask_p = _native.ptr(self._mask)
         _native.check(self.lib.so100_reset(self._handle, ctypes.byref(self._buf), mask_p, seeds_p, self._stream()),
                       "so100_reset")
+        if self.renderer is not None:
+            self.renderer.render()
         info = {"is_success": torch.zeros_like(self.success)}
         return self._observation(), info
 
@@ -212,12 +226,16 @@ class SO100VecEnv:
             if a.shape != (self.num_envs, 6):
                 raise ValueError(f"actions must be [{self.num_envs}, 6], got {a.shape}")
             self.actions.copy_(torch.from_numpy(a))
-        _native.check(self.lib.so100_step(self._handle, ctypes.byref(self._buf), self._flags, self._stream()),
-                      "so100_step")
-        done = self.terminated | self.truncated
+        if self.renderer is None:
+            _native.check(self.lib.so100_step(self._handle, ctypes.byref(self._buf), self._flags, self._stream()),
+                          "so100_step")
+            done = self.terminated | self.truncated
+        else:
+            done = self._step_pixels()
         info = {"is_success": self.success, "diverged": self.diverged, "contact_bits": self.contact_bits}
         if self.autoreset:
-            info["final_observation"] = self.final_obs
+            info["final_observation"] = self.final_obs if self.renderer is None else \
+                {"pixels": self.final_pixels, "agent_pos": self.final_obs[:, 9:15]}
             info["_final_observation"] = done
         if self.is_goal:
             info["TimeLimit.truncated"] = self.truncated
@@ -233,12 +251,36 @@ class SO100VecEnv:
         self._action_ref = actions
         self._buf.action = _native.ptr(actions)
 
+    def _step_pixels(self):
+        """Pixel observations: step without the in-kernel reset, draw the terminal images of finished envs,
+        reset them with the masked reset kernel (same seeds/episode counters as the in-kernel reset), then
+        draw every env.  All on the current stream, no host synchronisation."""
+        s = self._stream()
+        flags = self._flags & ~_native.SO100_FLAG_AUTORESET
+        _native.check(self.lib.so100_step(self._handle, ctypes.byref(self._buf), flags, s), "so100_step")
+        done = self.terminated | self.truncated
+        if self.autoreset:
+            self.final_obs.copy_(self.obs)
+            self._mask.copy_(done)
+            self.renderer.render(out=self.final_pixels, mask=self._mask)
+            _native.check(self.lib.so100_reset(self._handle, ctypes.byref(self._buf), _native.ptr(self._mask), None,
+                                               s), "so100_reset")
+        self.renderer.render()
+        return done
+
     def step_async_raw(self):
         """Launch one env step on the current stream using the actions already in ``self.actions``
         (no argument handling, no output views) — the benchmark's hot loop."""
         self.lib.so100_step(self._handle, ctypes.byref(self._buf), self._flags, self._stream())
 
     def _observation(self):
+        if self.renderer is not None:
+            agent_pos = self.obs[:, 9:15]                       # qpos[:6] float32 (single_arm.py:45-50)
+            if self.is_goal:                                     # _flatten_observation (env.py:267-270)
+                flat = self.pixels.reshape(self.num_envs, -1).to(_torch().float32).div_(255.0)
+                return {"observation": _torch().cat([flat, agent_pos], dim=1), "achieved_goal": self.achieved_goal,
+                        "desired_goal": self.desired_goal}
+            return {"pixels": self.pixels, "agent_pos": agent_pos}
         if self.is_goal:
             return {"observation": self.obs, "achieved_goal": self.achieved_goal, "desired_goal": self.desired_goal}
         return self.obs

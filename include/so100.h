@@ -112,6 +112,30 @@ int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs);
  * uint64).  Enqueued on `stream`, no synchronisation. */
 int so100_contact_count(so100_env* env, uint64_t* accum, void* stream);
 
+/* ---- camera images: the reference's default observation, obs_type
+ * "so100_pixels_agent_pos" (gym_so100/__init__.py:4-32) = the `top` camera rendered by dm_control
+ * (gym_so100/env.py:84-94,130-136; scene_so100.xml:30).  A rasteriser of its own (not MuJoCo's OpenGL
+ * output): flat Lambert shading of the visible geoms under the scene's lights.  DESIGN.md §3.7. */
+#define SO100_MAX_LIGHTS 4
+typedef struct so100_camera {
+  float pos[3];                     /* camera position (world) */
+  float mat[9];                     /* row-major rotation; columns = camera x (right), y (up), z (backward) */
+  float fovy;                       /* vertical field of view, degrees */
+  float znear;                      /* triangles with a vertex nearer than this are not drawn */
+  float head_ambient, head_diffuse; /* headlight (scene_so100.xml:9) */
+  int   nlight;                     /* directional lights (scene_so100.xml:13-18) */
+  float light_dir[SO100_MAX_LIGHTS][3];
+  float light_diffuse[SO100_MAX_LIGHTS];
+} so100_camera;
+/* Upload the scene's triangles (host arrays): tri [ntri][3][3] vertices in their body's frame, body
+ * [ntri] (0 world, 1 Base, 2..7 arm links, 8 cube), rgb [ntri][3] base colour in [0, 1]. */
+int so100_render_mesh(so100_env* env, const float* tri, const int* body, const float* rgb, int ntri);
+/* Render the N envs at qpos (device [N][13]) from `cam` into out (device [N][height][width][3] uint8);
+ * mask (device [N] uint8, NULL = all) limits the envs drawn, the others' images are left as they were.
+ * Enqueued on stream; width <= 4096 and width * height <= 1 << 22. */
+int so100_render(so100_env* env, const float* qpos, const uint8_t* mask, const so100_camera* cam, int width,
+                 int height, uint8_t* out, void* stream);
+
 /* Batched sparse GoalEnv reward (env.py:341-353): out[i] = ||a_i - d_i|| < threshold ? 0 : -1. */
 int so100_goal_reward(so100_env* env, int n, const float* achieved, const float* desired, float* out,
                       void* stream);
