@@ -20,4 +20,6 @@ python tests/_trace_report.py $O/trace > $O/trace_report.txt 2>&1 || exit $?
 lscpu > $O/lscpu.txt 2>&1; nproc > $O/nproc.txt; echo "OMP_NUM_THREADS=$OMP_NUM_THREADS" >> $O/nproc.txt
 timeout -k 10 300 python bench.py --solver pgs --no-cpu-baseline > $O/bench_pgs.json 2> $O/bench_pgs.err || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_pgs -o bench_pgs --output-format csv -- python bench.py --solver pgs --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace_pgs.log 2>&1 || exit $?
+timeout -k 10 300 python -u tests/dev/render_bench.py $O/render_bench.json > $O/render_bench.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_render -o render --output-format csv -- python tests/dev/render_bench.py $O/render_bench_prof.json > $O/trace_render.log 2>&1 || exit $?
 echo ROUNDDONE
