@@ -44,6 +44,16 @@ struct Chunk {
   hipEvent_t done = nullptr;
 };
 
+struct StepGraph {
+  hipGraphExec_t exec = nullptr;
+  hipEvent_t done = nullptr;    // recorded after each replay (eviction waits for it)
+  so100_buffers buf{};
+  int flags = 0;
+  uint32_t par = 0;             // substep-counter parity at the captured step's start
+  uint64_t last_use = 0;
+};
+constexpr size_t kMaxStepGraphs = 32;
+
 struct so100_env {
   int device;
   int n;
@@ -64,7 +74,28 @@ struct so100_env {
   // profiling (so100_profile_enable): events[step][2 nsubstep + 2]
   std::vector<hipEvent_t> prof_ev;
   int prof_cap = 0, prof_used = 0;
+  // step graphs: the 21 launches per chunk, the chunk fork and join, captured once per (buffers, flags,
+  // substep parity) and replayed with one hipGraphLaunch when SO100_GRAPH=1.  A small LRU cache serves
+  // callers that rotate a few action buffers (bench.py's pool of 16).  Off by default: the step is not
+  // launch-bound (measured equal rates at 8,192 / 16,384 / 65,536 envs).
+  bool use_graph = false;
+  hipStream_t cap_s = nullptr;
+  std::vector<StepGraph> graphs;
+  uint64_t graph_clock = 0;
 };
+
+// An instantiated step graph can still be running when it is evicted: wait for its last replay first.
+static void graph_destroy(StepGraph& g) {
+  if (g.done) { (void)hipEventSynchronize(g.done); (void)hipEventDestroy(g.done); }
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  g.exec = nullptr;
+  g.done = nullptr;
+}
+
+static void graph_free(so100_env* env) {
+  for (StepGraph& g : env->graphs) graph_destroy(g);
+  env->graphs.clear();
+}
 
 static hipError_t free_chunks(so100_env* env) {
   hipError_t e = hipSuccess;
@@ -412,6 +443,7 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
   so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, h.solver, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
+  if (const char* v = getenv("SO100_GRAPH")) env->use_graph = atoi(v) != 0;
   e = make_chunks(env, default_chunks(n_envs));
   if (e != hipSuccess) {
     (void)free_chunks(env);
@@ -427,6 +459,8 @@ int so100_destroy(so100_env* env) {
   if (!env) return 0;
   DeviceGuard g(env->device);
   profile_free(env);
+  graph_free(env);
+  if (env->cap_s) (void)hipStreamDestroy(env->cap_s);
   if (env->r_tri) (void)hipFree(env->r_tri);
   if (env->r_body) (void)hipFree(env->r_body);
   if (env->r_rgb) (void)hipFree(env->r_rgb);
@@ -447,6 +481,7 @@ int so100_configure(so100_env* env, int task, int max_episode_steps, uint64_t ba
   env->base_seed = base_seed;
   if (env_offset < 0) return fail("so100_configure: env_offset < 0");
   env->env_offset = env_offset;
+  graph_free(env);                           // kernel arguments changed
   return 0;
 }
 
@@ -466,26 +501,14 @@ int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, con
   return e == hipSuccess ? 0 : fail_hip("so100_reset", e);
 }
 
-int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) {
-  if (!env) return fail("so100_step: env is NULL");
-  if (check_state(b)) return -1;
-  if (!b->action) return fail("so100_step: action is NULL");
-  if (env->task == SO100_TASK_GOAL && !b->desired_goal) return fail("so100_step: GoalEnv needs desired_goal");
-  if ((flags & SO100_FLAG_DR) && !b->dr_params) return fail("so100_step: FLAG_DR needs dr_params");
-  if ((flags & SO100_FLAG_AUTORESET) && !b->episode) return fail("so100_step: FLAG_AUTORESET needs episode");
-  DeviceGuard g(env->device);
-  hipEvent_t* ev = nullptr;
-  const int per = 2 * env->nsubstep + 2;
-  if (env->prof_used < env->prof_cap) ev = env->prof_ev.data() + (size_t)(env->prof_used++) * per;
-  const hipStream_t s = (hipStream_t)stream;
+// The launches of one env step on stream s: chunk 0 on s, chunks 1.. on their own streams forked from s
+// and joined back to it.  The profiling events (if any) ride on chunk 0.
+static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags, hipStream_t s, hipEvent_t* ev) {
   if (env->chunks.size() == 1) {
     Chunk& c = env->chunks[0];
-    hipError_t e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c.ws, *b, c.count, env->task, flags, env->max_steps,
-                                      env->base_seed, env->env_offset, s, ev);
-    return e == hipSuccess ? 0 : fail_hip("so100_step", e);
+    return so100::launch_step(env->d_model, env->nsubstep, env->solver, c.ws, *b, c.count, env->task, flags, env->max_steps,
+                              env->base_seed, env->env_offset, s, ev);
   }
-  // fork: chunks 1.. wait for the caller's prior work, chunk 0 runs on the caller's stream; join: the
-  // caller's stream waits for every other chunk.  The profiling events (if any) ride on chunk 0.
   hipError_t e = hipEventRecord(env->fork, s);
   for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) {
     Chunk& c = env->chunks[k];
@@ -500,6 +523,79 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
     e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
                            env->base_seed, env->env_offset, s, ev);
   for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) e = hipStreamWaitEvent(s, env->chunks[k].done, 0);
+  return e;
+}
+
+// Capture the step for (b, flags) on the private capture stream and instantiate it into g.
+static hipError_t build_step_graph(so100_env* env, const so100_buffers* b, int flags, StepGraph& g) {
+  const uint32_t par = env->chunks[0].ws.sub_count & 1u;
+  hipError_t e = hipSuccess;
+  if (!env->cap_s) e = hipStreamCreateWithFlags(&env->cap_s, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g.done, hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  e = hipStreamBeginCapture(env->cap_s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) return e;
+  hipError_t el = enqueue_step(env, b, flags, env->cap_s, nullptr);
+  hipGraph_t graph = nullptr;
+  e = hipStreamEndCapture(env->cap_s, &graph);
+  if (el != hipSuccess) e = el;
+  if (e == hipSuccess) e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+  if (graph) (void)hipGraphDestroy(graph);
+  if (e != hipSuccess) { g.exec = nullptr; return e; }
+  g.buf = *b;
+  g.flags = flags;
+  g.par = par;
+  return hipSuccess;
+}
+
+// Replay the step graph for (b, flags) on s, capturing it first if it is not cached.
+static hipError_t graph_step(so100_env* env, const so100_buffers* b, int flags, hipStream_t s) {
+  const uint32_t par = env->chunks[0].ws.sub_count & 1u;
+  StepGraph* hit = nullptr;
+  for (StepGraph& g : env->graphs)
+    if (g.flags == flags && g.par == par && memcmp(&g.buf, b, sizeof(so100_buffers)) == 0) { hit = &g; break; }
+  hipError_t e = hipSuccess;
+  if (hit) {
+    // the capture advanced the host substep counters as an eager step would; a replay does it here
+    for (Chunk& c : env->chunks) c.ws.sub_count += (uint32_t)env->nsubstep;
+  } else {
+    if (env->graphs.size() >= kMaxStepGraphs) {
+      size_t lru = 0;
+      for (size_t i = 1; i < env->graphs.size(); i++)
+        if (env->graphs[i].last_use < env->graphs[lru].last_use) lru = i;
+      graph_destroy(env->graphs[lru]);
+      env->graphs.erase(env->graphs.begin() + (long)lru);
+    }
+    StepGraph g;
+    e = build_step_graph(env, b, flags, g);
+    if (e != hipSuccess) { graph_destroy(g); return e; }
+    env->graphs.push_back(g);
+    hit = &env->graphs.back();
+  }
+  hit->last_use = ++env->graph_clock;
+  e = hipGraphLaunch(hit->exec, s);
+  if (e == hipSuccess) e = hipEventRecord(hit->done, s);
+  return e;
+}
+
+int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) {
+  if (!env) return fail("so100_step: env is NULL");
+  if (check_state(b)) return -1;
+  if (!b->action) return fail("so100_step: action is NULL");
+  if (env->task == SO100_TASK_GOAL && !b->desired_goal) return fail("so100_step: GoalEnv needs desired_goal");
+  if ((flags & SO100_FLAG_DR) && !b->dr_params) return fail("so100_step: FLAG_DR needs dr_params");
+  if ((flags & SO100_FLAG_AUTORESET) && !b->episode) return fail("so100_step: FLAG_AUTORESET needs episode");
+  DeviceGuard g(env->device);
+  hipEvent_t* ev = nullptr;
+  const int per = 2 * env->nsubstep + 2;
+  if (env->prof_used < env->prof_cap) ev = env->prof_ev.data() + (size_t)(env->prof_used++) * per;
+  const hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (env->use_graph && !ev) {
+    e = graph_step(env, b, flags, s);
+  } else {
+    e = enqueue_step(env, b, flags, s, ev);
+  }
   return e == hipSuccess ? 0 : fail_hip("so100_step", e);
 }
 

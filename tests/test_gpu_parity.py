@@ -647,3 +647,34 @@ def test_self_collision_parity(solver, oracle64, oracle32):
     assert np.mean(qv_err > 1e-4) <= 1.5 * np.mean(qv_floor > 1e-4) + 0.05    # tail mass (MPR: see above)
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     env.close()
+
+
+def test_step_graph_replay_matches_eager(monkeypatch):
+    """so100_step replays a captured hipGraph of the step (chunk fork/join included); SO100_GRAPH=0 launches
+    eagerly.  Both must give bit-identical trajectories, across re-captures (new action buffer, flags)."""
+    import torch
+    from gym_so100 import SO100VecEnv
+    n = 4096                                        # 4 chunks: the forked streams are captured too
+    monkeypatch.setenv("SO100_GRAPH", "0")
+    eager = SO100VecEnv(n, max_episode_steps=7, seed=3)
+    monkeypatch.setenv("SO100_GRAPH", "1")
+    graph = SO100VecEnv(n, max_episode_steps=7, seed=3)
+    assert eager.chunk_info()[0] == 4
+    eager.reset(seed=9)
+    graph.reset(seed=9)
+    g = torch.Generator().manual_seed(1)
+    other = torch.zeros(n, 6, device="cuda:0")
+    for t in range(20):
+        act = (torch.rand(n, 6, generator=g) * 2 - 1).cuda()
+        if t == 10:                                 # a different action buffer: the graph is re-captured
+            other.copy_(act)
+            graph.set_action_buffer(other)
+            eager.set_action_buffer(other)
+        for e in (eager, graph):
+            if t >= 10:
+                e.step_async_raw()
+            else:
+                e.step(act)
+        torch.cuda.synchronize()
+        for name in ("qpos", "qvel", "qacc_warmstart", "obs", "reward", "terminated", "truncated", "elapsed", "episode"):
+            assert torch.equal(getattr(eager, name), getattr(graph, name)), (t, name)
