@@ -412,6 +412,27 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->action_hi[i] = (float)s->action_hi[i];
     d->action_span[i] = (float)(s->action_hi[i] - s->action_lo[i]);
   }
+  // EE / mocap weld
+  if (s->ee != 0 && s->ee != 1) return fail("model: ee must be 0 or 1");
+  d->ee = s->ee;
+  {
+    double q[4], R[9];
+    normq(s->weld_quat2, q);
+    quat2mat(q, R);
+    for (int k = 0; k < 9; k++) d->weld_mat2[k] = (float)R[k];
+    for (int k = 0; k < 3; k++) d->weld_pos2[k] = (float)s->weld_pos2[k];
+    for (int k = 0; k < 5; k++) d->weld_solimp[k] = (float)s->weld_solimp[k];
+    solref_kb(s->weld_solref, s->weld_solimp, s->timestep, &K, &B);
+    d->weld_K = (float)K;
+    d->weld_B = (float)B;
+    d->weld_ts = (float)s->weld_torquescale;
+    for (int k = 0; k < 2; k++) d->weld_invw[k] = (float)s->weld_invweight0[k];
+    for (int k = 0; k < 3; k++) d->mocap0[k] = (float)s->mocap_pos0[k];
+    normq(s->mocap_quat0, q);
+    for (int k = 0; k < 4; k++) d->mocap0[3 + k] = (float)q[k];
+    if (s->ee && !(s->weld_invweight0[0] > 0 && s->weld_invweight0[1] > 0 && s->weld_solimp[2] > 0))
+      return fail("model: weld parameters");
+  }
   return 0;
 }
 }  // namespace

@@ -96,6 +96,14 @@ struct DevModel {
   float action_lo[6], action_hi[6], action_span[6];
   double spawn_lo[3], spawn_hi[3];
   float goal_bin_lo[3], goal_bin_hi[3];   // env.py:245-249
+
+  // EE / mocap variant: weld of ee_site (Fixed_Jaw frame) to the mocap pose (so_arm100_ee.xml:171-173)
+  int ee;
+  float weld_pos2[3], weld_mat2[9];
+  float weld_solimp[5];
+  float weld_K, weld_B, weld_ts;
+  float weld_invw[2];                     // tran, rot
+  float mocap0[7];                        // default mocap pose (pos, quat)
 };
 
 // ------------------------------------------------------------------ substep workspace (HBM)

@@ -67,8 +67,9 @@ struct __attribute__((aligned(16))) EnvShared {
     };
     SerialScratch ser;           // dynamics scratch (dead before collision) + link frames (live through it)
   };
+  float mocap[8];                // EE variant: mocap pose (pos, quat wxyz)
   // stride = 13.25 x 256 B: the 4 envs of a wave hit different LDS bank windows for the same field
-  float bank_pad[16];
+  float bank_pad[8];
 };
 
 // ------------------------------------------------------------------ small math (same formulas as oracle)

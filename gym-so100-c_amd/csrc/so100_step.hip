@@ -178,6 +178,123 @@ DEV float hash_normal(uint64_t key) {
 // comPos, CRBA, Cholesky (lane 0) + M^-1 columns, RNE and actuation, with every sum in the serial
 // order of the lane-0 version (prefix sums of cvel/cacc, suffix sums of crb/bias) so results are the
 // same bit-for-bit.  Requires fk_stage first and a barrier.
+// ------------------------------------------------------------------ EE / mocap variant: weld equality
+// MuJoCo's mju_mat2Quat with the sign w >= 0 (oracle mat2quat_pos)
+DEV void mat2quat_pos(float* q, const float* r) {
+  const float tr = r[0] + r[4] + r[8];
+  if (tr > 0.f) {
+    q[0] = 0.5f * sqrtf(tr + 1.f);
+    const float i4 = 1.f / (4.f * q[0]);
+    q[1] = (r[7] - r[5]) * i4; q[2] = (r[2] - r[6]) * i4; q[3] = (r[3] - r[1]) * i4;
+  } else if (r[0] > r[4] && r[0] > r[8]) {
+    q[1] = 0.5f * sqrtf(1.f + r[0] - r[4] - r[8]);
+    const float i4 = 1.f / (4.f * q[1]);
+    q[0] = (r[7] - r[5]) * i4; q[2] = (r[1] + r[3]) * i4; q[3] = (r[2] + r[6]) * i4;
+  } else if (r[4] > r[8]) {
+    q[2] = 0.5f * sqrtf(1.f - r[0] + r[4] - r[8]);
+    const float i4 = 1.f / (4.f * q[2]);
+    q[0] = (r[2] - r[6]) * i4; q[1] = (r[1] + r[3]) * i4; q[3] = (r[5] + r[7]) * i4;
+  } else {
+    q[3] = 0.5f * sqrtf(1.f - r[0] - r[4] + r[8]);
+    const float i4 = 1.f / (4.f * q[3]);
+    q[0] = (r[3] - r[1]) * i4; q[1] = (r[2] + r[6]) * i4; q[2] = (r[5] + r[7]) * i4;
+  }
+  quat_normalize(q);
+  if (q[0] < 0.f) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+}
+
+// [3P] mj_makeEquality mjEQ_WELD for so_arm100_ee.xml:171-173 (site1 on the mocap body, site2 = ee_site on
+// Fixed_Jaw), restated as oracle weld_fold: 6 always-active quadratic rows, eliminated exactly into the arm
+// block of M (M += J'DJ) and the joint force (J'D aref, added to tau at the end of dynamics_par; DESIGN.md
+// §4 deviation 10).  Called between the CRBA and the Cholesky; scratch: S.X (J rows, dead until the
+// M^-1 columns), S.F (dead after the CRBA).  Uniform per block (m->ee), so its barriers are safe.
+DEV void weld_fold(const DevModel* __restrict__ m, EnvShared& sh, int lane) {
+  SerialScratch& S = sh.ser;
+  float (*J)[8] = S.X;                       // J[row][dof 0..5]
+  // F[0][0..5] residual, F[1][0..3] e, F[2][0..7] + F[3][0] R2, F[3][4..6] p2, F[4] D, F[5] D aref
+  if (lane == 0) {
+    float R2[9], p2[3], t[3], q1[4], R1[9], Rr[9], e[4];
+    mulmm3(R2, S.xm[4], m->weld_mat2);
+    mulmv3(t, S.xm[4], m->weld_pos2);
+#pragma unroll
+    for (int k = 0; k < 3; k++) p2[k] = S.xp[4][k] + t[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) q1[k] = sh.mocap[3 + k];
+    quat_normalize(q1);
+    quat2mat(R1, q1);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) Rr[3 * i + j] = R2[i] * R1[j] + R2[3 + i] * R1[3 + j] + R2[6 + i] * R1[6 + j];
+    mat2quat_pos(e, Rr);
+#pragma unroll
+    for (int k = 0; k < 3; k++) { S.F[0][k] = sh.mocap[k] - p2[k]; S.F[0][3 + k] = m->weld_ts * e[1 + k]; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) S.F[1][k] = e[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) S.F[2][k] = R2[k];
+    S.F[3][0] = R2[8];
+#pragma unroll
+    for (int k = 0; k < 3; k++) S.F[3][4 + k] = p2[k];
+  }
+  __syncthreads();
+  // columns: lane j = hinge j (the Jaw hinge, j = 5, is not on the ee chain)
+  if (lane < 6) {
+    const int j = lane;
+    float R2[9], p2[3], e[4], ax[3], dp[3], c[3], a[3], v[3], vc[3];
+#pragma unroll
+    for (int k = 0; k < 8; k++) R2[k] = S.F[2][k];
+    R2[8] = S.F[3][0];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { p2[k] = S.F[3][4 + k]; ax[k] = sh.axis[j][k]; dp[k] = p2[k] - sh.anchor[j][k]; a[k] = -ax[k]; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) e[k] = S.F[1][k];
+    cross3(c, ax, dp);
+    mulmtv3(v, R2, a);
+    cross3(vc, v, e + 1);
+    const bool on = j < 5;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      J[k][j] = on ? -c[k] : 0.f;
+      J[3 + k][j] = on ? 0.5f * m->weld_ts * (e[0] * v[k] + vc[k]) : 0.f;
+    }
+  }
+  __syncthreads();
+  // rows: lane i
+  if (lane < 6) {
+    const int i = lane;
+    float vel = 0.f;
+#pragma unroll
+    for (int j = 0; j < 6; j++) vel += J[i][j] * sh.qvel[j];
+    const float pos = S.F[0][i];
+    const float imp = getimpedance(m->weld_solimp, pos, 0.f);
+    const float R = fmaxf(kMinVal, (1.f - imp) / imp * m->weld_invw[i < 3 ? 0 : 1]);
+    const float D = 1.f / R;
+    S.F[4][i] = D;
+    S.F[5][i] = D * (-m->weld_B * vel - m->weld_K * imp * pos);
+  }
+  __syncthreads();
+  // M += J'DJ (lane i: entries j <= i and their mirrors, as the CRBA), J'D aref -> F[1]
+  if (lane < 6) {
+    const int i = lane;
+    float f = 0.f;
+#pragma unroll
+    for (int r = 0; r < 6; r++) f += J[r][i] * S.F[5][r];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      if (j <= i) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 6; r++) v += J[r][i] * S.F[4][r] * J[r][j];
+        S.M[i][j] += v;
+        if (j != i) S.M[j][i] += v;
+      }
+    }
+    sh.qacc_smooth[i] = f;                    // staged here until tau (qacc_smooth is written last)
+  }
+  __syncthreads();
+}
+
 DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale) {
   SerialScratch& S = sh.ser;
   // ---- comPos (body a = lane): cinert about the tree reference point r = Base xpos; cdof
@@ -249,6 +366,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     }
   }
   __syncthreads();
+  if (m->ee) weld_fold(m, sh, lane);
   // ---- Cholesky of the 6x6 (lane 0), diagonal reciprocals stored for the column solves
   if (lane == 0) {
     float L[6][6], Linv[6];
@@ -367,7 +485,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     const float c = fminf(fmaxf(sh.ctrl[a], m->act_clo[a]), m->act_chi[a]);
     float f = m->act_kp[a] * c - m->act_kp[a] * sh.qpos[a] - m->act_kv[a] * sh.qvel[a];
     f = fminf(fmaxf(f, m->act_flo[a]), m->act_fhi[a]);
-    S.tau[a] = f - bias;
+    S.tau[a] = f - bias + (m->ee ? sh.qacc_smooth[a] : 0.f);   // + J'D aref of the weld (weld_fold)
   }
   __syncthreads();
   if (lane < 6) {
@@ -1542,6 +1660,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
                                             ((uint64_t)episode0 << 20) ^ (uint64_t)(elapsed0 * 8 + lane)));
       sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
     }
+    if (m->ee && lane < 7) sh.mocap[lane] = B.mocap ? B.mocap[(size_t)e * 7 + lane] : m->mocap0[lane];
     // ---------------- S1: stage state in LDS
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
     if (lane < SO100_NV) sh.qvel[lane] = qvel_r;

@@ -67,6 +67,9 @@ class SO100Model(ctypes.Structure):
         ("spawn_lo", _arr(_d, 3)), ("spawn_hi", _arr(_d, 3)),
         ("bin_hw", _d), ("bin_h", _d), ("cube_half", _d), ("goal_threshold", _d), ("max_reward", _d),
         ("goal_bin_lo", _arr(_d, 3)), ("goal_bin_hi", _arr(_d, 3)),
+        ("ee", ctypes.c_int), ("weld_pos2", _arr(_d, 3)), ("weld_quat2", _arr(_d, 4)), ("weld_solref", _arr(_d, 2)),
+        ("weld_solimp", _arr(_d, 5)), ("weld_torquescale", _d), ("weld_invweight0", _arr(_d, 2)),
+        ("mocap_pos0", _arr(_d, 3)), ("mocap_quat0", _arr(_d, 4)),
     ]
 
 
@@ -93,14 +96,19 @@ def load_model_dict(path=ASSET):
         return json.load(f)
 
 
+VARIANTS = ("joint", "ee")
 SOLVERS = {"pgs": 0, "newton": 1}      # SO100_SOLVER_* (include/so100_model.h)
 
 
-def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton"):
+def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton", variant="joint"):
     """Return an ``SO100Model`` ctypes struct filled from the derived model table.
 
     solver: "newton" (default: MuJoCo's default solver, which the reference's model uses --
-    so_arm100.xml:4 sets no solver) or "pgs" (north_star's projected Gauss-Seidel)."""
+    so_arm100.xml:4 sets no solver) or "pgs" (north_star's projected Gauss-Seidel).
+    variant: "joint" (so100_transfer_cube.xml, the registered envs) or "ee" (so100_transfer_cube_ee.xml:
+    a weld equality pulls ee_site to a per-env mocap pose, so_arm100_ee.xml:155,171-173)."""
+    if variant not in VARIANTS:
+        raise ValueError(f"variant {variant!r}: one of {VARIANTS}")
     d = load_model_dict(path)
     m = SO100Model()
     o = d["opt"]
@@ -174,6 +182,16 @@ def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton"):
     hi = [float(np.float32(C.bin_max[0]) - np.float32(0.005)), float(np.float32(C.bin_max[1]) - np.float32(0.005)), 0.05]
     _set(m, "goal_bin_lo", lo)
     _set(m, "goal_bin_hi", hi)
+    w = d["weld"]
+    m.ee = 1 if variant == "ee" else 0
+    _set(m, "weld_pos2", w["pos2"])
+    _set(m, "weld_quat2", w["quat2"])
+    _set(m, "weld_solref", w["solref"])
+    _set(m, "weld_solimp", w["solimp"])
+    m.weld_torquescale = w["torquescale"]
+    _set(m, "weld_invweight0", w["invweight0"])
+    _set(m, "mocap_pos0", w["mocap_pos"])
+    _set(m, "mocap_quat0", w["mocap_quat"])
     return m
 
 

@@ -68,6 +68,9 @@ class SO100VecEnv:
         obs_type: "so100_state" (15 floats) or "so100_pixels_agent_pos" (the reference's registered
             default: top-camera image + joint positions; GoalEnv: the flattened form of env.py:267-270).
         observation_width, observation_height: image size for pixel observations (env.py:34-35).
+        variant: "joint" (so100_transfer_cube.xml, the registered envs) or "ee" (so100_transfer_cube_ee.xml:
+            a weld equality pulls ee_site to each env's mocap pose ``self.mocap`` [N,7], set with
+            ``set_mocap``; teleop_ee.py drives the same inputs).
         device: torch device string ("cuda:0").
         seed: base seed for in-kernel (auto-)reset spawns.
         max_episode_steps: TimeLimit; default per task as registered by the reference.
@@ -85,7 +88,8 @@ class SO100VecEnv:
 
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
-                 iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480):
+                 iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480,
+                 variant="joint"):
         torch = _torch()
         if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
             raise NotImplementedError(f"obs_type={obs_type!r}: 'so100_state' or 'so100_pixels_agent_pos'")
@@ -103,7 +107,8 @@ class SO100VecEnv:
         self.base_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.env_offset = int(env_offset)
         self.solver = solver
-        self.model = build_model(iterations=iterations, solver=solver)
+        self.variant = variant
+        self.model = build_model(iterations=iterations, solver=solver, variant=variant)
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._handle = self.lib.so100_create(ctypes.byref(self.model), self.num_envs, dev_index)
         if not self._handle:
@@ -131,6 +136,10 @@ class SO100VecEnv:
         self.desired_goal = torch.zeros(n, 3, dtype=f32, device=d) if self.is_goal else None
         self.total_steps = torch.zeros(n, dtype=i32, device=d) if self.is_goal else None
         self.debug = torch.zeros(n, _native.SO100_DBG_STRIDE, dtype=f32, device=d) if debug else None
+        self.mocap = None
+        if variant == "ee":          # mj_resetData's mocap pose: the mocap body's (so_arm100_ee.xml:155)
+            m0 = list(self.model.mocap_pos0) + list(self.model.mocap_quat0)
+            self.mocap = torch.tensor(m0, dtype=f32, device=d).repeat(n, 1).contiguous()
         self.dr_params = None
         self._flags = _native.SO100_FLAG_AUTORESET if self.autoreset else 0
         if domain_randomization:
@@ -152,9 +161,27 @@ class SO100VecEnv:
         b = self._buf
         for name in ("qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "obs", "reward", "terminated",
                      "truncated", "success", "final_obs", "diverged", "contact_bits", "achieved_goal",
-                     "desired_goal", "total_steps", "dr_params", "debug"):
+                     "desired_goal", "total_steps", "dr_params", "debug", "mocap"):
             setattr(b, name, P(getattr(self, name)))
         b.action = P(self.actions)
+
+    def set_mocap(self, pos, quat=None, mask=None):
+        """EE variant: the mocap target pose of every env (pos [N,3], quat [N,4] wxyz; the data.mocap_pos /
+        data.mocap_quat that teleop_ee.py:52-98 edits), or of the envs in mask."""
+        torch = _torch()
+        if self.mocap is None:
+            raise ValueError("set_mocap needs variant='ee'")
+        p = torch.as_tensor(pos, dtype=torch.float32, device=self.device).reshape(-1, 3)
+        q = None if quat is None else torch.as_tensor(quat, dtype=torch.float32, device=self.device).reshape(-1, 4)
+        if mask is None:
+            self.mocap[:, :3] = p
+            if q is not None:
+                self.mocap[:, 3:] = q
+        else:
+            m = torch.as_tensor(mask, device=self.device).bool()
+            self.mocap[m, :3] = p if p.shape[0] != self.num_envs else p[m]
+            if q is not None:
+                self.mocap[m, 3:] = q if q.shape[0] != self.num_envs else q[m]
 
     def _stream(self):
         return _native.stream_ptr(_torch(), self.device)

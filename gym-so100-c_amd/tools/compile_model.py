@@ -428,6 +428,37 @@ def compile_model():
             pairs.append(dict(g1=-1 - k1, g2=-1 - k2, body1=b1, body2=b2, name1=h1["name"], name2=h2["name"],
                               hull=k2, hull1=k1, **mixed(h1, h2)))
 
+    # ---- EE / mocap variant (so100_transfer_cube_ee.xml: the same scene with trs_so_arm100/so_arm100_ee.xml,
+    # whose only differences are the mocap body at :155 and the weld equality at :171-173) ----
+    ee = ET.parse(os.path.join(ASSETS, "trs_so_arm100", "so_arm100_ee.xml")).getroot()
+    weld = ee.find("equality").find("weld")
+    assert weld.get("site1") == "mocap_target_site" and weld.get("site2") == "ee_site"
+    mocap = [b for b in ee.find("worldbody").findall("body") if b.get("mocap") == "true"][0]
+    msite = [x for x in mocap.findall("site") if x.get("name") == "mocap_target_site"][0]
+    assert vec(msite.get("pos", "0 0 0"), 3).tolist() == [0, 0, 0] and not msite.get("quat")
+    cf = bodies["vx300s_left/camera_focus"]
+    assert bodies["vx300s_left/camera_focus"]["parent"] == "Fixed_Jaw" and np.allclose(cf["quat"], [1, 0, 0, 0])
+    ee_local = cf["pos"] + vec([x for x in cf["sites"] if x["name"] == "ee_site"][0].get("pos", "0 0 0"), 3)
+    # body_invweight0 of the ee_site body (massless, COM at its origin; welded to Fixed_Jaw) at qpos0
+    fj = bid["Fixed_Jaw"]
+    c = xpos[fj] + quat2mat(xquat[fj]) @ ee_local
+    Jv = np.zeros((3, nv)); Jw = np.zeros((3, nv))
+    a = fj
+    while a > 0:
+        if a in jnt_body:
+            j = jnt_body.index(a)
+            Jw[:, j] = xaxis[j]
+            Jv[:, j] = np.cross(xaxis[j], c - xanchor[j])
+        a = body_parent[a]
+    Aw = np.vstack([Jv, Jw]) @ Minv @ np.vstack([Jv, Jw]).T
+    solimp = vec(weld.get("solimp"), 3).tolist() + [0.5, 2.0]          # MuJoCo defaults for mid, power
+    weld_info = dict(body2=fj, pos2=ee_local.tolist(), quat2=[1.0, 0.0, 0.0, 0.0],
+                     solref=vec(weld.get("solref"), 2).tolist(), solimp=solimp,
+                     torquescale=float(weld.get("torquescale", 1)),
+                     invweight0=[float(np.trace(Aw[:3, :3]) / 3), float(np.trace(Aw[3:, 3:]) / 3)],
+                     mocap_pos=vec(mocap.get("pos"), 3).tolist(), mocap_quat=[1.0, 0.0, 0.0, 0.0],
+                     mocap_box=dict(size=vec(mocap.find("geom").get("size"), 3).tolist()))
+
     # ---- sites ----
     cube_site = vec(bodies["box"]["sites"][0]["pos"], 3)
     cf = bodies["vx300s_left/camera_focus"]
@@ -453,6 +484,7 @@ def compile_model():
                  meaninertia=meaninertia),
         qpos0_box=box_pos0.tolist(),
         M0=M.tolist(),
+        weld=weld_info,
     )
     return model
 

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 4   /* 4: so100_model.solver, hull centroids, 98 contact pairs */
+#define SO100_ABI_VERSION 5   /* 5: EE/mocap weld (so100_model.ee, so100_buffers.mocap), render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -63,6 +63,10 @@ typedef struct so100_buffers {
   const float* dr_params;
   /* diagnostics: [N, SO100_DBG_STRIDE] floats or NULL */
   float*    debug;
+  /* EE / mocap variant (model.ee = 1): [N,7] mocap body pose, position(3) + quaternion wxyz(4), the
+   * target the weld equality pulls ee_site to (teleop_ee.py:52-98 drives data.mocap_pos/quat); NULL =
+   * the model's default pose */
+  const float* mocap;
 } so100_buffers;
 
 #define SO100_DBG_STRIDE 96  /* ncon, solver_iter, improvement, nefc, qacc[12], contact(dist,fn)[16], ... */

@@ -149,6 +149,18 @@ typedef struct so100_model {
   double max_reward;                /* single_arm.py:130,227,297 */
   double goal_bin_lo[3];            /* env.py:245-249 bin_goal_space (constants.py:29-30) */
   double goal_bin_hi[3];
+
+  /* EE / mocap variant (so100_transfer_cube_ee.xml with trs_so_arm100/so_arm100_ee.xml:155,171-173): a
+   * weld equality between the mocap body's site and ee_site drives the end effector to a per-env pose */
+  int    ee;                        /* 1: weld on (so100_buffers.mocap), 0: the reference's default model */
+  double weld_pos2[3];              /* ee_site in the Fixed_Jaw frame */
+  double weld_quat2[4];             /* ee_site frame orientation in the Fixed_Jaw frame */
+  double weld_solref[2];            /* so_arm100_ee.xml:172 */
+  double weld_solimp[5];
+  double weld_torquescale;
+  double weld_invweight0[2];        /* body_invweight0 (tran, rot) of the ee_site body; the mocap body's is 0 */
+  double mocap_pos0[3];             /* so_arm100_ee.xml:155 mocap body pose (default of the mocap input) */
+  double mocap_quat0[4];
 } so100_model;
 
 #ifdef __cplusplus

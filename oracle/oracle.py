@@ -50,6 +50,9 @@ def _make_types(real):
             ("efc_aref", _arr(real, NEFC)), ("efc_b", _arr(real, NEFC)), ("efc_AR", _arr(real, NEFC, NEFC)),
             ("efc_force", _arr(real, NEFC)), ("qacc", _arr(real, NV)),
             ("solver_iter", i), ("solver_improvement", real), ("elapsed_steps", i),
+            ("mocap_pos", _arr(real, 3)), ("mocap_quat", _arr(real, 4)),
+            ("weld_pos", _arr(real, 6)), ("weld_J", _arr(real, 6, NV)), ("weld_D", _arr(real, 6)),
+            ("weld_aref", _arr(real, 6)), ("weld_f", _arr(real, NV)),
         ]
     return Contact, Data
 

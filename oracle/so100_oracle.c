@@ -1144,10 +1144,102 @@ static void make_constraint(const so100_model* m, so100o_data* d) {
   for (int i = 0; i < r; i++) d->efc_D[i] = 1 / d->efc_R[i];
 }
 
+/* ============================================================== EE / mocap variant: weld equality */
+/* [3P] mju_mat2Quat, then the sign with w >= 0 (the shortest rotation) */
+static void mat2quat_pos(real q[4], const real r[9]) {
+  const real tr = r[0] + r[4] + r[8];
+  if (tr > 0) {
+    q[0] = (real)0.5 * (real)sqrt((double)(tr + 1));
+    q[1] = (r[7] - r[5]) / (4 * q[0]); q[2] = (r[2] - r[6]) / (4 * q[0]); q[3] = (r[3] - r[1]) / (4 * q[0]);
+  } else if (r[0] > r[4] && r[0] > r[8]) {
+    q[1] = (real)0.5 * (real)sqrt((double)(1 + r[0] - r[4] - r[8]));
+    q[0] = (r[7] - r[5]) / (4 * q[1]); q[2] = (r[1] + r[3]) / (4 * q[1]); q[3] = (r[2] + r[6]) / (4 * q[1]);
+  } else if (r[4] > r[8]) {
+    q[2] = (real)0.5 * (real)sqrt((double)(1 - r[0] + r[4] - r[8]));
+    q[0] = (r[2] - r[6]) / (4 * q[2]); q[1] = (r[1] + r[3]) / (4 * q[2]); q[3] = (r[5] + r[7]) / (4 * q[2]);
+  } else {
+    q[3] = (real)0.5 * (real)sqrt((double)(1 - r[0] - r[4] + r[8]));
+    q[0] = (r[3] - r[1]) / (4 * q[3]); q[1] = (r[2] + r[6]) / (4 * q[3]); q[2] = (r[5] + r[7]) / (4 * q[3]);
+  }
+  quat_normalize(q);
+  if (q[0] < 0) for (int k = 0; k < 4; k++) q[k] = -q[k];
+}
+
+/* [3P] mj_makeEquality, mjEQ_WELD (engine_core_constraint.c), for so_arm100_ee.xml:171-173: site1 =
+ * mocap_target_site (the mocap body: no dofs), site2 = ee_site (welded to Fixed_Jaw, body 6).
+ *   residual  r = (p1 - p2, torquescale * imag(e)),  e = conj(q2) q1 = quat(R2' R1), w >= 0;
+ *   Jacobian  J_pos = jacp(mocap, p1) - jacp(ee, p2) = -jacp(ee, p2);
+ *             J_rot col j = 0.5 torquescale imag(conj(q2) (0, a_j) q1) = 0.5 ts imag((0, R2' a_j) e),
+ *             a_j = jacr(mocap) - jacr(ee) = -axis_j (hinges on the ee body's chain);
+ *   impedance of |r_i| (getimpedance), R = (1-imp)/imp * (invweight0(mocap) = 0 + invweight0(ee body)),
+ *   aref = -B (J qvel) - K imp r.
+ * MuJoCo takes e from the bodies' quaternions as they come (no sign choice); the two agree whenever
+ * their product has w >= 0, i.e. for relative rotations below 180 degrees of the tracked branch.
+ * The six rows are always active and quadratic (mjCNSTR_EQUALITY), so they are eliminated from the
+ * constrained problem exactly: M <- M + J'DJ here and qfrc += J'D aref in the acceleration stage
+ * (DESIGN.md §4 deviation 10); the solvers then see the frictionloss, limit and contact rows only. */
+static void weld_fold(const so100_model* m, so100o_data* d) {
+  const int b = 6;                                                 /* Fixed_Jaw */
+  real pos2[3], q2l[4], R2l[9], R2[9], p2[3], t[3];
+  load3(pos2, m->weld_pos2);
+  load4(q2l, m->weld_quat2);
+  quat_normalize(q2l);
+  quat2mat(R2l, q2l);
+  mulmm3(R2, d->xmat[b], R2l);
+  mulmv3(t, d->xmat[b], pos2);
+  for (int k = 0; k < 3; k++) p2[k] = d->xpos[b][k] + t[k];
+  real q1[4] = {d->mocap_quat[0], d->mocap_quat[1], d->mocap_quat[2], d->mocap_quat[3]}, R1[9], Rr[9], e[4];
+  quat_normalize(q1);
+  quat2mat(R1, q1);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) Rr[3 * i + j] = R2[i] * R1[j] + R2[3 + i] * R1[3 + j] + R2[6 + i] * R1[6 + j];
+  mat2quat_pos(e, Rr);
+  const real ts = (real)m->weld_torquescale;
+  for (int k = 0; k < 3; k++) { d->weld_pos[k] = d->mocap_pos[k] - p2[k]; d->weld_pos[3 + k] = ts * e[1 + k]; }
+  memset(d->weld_J, 0, sizeof(d->weld_J));
+  for (int j = 0; j < SO100_NHINGE; j++) {
+    if (m->jnt_body[j] > b) continue;                              /* the Jaw hinge is not on the chain */
+    const real* ax = d->xaxis[j];
+    real dp[3] = {p2[0] - d->xanchor[j][0], p2[1] - d->xanchor[j][1], p2[2] - d->xanchor[j][2]}, c[3];
+    cross3(c, ax, dp);
+    real a[3] = {-ax[0], -ax[1], -ax[2]}, v[3], vc[3];
+    mulmtv3(v, R2, a);
+    cross3(vc, v, e + 1);
+    for (int k = 0; k < 3; k++) {
+      d->weld_J[k][j] = -c[k];
+      d->weld_J[3 + k][j] = (real)0.5 * ts * (e[0] * v[k] + vc[k]);
+    }
+  }
+  real K, B;
+  solref_kb(m->weld_solref, m->weld_solimp, (real)m->timestep, &K, &B);
+  for (int i = 0; i < 6; i++) {
+    real vel = 0;
+    for (int j = 0; j < SO100_NV; j++) vel += d->weld_J[i][j] * d->qvel[j];
+    const real imp = getimpedance(m->weld_solimp, d->weld_pos[i], 0);
+    real R = (1 - imp) / imp * (real)m->weld_invweight0[i < 3 ? 0 : 1];
+    R = R > MINVAL ? R : MINVAL;
+    d->weld_D[i] = 1 / R;
+    d->weld_aref[i] = -B * vel - K * imp * d->weld_pos[i];
+  }
+  for (int i = 0; i < SO100_NV; i++) {
+    real f = 0;
+    for (int r = 0; r < 6; r++) f += d->weld_J[r][i] * d->weld_D[r] * d->weld_aref[r];
+    d->weld_f[i] = f;
+    for (int j = 0; j <= i; j++) {
+      real v = 0;
+      for (int r = 0; r < 6; r++) v += d->weld_J[r][i] * d->weld_D[r] * d->weld_J[r][j];
+      d->qM[i][j] += v;
+      if (j != i) d->qM[j][i] += v;
+    }
+  }
+}
+
 void so100o_fwd_position(const so100_model* m, so100o_data* d) {
   kinematics(m, d);
   com_pos(m, d);
   crb(m, d);
+  if (m->ee) weld_fold(m, d);
+  else memset(d->weld_f, 0, sizeof(d->weld_f));
   factor_m(d);
   collision(m, d);
   make_constraint(m, d);
@@ -1615,7 +1707,7 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   }
   /* [3P] mj_fwdAcceleration: qacc_smooth = M^-1 (qfrc_actuator - qfrc_bias) (no passive forces) */
   real rhs[NV];
-  for (int k = 0; k < NV; k++) rhs[k] = d->qfrc_actuator[k] - d->qfrc_bias[k];
+  for (int k = 0; k < NV; k++) rhs[k] = d->qfrc_actuator[k] - d->qfrc_bias[k] + d->weld_f[k];
   solve_m(d, d->qacc_smooth, rhs);
   const int nefc = d->nefc;
   if (nefc == 0) { memcpy(d->qacc, d->qacc_smooth, sizeof(d->qacc)); d->solver_iter = 0; return; }
@@ -1689,9 +1781,11 @@ void so100o_substep(const so100_model* m, so100o_data* d) {
 
 /* ============================================================== env layer */
 /* SO100CubeToBinTask.initialize_episode (single_arm.py:299-309) inside physics.reset_context():
- * mj_resetData (qvel = 0, warmstart = 0) then qpos[:6] = start pose, ctrl = start pose, cube pose. */
+ * mj_resetData (qvel = 0, warmstart = 0, mocap pose = the mocap body's) then qpos[:6] = start pose, ctrl = start pose, cube pose. */
 void so100o_reset(const so100_model* m, so100o_data* d, const double box_pose[7]) {
   memset(d, 0, sizeof(*d));
+  load3(d->mocap_pos, m->mocap_pos0);                       /* mj_resetData: mocap = the body's pose */
+  load4(d->mocap_quat, m->mocap_quat0);
   for (int k = 0; k < 6; k++) { d->qpos[k] = (real)m->start_qpos[k]; d->ctrl[k] = (real)m->start_qpos[k]; }
   for (int k = 0; k < 7; k++) d->qpos[6 + k] = (real)box_pose[k];
   so100o_fwd_position(m, d);

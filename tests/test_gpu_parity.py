@@ -73,9 +73,18 @@ def test_reset_obs_matches_oracle(venv, model, oracle64):
 
 
 # ----------------------------------------------------------------------------- physics, teacher-forced
-def _teacher_forced(venv, model, oracle, steps, seed):
+def _set_mocap(d, mocap):
+    for k in range(3):
+        d.mocap_pos[k] = float(mocap[k])
+    for k in range(4):
+        d.mocap_quat[k] = float(mocap[3 + k])
+
+
+def _teacher_forced(venv, model, oracle, steps, seed, mocap=None):
     n = venv.num_envs
     venv.reset(seed=seed)
+    if mocap is not None:
+        venv.set_mocap(mocap[:, :3], mocap[:, 3:])
     rng = np.random.default_rng(seed)
     d = oracle.new_data()
     qp_err, qv_err, rew_bad, bit_bad = [], [], 0, 0
@@ -92,22 +101,28 @@ def _teacher_forced(venv, model, oracle, steps, seed):
         gr, gb = rew.cpu().numpy(), info["contact_bits"].cpu().numpy().astype(np.uint32)
         for i in range(n):
             oracle.set_state(d, qpos[i], qvel[i], warm[i])
+            if mocap is not None:
+                _set_mocap(d, mocap[i])
             _, r, _ = oracle.env_step(model, d, 0, act[i])
             oq, ov, _, _ = oracle.get_state(d)
             qp_err.append(np.abs(oq - gq[i]).max())
             qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
             rew_bad += abs(r - gr[i]) > 1e-6
             bit_bad += oracle.contact_bits(d) != gb[i]
-            states.append((qpos[i], qvel[i], warm[i], act[i]))
+            states.append((qpos[i], qvel[i], warm[i], act[i]) + ((mocap[i],) if mocap is not None else ()))
     return np.array(qp_err), np.array(qv_err), rew_bad, bit_bad, states
 
 
 def _oracle_precision_floor(model, o64, o32, states):
     d64, d32 = o64.new_data(), o32.new_data()
     qp, qv = [], []
-    for qpos, qvel, warm, act in states:
+    for st in states:
+        qpos, qvel, warm, act = st[:4]
         o64.set_state(d64, qpos, qvel, warm)
         o32.set_state(d32, qpos, qvel, warm)
+        if len(st) > 4:
+            _set_mocap(d64, st[4])
+            _set_mocap(d32, st[4])
         o64.env_step(model, d64, 0, act)
         o32.env_step(model, d32, 0, act)
         a, b = o64.get_state(d64), o32.get_state(d32)
@@ -678,3 +693,39 @@ def test_step_graph_replay_matches_eager(monkeypatch):
         torch.cuda.synchronize()
         for name in ("qpos", "qvel", "qacc_warmstart", "obs", "reward", "terminated", "truncated", "elapsed", "episode"):
             assert torch.equal(getattr(eager, name), getattr(graph, name)), (t, name)
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_ee_weld_parity(solver, oracle64, oracle32):
+    """EE / mocap variant (so100_transfer_cube_ee.xml): per-env mocap targets within 4 cm and
+    0.4 rad of the end effector's start frame; teacher-forced against the fp64 oracle, fp32-oracle bars."""
+    from scipy.spatial.transform import Rotation
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import build_model
+    model = build_model(solver=solver, variant="ee")
+    n = 32
+    venv = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, solver=solver, variant="ee")
+    venv.reset(seed=77)
+    torch.cuda.synchronize()
+    d = oracle64.new_data()
+    q0 = venv.qpos.cpu().numpy().astype(np.float64)
+    rng = np.random.default_rng(5)
+    mocap = np.zeros((n, 7))
+    for i in range(n):
+        oracle64.set_state(d, q0[i], np.zeros(12), np.zeros(12))
+        oracle64.call("so100o_fwd_position", model, d)
+        R = np.array(d.xmat[6][:]).reshape(3, 3)
+        rot = Rotation.from_rotvec(rng.uniform(-0.4, 0.4, 3)) * Rotation.from_matrix(R)
+        mocap[i, :3] = np.array(d.site_ee[:]) + rng.uniform(-0.04, 0.04, 3)
+        mocap[i, 3:] = rot.as_quat()[[3, 0, 1, 2]]
+    qp, qv, rew_bad, bit_bad, states = _teacher_forced(venv, model, oracle64, steps=30, seed=77, mocap=mocap)
+    ee_gap = np.linalg.norm(venv.obs[:, 6:9].cpu().numpy() - mocap[:, :3], axis=1)
+    venv.close()
+    fqp, fqv = _oracle_precision_floor(model, oracle64, oracle32, states)
+    print(f"\n[ee {solver}] qvel rel median {np.median(qv):.2e} p90 {np.quantile(qv, .9):.2e} max {qv.max():.2e}"
+          f" (fp32 floor median {np.median(fqv):.2e} p90 {np.quantile(fqv, .9):.2e} max {fqv.max():.2e});"
+          f" ee-target gap after 30 steps: median {np.median(ee_gap):.3f} m")
+    assert np.median(qp) <= 1e-5 and np.median(qv) <= 1e-5
+    assert np.quantile(qv, 0.9) <= 2 * np.quantile(fqv, 0.9) + 1e-4
+    assert qv.max() <= 2 * fqv.max() + 1e-3
+    assert np.median(ee_gap) < 0.04

@@ -145,3 +145,29 @@ def test_reference_observation_shapes():
     obs, r, term, trunc, info = g.step(np.zeros(6, np.float32))
     assert obs["observation"].shape == (32 * 24 * 3 + 6,)
     assert g.observation_space["observation"].shape == (32 * 24 * 3 + 6,)
+
+
+def test_demo_recorder_reference_layout(tmp_path):
+    """Episodes recorded from 4 GPU envs in the reference's expert-demonstration layout
+    (record_teleop.py:163-184): per step the observation the step returned, channel-first pixels."""
+    from gym_so100.demos import DemoRecorder, load_demonstrations, lerobot_frames
+    env = SO100VecEnv(4, obs_type="so100_pixels_agent_pos", observation_width=64, observation_height=48,
+                      max_episode_steps=6)
+    rec = DemoRecorder(env, env_ids=[0, 2], max_episodes=3)
+    env.reset(seed=0)
+    g = torch.Generator().manual_seed(0)
+    for t in range(14):
+        act = torch.rand(4, 6, generator=g) * 2 - 1
+        obs, r, term, trunc, info = env.step(act)
+        rec.add(act, obs, r, term, trunc, info)
+    assert len(rec.demonstrations) == 3 and rec.done
+    ep = rec.demonstrations[0]
+    assert len(ep["observations"]) == len(ep["actions"]) == len(ep["rewards"]) == len(ep["infos"]) == 6
+    o = ep["observations"][0]
+    assert o["pixels"].shape == (1, 3, 48, 64) and o["pixels"].dtype == np.uint8
+    assert o["agent_pos"].shape == (1, 6) and o["agent_pos"].dtype == np.float32
+    assert ep["infos"][-1][0].get("TimeLimit.truncated") is True
+    path = rec.save(str(tmp_path / "expert_demonstrations.pkl"))
+    back = load_demonstrations(path)
+    np.testing.assert_array_equal(back[1]["observations"][3]["pixels"], rec.demonstrations[1]["observations"][3]["pixels"])
+    assert len(lerobot_frames(back[0])) == 6
