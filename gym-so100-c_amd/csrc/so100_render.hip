@@ -44,7 +44,8 @@ struct RenderArgs {
   uint8_t* out;                         // [n][height][width][3]
 };
 
-DEV uint32_t shade(const RenderArgs& a, const float* p0, const float* p1, const float* p2, uint32_t rgb) {
+DEV uint32_t shade(const RenderArgs& a, const float* cm, const float* p0, const float* p1, const float* p2,
+                   uint32_t rgb) {
   float e1[3], e2[3], nrm[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) { e1[k] = p1[k] - p0[k]; e2[k] = p2[k] - p0[k]; }
@@ -57,7 +58,7 @@ DEV uint32_t shade(const RenderArgs& a, const float* p0, const float* p1, const 
   float v[3] = {a.cam.pos[0] - p0[0], a.cam.pos[1] - p0[1], a.cam.pos[2] - p0[2]};
   if (dot3(nrm, v) < 0.f) { nrm[0] = -nrm[0]; nrm[1] = -nrm[1]; nrm[2] = -nrm[2]; }
   // headlight: along the view direction (camera -z), so its diffuse term is n . z_cam
-  const float zc[3] = {a.cam.mat[2], a.cam.mat[5], a.cam.mat[8]};
+  const float zc[3] = {cm[2], cm[5], cm[8]};
   float lum = a.cam.head_ambient + a.cam.head_diffuse * fmaxf(0.f, dot3(nrm, zc));
   for (int l = 0; l < a.cam.nlight; l++) lum += a.cam.light_diffuse[l] * fmaxf(0.f, -dot3(nrm, a.cam.light_dir[l]));
   uint32_t out = 0;
@@ -76,6 +77,7 @@ __global__ void __launch_bounds__(kRenderThreads) so100_render_kernel(RenderArgs
   __shared__ unsigned long long zb[kTilePx];
   __shared__ int big[kBigCap];
   __shared__ int nbig;
+  __shared__ float cmat[9];                        // camera frame (columns x, y, z) for this env
   const DevModel* __restrict__ m = a.m;
   const int tid = threadIdx.x, env = blockIdx.x;
   if (env >= a.n || (a.mask && !a.mask[env])) return;     // uniform per block
@@ -104,6 +106,22 @@ __global__ void __launch_bounds__(kRenderThreads) so100_render_kernel(RenderArgs
       }
       for (int k = 0; k < 9; k++) frm[b][k] = R[k];
       for (int k = 0; k < 3; k++) frm[b][9 + k] = P[k];
+    }
+    if (a.cam.track) {
+      // mode="targetbody" on the ee body (scene_so100.xml:30 front_close -> vx300s_left/camera_focus, whose
+      // origin is ee_site): MuJoCo's mj_camlight frame z = pos - target, x = (0,0,1) x z, y = z x x
+      float z[3] = {a.cam.pos[0] - sh.site_ee[0], a.cam.pos[1] - sh.site_ee[1], a.cam.pos[2] - sh.site_ee[2]};
+      float x[3], y[3];
+      const float up[3] = {0.f, 0.f, 1.f};
+      float n = sqrtf(dot3(z, z));
+      if (n < 1e-15f) { z[0] = 1.f; z[1] = z[2] = 0.f; } else { z[0] /= n; z[1] /= n; z[2] /= n; }
+      cross3(x, up, z);
+      n = sqrtf(dot3(x, x));
+      if (n < 1e-15f) { x[0] = 1.f; x[1] = x[2] = 0.f; } else { x[0] /= n; x[1] /= n; x[2] /= n; }
+      cross3(y, z, x);
+      for (int k = 0; k < 3; k++) { cmat[3 * k] = x[k]; cmat[3 * k + 1] = y[k]; cmat[3 * k + 2] = z[k]; }
+    } else {
+      for (int k = 0; k < 9; k++) cmat[k] = a.cam.mat[k];
     }
   }
   __syncthreads();
@@ -135,9 +153,9 @@ __global__ void __launch_bounds__(kRenderThreads) so100_render_kernel(RenderArgs
         w[1] = R[3] * q.x + R[4] * q.y + R[5] * q.z + R[10];
         w[2] = R[6] * q.x + R[7] * q.y + R[8] * q.z + R[11];
         const float d[3] = {w[0] - a.cam.pos[0], w[1] - a.cam.pos[1], w[2] - a.cam.pos[2]};
-        const float cx = a.cam.mat[0] * d[0] + a.cam.mat[3] * d[1] + a.cam.mat[6] * d[2];
-        const float cy = a.cam.mat[1] * d[0] + a.cam.mat[4] * d[1] + a.cam.mat[7] * d[2];
-        const float cz = a.cam.mat[2] * d[0] + a.cam.mat[5] * d[1] + a.cam.mat[8] * d[2];
+        const float cx = cmat[0] * d[0] + cmat[3] * d[1] + cmat[6] * d[2];
+        const float cy = cmat[1] * d[0] + cmat[4] * d[1] + cmat[7] * d[2];
+        const float cz = cmat[2] * d[0] + cmat[5] * d[1] + cmat[8] * d[2];
         const float depth = -cz;
         ok = ok && depth > a.cam.znear;
         const float id = 1.f / depth;
@@ -155,7 +173,7 @@ __global__ void __launch_bounds__(kRenderThreads) so100_render_kernel(RenderArgs
       by0 = max(y0, (int)floorf(fminf(sy[0], fminf(sy[1], sy[2])) - 0.5f));
       by1 = min(y1 - 1, (int)ceilf(fmaxf(sy[0], fmaxf(sy[1], sy[2])) - 0.5f));
       if (bx0 > bx1 || by0 > by1) return false;
-      col = shade(a, pw[0], pw[1], pw[2], a.tri_rgb[t]);
+      col = shade(a, cmat, pw[0], pw[1], pw[2], a.tri_rgb[t]);
       return true;
     };
     // one pixel of a set-up triangle: edge functions at the pixel centre, perspective-correct depth

@@ -30,7 +30,8 @@ SO100_MAX_LIGHTS = 4
 
 class SO100Camera(ctypes.Structure):
     """Mirror of ``so100_camera`` (include/so100.h): pose, fovy, headlight and directional lights."""
-    _fields_ = [("pos", ctypes.c_float * 3), ("mat", ctypes.c_float * 9), ("fovy", ctypes.c_float),
+    _fields_ = [("pos", ctypes.c_float * 3), ("mat", ctypes.c_float * 9), ("track", ctypes.c_int),
+                ("fovy", ctypes.c_float),
                 ("znear", ctypes.c_float), ("head_ambient", ctypes.c_float), ("head_diffuse", ctypes.c_float),
                 ("nlight", ctypes.c_int), ("light_dir", (ctypes.c_float * 3) * SO100_MAX_LIGHTS),
                 ("light_diffuse", ctypes.c_float * SO100_MAX_LIGHTS)]

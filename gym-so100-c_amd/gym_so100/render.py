@@ -18,7 +18,8 @@ import numpy as np
 from . import _native
 
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so100_render.npz")
-CAMERAS = ("top", "angle", "left_pillar", "right_pillar")
+CAMERAS = ("top", "angle", "left_pillar", "right_pillar", "front_close")
+TRACKING = ("front_close",)              # mode="targetbody" on the ee body: frame per env
 ZNEAR = 0.01
 
 
@@ -39,6 +40,7 @@ def make_camera(scene, name="top"):
     cam = _native.SO100Camera()
     cam.pos[:] = [float(x) for x in scene[f"cam_{name}_pos"]]
     cam.mat[:] = [float(x) for x in scene[f"cam_{name}_mat"].reshape(-1)]
+    cam.track = 1 if name in TRACKING else 0
     cam.fovy = float(scene["fovy"])
     cam.znear = ZNEAR
     cam.head_ambient, cam.head_diffuse = (float(x) for x in scene["head"])

@@ -73,13 +73,15 @@ def box_tris(center, half):
     return np.array(out)
 
 
-# scene_so100.xml:7-30: headlight, the three directional lights and the cameras (all mode="targetbody"
-# on the static table body at (0, .6, 0); front_close targets a body the model does not have)
+# scene_so100.xml:7-30: headlight, the three directional lights and the cameras (mode="targetbody" on the
+# static table body at (0, .6, 0); front_close tracks vx300s_left/camera_focus, the ee_site body, so its
+# frame is computed per env in the kernel)
 HEADLIGHT = dict(ambient=0.4, diffuse=0.4)            # ambient from :9; diffuse MuJoCo's default 0.4
 LIGHTS = [((1, 1, -1), 0.3), ((-1, 1, -1), 0.3), ((0, -1, -1), 0.3)]
 CAMERAS = {"top": (0, 0.6, 0.8), "angle": (0, 0, 0.6), "left_pillar": (-0.5, 0.2, 0.6),
            "right_pillar": (0.5, 0.2, 0.6)}
 CAMERA_TARGET = (0.0, 0.6, 0.0)
+FRONT_CLOSE = (0.0, 0.2, 0.4)
 FOVY = 78.0
 
 
@@ -133,6 +135,8 @@ def main():
     for name, pos in CAMERAS.items():
         cams["cam_" + name + "_pos"] = np.asarray(pos, np.float32)
         cams["cam_" + name + "_mat"] = targetbody_frame(pos, CAMERA_TARGET).astype(np.float32)
+    cams["cam_front_close_pos"] = np.asarray(FRONT_CLOSE, np.float32)
+    cams["cam_front_close_mat"] = np.eye(3, dtype=np.float32)          # unused: tracked per env
     np.savez_compressed(OUT, tri=tris, body=np.array(body, np.int32), rgb=np.array(rgb, np.float32),
                         fovy=np.float32(FOVY), head=np.array([HEADLIGHT["ambient"], HEADLIGHT["diffuse"]], np.float32),
                         light_dir=np.array([normalize(np.asarray(d, float)) for d, _ in LIGHTS], np.float32),

@@ -124,6 +124,7 @@ int so100_contact_count(so100_env* env, uint64_t* accum, void* stream);
 typedef struct so100_camera {
   float pos[3];                     /* camera position (world) */
   float mat[9];                     /* row-major rotation; columns = camera x (right), y (up), z (backward) */
+  int   track;                      /* 1: mode="targetbody" on the ee body, frame recomputed per env (mat unused) */
   float fovy;                       /* vertical field of view, degrees */
   float znear;                      /* triangles with a vertex nearer than this are not drawn */
   float head_ambient, head_diffuse; /* headlight (scene_so100.xml:9) */

@@ -34,8 +34,22 @@ def shade(cam, p, rgb8):
     return q[:, 0] | (q[:, 1] << 8) | (q[:, 2] << 16)
 
 
-def render(scene_tri, scene_body, scene_rgb, frames, cam, width, height):
-    """frames: [NBODY] of (R [3,3], p [3]) world frames; returns uint8 [H, W, 3]."""
+def tracking_frame(pos, target):
+    """MuJoCo's targetbody camera frame (mj_camlight): z = pos - target, x = (0,0,1) x z, y = z x x."""
+    z = np.asarray(pos, float) - np.asarray(target, float)
+    n = np.linalg.norm(z)
+    z = z / n if n > 1e-15 else np.array([1.0, 0, 0])
+    x = np.cross([0.0, 0.0, 1.0], z)
+    n = np.linalg.norm(x)
+    x = x / n if n > 1e-15 else np.array([1.0, 0, 0])
+    return np.stack([x, np.cross(z, x), z], axis=1)
+
+
+def render(scene_tri, scene_body, scene_rgb, frames, cam, width, height, target=None):
+    """frames: [NBODY] of (R [3,3], p [3]) world frames; target: the tracked point (ee_site) of a
+    tracking camera; returns uint8 [H, W, 3]."""
+    if cam.get("track"):
+        cam = dict(cam, mat=tracking_frame(cam["pos"], target))
     R = np.stack([f[0] for f in frames])[scene_body]                   # [T,3,3]
     P = np.stack([f[1] for f in frames])[scene_body]                   # [T,3]
     w = np.einsum("tij,tvj->tvi", R, scene_tri.astype(np.float64)) + P[:, None, :]
@@ -78,7 +92,7 @@ def render(scene_tri, scene_body, scene_rgb, frames, cam, width, height):
 def camera_dict(cam_struct):
     """so100_camera ctypes struct -> numpy dict for render()."""
     return {"pos": np.array(cam_struct.pos[:], np.float64),
-            "mat": np.array(cam_struct.mat[:], np.float64).reshape(3, 3),
+            "mat": np.array(cam_struct.mat[:], np.float64).reshape(3, 3), "track": int(cam_struct.track),
             "fovy": float(cam_struct.fovy), "znear": float(cam_struct.znear),
             "head_ambient": float(cam_struct.head_ambient), "head_diffuse": float(cam_struct.head_diffuse),
             "light_dir": [np.array(cam_struct.light_dir[i][:], np.float64) for i in range(cam_struct.nlight)],

@@ -171,3 +171,26 @@ def test_demo_recorder_reference_layout(tmp_path):
     back = load_demonstrations(path)
     np.testing.assert_array_equal(back[1]["observations"][3]["pixels"], rec.demonstrations[1]["observations"][3]["pixels"])
     assert len(lerobot_frames(back[0])) == 6
+
+
+def test_tracking_camera_matches_numpy_rasteriser(model, oracle64):
+    """front_close: the camera frame follows each env's end effector (computed in the kernel)."""
+    W, H, N = 96, 72, 4
+    env = SO100VecEnv(N, obs_type="so100_pixels_agent_pos", observation_width=W, observation_height=H,
+                      autoreset=False, max_episode_steps=0)
+    rollout(env, 15, seed=9)
+    cam_r = R.CameraRenderer(env, W, H, camera="front_close")
+    img = cam_r.render().cpu().numpy()
+    qpos = env.qpos.cpu().numpy().astype(np.float64)
+    scene = R.load_scene()
+    cam = render_ref.camera_dict(cam_r.camera)
+    for i in range(N):
+        fr = frames_of(oracle64, model, qpos[i])
+        d = oracle64.new_data()
+        oracle64.reset(model, d, np.array(qpos[i][6:13]))
+        for k in range(6):
+            d.qpos[k] = qpos[i][k]
+        oracle64.call("so100o_fwd_position", model, d)
+        ref = render_ref.render(scene["tri"], scene["body"], scene["rgb"], fr, cam, W, H, target=np.array(d.site_ee[:]))
+        diff = np.any(img[i] != ref, axis=-1)
+        assert diff.mean() < 0.01, (i, diff.sum())

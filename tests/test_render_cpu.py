@@ -45,7 +45,7 @@ def test_scene_asset(scene):
     assert np.all(body[np.all(rgb == [1, 0, 0], axis=1)] == 8)
 
 
-@pytest.mark.parametrize("name", R.CAMERAS)
+@pytest.mark.parametrize("name", [c for c in R.CAMERAS if c not in R.TRACKING])
 def test_targetbody_cameras(scene, name):
     pos, mat = scene[f"cam_{name}_pos"].astype(float), scene[f"cam_{name}_mat"].astype(float)
     np.testing.assert_allclose(mat.T @ mat, np.eye(3), atol=1e-6)
@@ -91,3 +91,23 @@ def test_numpy_rasteriser_depth_order(scene, model, oracle64):
     u, v = project(cam, (c[0], c[1], 0.0), W, H)
     np.testing.assert_array_equal(above[v, u], [255, 0, 0])
     assert below[v, u][0] == below[v, u][1] == below[v, u][2] > 0
+
+
+def test_tracking_camera_looks_at_the_end_effector(scene, model, oracle64):
+    """front_close (scene_so100.xml:30) targets vx300s_left/camera_focus, whose origin is ee_site: the
+    end effector projects to the image centre whatever the arm pose."""
+    cam = render_ref.camera_dict(R.make_camera(scene, "front_close"))
+    assert cam["track"] == 1
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        arm = rng.uniform(-0.8, 0.8, 6)
+        d = oracle64.new_data()
+        oracle64.reset(model, d, np.array([-0.2, 0.45, 0.01, 1, 0, 0, 0]))
+        for k in range(6):
+            d.qpos[k] = arm[k]
+        oracle64.call("so100o_fwd_position", model, d)
+        ee = np.array(d.site_ee[:])
+        mat = render_ref.tracking_frame(cam["pos"], ee)
+        np.testing.assert_allclose(mat.T @ mat, np.eye(3), atol=1e-12)
+        u, v = project(dict(cam, mat=mat), ee, 64, 48)
+        assert (u, v) == (32, 24)
