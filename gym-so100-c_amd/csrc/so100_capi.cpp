@@ -274,13 +274,25 @@ int build_device_model(const so100_model* s, DevModel* d) {
     if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
   }
   // hull-hull self-collision pairs: two hulls on different arm links
-  for (int p = SO100_PAIR_SELF0; p < SO100_NPAIR; p++) {
+  for (int p = SO100_PAIR_SELF0; p < SO100_PAIR_PAD0; p++) {
     const int k1 = -1 - s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
     if (k1 < 0 || k1 >= SO100_NHULL || k2 < 0 || k2 >= SO100_NHULL) return fail("model: self pair must be two hulls");
     if (s->pair_body1[p] != s->hull_body[k1] || s->pair_body2[p] != s->hull_body[k2] || k1 == k2)
       return fail("model: self pair bodies");
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: self pairs must have condim 3 or 4");
     if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
+  }
+  // pad pairs: (finger pad i, table) at SO100_PAIR_PAD0 + i, (pad i, bin box j) at SO100_PAIR_PADBIN0 + 5 i + j
+  for (int p = SO100_PAIR_PAD0; p < SO100_NPAIR; p++) {
+    const bool tbl = p < SO100_PAIR_PADBIN0;
+    const int q = p - SO100_PAIR_PADBIN0;
+    const int i = tbl ? p - SO100_PAIR_PAD0 : q / SO100_NBINBOX, j = tbl ? 0 : 1 + q % SO100_NBINBOX;
+    const int g1 = s->pair_geom1[p], g2 = s->pair_geom2[p];
+    if (g1 != 1 + i || g2 != (j == 0 ? 0 : SO100_CUBE_GEOM + j)) return fail("model: pad pair p must be (pad i, table | bin box j)");
+    if (s->geom_body[g1] != 6 && s->geom_body[g1] != 7) return fail("model: pads must sit on the jaws");
+    if (s->geom_body[g2] != 0) return fail("model: table and bin boxes must be static");
+    if (s->pair_body1[p] != s->geom_body[g1] || s->pair_body2[p] != 0) return fail("model: pad pair bodies");
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: pad pairs must have condim 3 or 4");
   }
   for (int g = 0; g < SO100_NGEOM; g++) {
     int b = s->geom_body[g];

@@ -1611,15 +1611,156 @@ DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_
   __syncthreads();
 }
 
+// write one box-box pair's contacts into slots base, base+1, ... (slots >= kMaxCon are dropped, as the
+// oracle's add_contact drops contacts beyond SO100_MAXCON)
+DEV void put_box_contacts(EnvShared& sh, const PairContacts& pc, int base, int p) {
+#pragma unroll
+  for (int c = 0; c < SO100_MAXCONPAIR; c++) {
+    const int slot = base + c;
+    if (c < pc.n && slot < kMaxCon) {
+      float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
+      make_frame(fr);
+#pragma unroll
+      for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
+      sh.con[slot].g.pos[0] = pc.pos[c][0]; sh.con[slot].g.pos[1] = pc.pos[c][1];
+      sh.con[slot].g.pos[2] = pc.pos[c][2]; sh.con[slot].g.pos[3] = pc.dist[c];
+      sh.con_dist[slot] = pc.dist[c];
+      sh.con_pair[slot] = p;
+    }
+  }
+}
+
+// Finger pads vs the table and the bin boxes (oracle collision(): pad_table, collide_box_pair).
+//   pairs 98..105 (pad i, table), lane i: the hull-table rule on the pad's 8 corners — the corners inside
+//     the top face's footprint and below the top count; one contact at the deepest corner's distance, at
+//     the counted corners' x-y centroid, midway in z between the deepest corner and the top; normal -z;
+//   pairs 106..145 (pad i, bin box j): a conservative test (the pad's bounding sphere against the static
+//     box, 3 pairs per lane), the candidates compacted in pair order and run through the box-box
+//     collider 16 at a time (a wave runs as many rounds as its busiest env needs; usually none).
+// Contacts are appended after `tot` in pair order; returns the new total.
+DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, int grp, bool valid, int tot) {
+#ifdef SO100_NO_PADS
+  return tot;                             // A/B diagnostic builds only (tests/_build_variant.sh)
+#endif
+  // ---- pad-table (lanes 0..7)
+  bool tfound = false;
+  float tx = 0.f, ty = 0.f, tz = 0.f;
+  if (valid && lane < SO100_NPAD) {
+    const int p = SO100_PAIR_PAD0 + lane, g = m->pair_g1[p];
+    const int b = m->geom_body[g];
+    const float* bm = sh.jaw_mat[b - 6];
+    const float* gm = m->geom_mat[g];
+    const float top = m->table_top, margin = m->pair_margin[p];
+    // broadphase: the pad's lowest point (centre z minus its half-extent along world z)
+    const float cz = sh.jaw_pos[b - 6][2] + bm[6] * m->geom_pos[g][0] + bm[7] * m->geom_pos[g][1] + bm[8] * m->geom_pos[g][2];
+    float ext = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) ext += fabsf(bm[6] * gm[k] + bm[7] * gm[3 + k] + bm[8] * gm[6 + k]) * m->geom_size[g][k];
+    float sx = 0.f, sy = 0.f, zmin = 0.f;
+    int cnt = 0;
+    if (cz - ext - top < margin + 1e-4f) {
+    float c[3], R[9];
+    geom_pose(m, sh, g, c, R);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float l0 = (k & 1 ? 1.f : -1.f) * m->geom_size[g][0];
+      const float l1 = (k & 2 ? 1.f : -1.f) * m->geom_size[g][1];
+      const float l2 = (k & 4 ? 1.f : -1.f) * m->geom_size[g][2];
+      const float w0 = R[0] * l0 + R[1] * l1 + R[2] * l2 + c[0];
+      const float w1 = R[3] * l0 + R[4] * l1 + R[5] * l2 + c[1];
+      const float w2 = R[6] * l0 + R[7] * l1 + R[8] * l2 + c[2];
+      const bool in = !(w0 < m->table_lo[0] || w0 > m->table_hi[0] || w1 < m->table_lo[1] || w1 > m->table_hi[1]) &&
+                      (w2 - top < margin);
+      if (in) {
+        sx += w0; sy += w1;
+        zmin = (cnt == 0 || w2 < zmin) ? w2 : zmin;
+        cnt++;
+      }
+    }
+    }
+    tfound = cnt > 0;
+    if (tfound) { tx = sx / (float)cnt; ty = sy / (float)cnt; tz = zmin; }
+  }
+  const uint32_t trow = (uint32_t)((__ballot(tfound) >> (grp * 16)) & 0xFFull);
+  {
+    const int slot = tot + __popc(trow & ((1u << lane) - 1u));
+    if (tfound && slot < kMaxCon) {
+      float fr[9] = {0.f, 0.f, -1.f, 0, 0, 0, 0, 0, 0};
+      make_frame(fr);
+#pragma unroll
+      for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
+      const float top = m->table_top;
+      sh.con[slot].g.pos[0] = tx; sh.con[slot].g.pos[1] = ty;
+      sh.con[slot].g.pos[2] = 0.5f * (tz + top); sh.con[slot].g.pos[3] = tz - top;
+      sh.con_dist[slot] = tz - top;
+      sh.con_pair[slot] = SO100_PAIR_PAD0 + lane;
+    }
+  }
+  tot += __popc(trow);
+  // ---- pad-bin candidates (3 pairs per lane)
+  uint64_t cm = 0ull;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int q = r * kLanes + lane;
+    bool cand = false;
+    if (valid && q < SO100_NPAIR_PADBIN) {
+      const int p = SO100_PAIR_PADBIN0 + q;
+      const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];   // g1: a pad on a jaw; g2: static
+      const int b = m->geom_body[g1];
+      const float* bp = sh.jaw_pos[b - 6];
+      const float* bm = sh.jaw_mat[b - 6];
+      float t[3];
+      mulmv3(t, bm, m->geom_pos[g1]);
+      // the pad's bounding sphere against the static box itself: the distance from the pad centre to
+      // the box, in the box frame
+      const float w[3] = {bp[0] + t[0] - m->geom_pos[g2][0], bp[1] + t[1] - m->geom_pos[g2][1],
+                          bp[2] + t[2] - m->geom_pos[g2][2]};
+      const float* R2 = m->geom_mat[g2];
+      float ex2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const float u = fabsf(R2[k] * w[0] + R2[3 + k] * w[1] + R2[6 + k] * w[2]) - m->geom_size[g2][k];
+        ex2 += u > 0.f ? u * u : 0.f;
+      }
+      const float rr = m->geom_rbound[g1] + m->pair_margin[p];
+      cand = ex2 <= rr * rr;
+    }
+    cm |= ((__ballot(cand) >> (grp * 16)) & 0xFFFFull) << (16 * r);
+  }
+  const int ncand = __popcll(cm);
+  const int rounds = (wave_max_i(ncand) + kLanes - 1) / kLanes;
+  for (int r = 0; r < rounds; r++) {
+    const int idx = r * kLanes + lane;
+    int p = -1;
+    if (idx < ncand) {
+      uint64_t x = cm;
+      for (int k = 0; k < idx; k++) x &= x - 1ull;
+      p = SO100_PAIR_PADBIN0 + __ffsll((unsigned long long)x) - 1;
+    }
+    PairContacts pc;
+    pc.n = 0;
+    if (p >= 0) collide_pair(m, sh, p, pc);
+    sh.cnt[lane] = pc.n;
+    __syncthreads();
+    int off = 0, sum = 0;
+#pragma unroll
+    for (int k = 0; k < kLanes; k++) { const int c = sh.cnt[k]; off += (k < lane) ? c : 0; sum += c; }
+    put_box_contacts(sh, pc, tot + off, p);
+    tot += sum;
+    __syncthreads();
+  }
+  return tot;
+}
+
+#ifndef SO100_STAGE_WAVES
+#define SO100_STAGE_WAVES 3      // waves per SIMD the stage kernel's register budget is sized for
+#endif
 // Substep stage kernel (one wave = 4 envs x 16 lanes).
 //   kMode 0: substep 0 — position/velocity stages and constraint assembly on the stored state;
 //   kMode 1: Euler with the previous substep's solver output, then the same assembly;
 //   kMode 2: Euler, then the mj_step1 position stage and the task epilogue (reward, obs, autoreset).
 // Assembly writes the solver's per-env record (Workspace) that so100_pgs_kernel consumes.
 template <int kMode, int kSolver>
-#ifndef SO100_STAGE_WAVES
-#define SO100_STAGE_WAVES 3      // waves per SIMD the stage kernel's register budget is sized for
-#endif
 __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kernel(StageArgs args) {
   __shared__ EnvShared shm[kEnvsPerBlock];
   const DevModel* __restrict__ m = args.m;
@@ -1704,20 +1845,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
       int off = 0, tot = 0;
 #pragma unroll
       for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
-#pragma unroll
-      for (int c = 0; c < SO100_MAXCONPAIR; c++) {
-        int slot = off + c;
-        if (c < pc.n && slot < kMaxCon) {
-          float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
-          make_frame(fr);
-#pragma unroll
-          for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
-          sh.con[slot].g.pos[0] = pc.pos[c][0]; sh.con[slot].g.pos[1] = pc.pos[c][1];
-          sh.con[slot].g.pos[2] = pc.pos[c][2]; sh.con[slot].g.pos[3] = pc.dist[c];
-          sh.con_dist[slot] = pc.dist[c];
-          sh.con_pair[slot] = lane;
-        }
-      }
+      put_box_contacts(sh, pc, off, lane);
       const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
       if (hfound && hslot < kMaxCon) {
         float fr[9] = {0.f, 0.f, 1.f, 0, 0, 0, 0, 0, 0};
@@ -1744,6 +1872,8 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
         sh.con_pair[mslot] = __float_as_int(st.nrm[3]);
       }
       tot += nmpr;
+      __syncthreads();
+      tot = pad_contacts(m, sh, lane, grp, valid, tot);
       if (lane == 0) sh.ncon = tot < kMaxCon ? tot : kMaxCon;
     }
     __syncthreads();

@@ -20,7 +20,10 @@ NPAIR_BOX, NHULL, HULL_NVERT, NBINBOX = 14, 9, 2560, 5
 PAIR_MPR0 = NPAIR_BOX + NHULL                  # (box, hull) pairs of the MPR convex collider start here
 PAIR_SELF0 = PAIR_MPR0 + (1 + NBINBOX) * NHULL  # 77: hull-hull self-collision pairs
 NPAIR_SELF = 21
-NPAIR = PAIR_SELF0 + NPAIR_SELF                  # 98
+PAIR_PAD0 = PAIR_SELF0 + NPAIR_SELF              # 98: (pad i, table) pairs 98..105
+PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 106: (pad i, bin box j) at 106 + 5 i + j, box-box
+NPAIR_PAD = 8 * (1 + NBINBOX)                    # 48
+NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 146
 NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
 MAXCON, CONDIM, NOBS = 16, 4, 15
 NEFC_MAX = NV + NHINGE + MAXCON * CONDIM

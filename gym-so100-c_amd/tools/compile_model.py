@@ -428,6 +428,20 @@ def compile_model():
             pairs.append(dict(g1=-1 - k1, g2=-1 - k2, body1=b1, body2=b2, name1=h1["name"], name2=h2["name"],
                               hull=k2, hull1=k1, **mixed(h1, h2)))
 
+    # Pairs 98..105: the 8 finger pads against the table; 106..145: against the 5 bin boxes (106 + 5 i + j).
+    # geom1 = the pad: the table is a mesh (box < mesh) and the bin boxes come after the arm in the model
+    # (so100_transfer_cube.xml includes the arm before the bin), so the normal points from the pad to the
+    # table / bin box.  Pad-table contacts follow the hull-table rule (one per pair); pad-bin pairs are
+    # box-box like the cube's.
+    pads = [f"{side}_jaw_pad_{i}" for side in ("fixed", "moving") for i in range(1, 5)]
+    pad_pairs = ([(n1, "table") for n1 in pads]
+                 + [(n1, n2) for n1 in pads for n2 in ("bin_wall", "bin_wall2", "bin_wall3", "bin_wall4", "bin_floor")])
+    for n1, n2 in pad_pairs:
+        g1, g2 = geoms[gid[n1]], geoms[gid[n2]]
+        pairs.append(dict(g1=gid[n1], g2=gid[n2], body1=g1["body"], body2=g2["body"], name1=n1, name2=n2,
+                          **mixed(g1, g2)))
+    assert len(pairs) == 146
+
     # ---- EE / mocap variant (so100_transfer_cube_ee.xml: the same scene with trs_so_arm100/so_arm100_ee.xml,
     # whose only differences are the mocap body at :155 and the weld equality at :171-173) ----
     ee = ET.parse(os.path.join(ASSETS, "trs_so_arm100", "so_arm100_ee.xml")).getroot()

@@ -37,7 +37,12 @@
 #define SO100_PAIR_SELF0 (SO100_PAIR_MPR0 + SO100_NPAIR_MPR)  /* 77: first hull-hull self-collision pair */
 #define SO100_NPAIR_SELF 21                                 /* hulls on non-adjacent arm links */
 #define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF)  /* 75 pairs through the MPR collider */
-#define SO100_NPAIR (SO100_PAIR_SELF0 + SO100_NPAIR_SELF)   /* 98 */
+#define SO100_PAIR_PAD0 (SO100_PAIR_SELF0 + SO100_NPAIR_SELF)  /* 98: first (pad, table | bin box) pair */
+#define SO100_NPAD 8                                        /* finger pads: geoms 1..8 */
+#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 106: (pad i, bin box j) at 106 + 5 i + j */
+#define SO100_NPAIR_PADBIN (SO100_NPAD * SO100_NBINBOX)     /* 40, box-box */
+#define SO100_NPAIR_PAD (SO100_NPAD + SO100_NPAIR_PADBIN)   /* 48: 98..105 (pad i, table), then pad-bin */
+#define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 146 */
 #define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_CUBE_BODY 8

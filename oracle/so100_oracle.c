@@ -612,7 +612,11 @@ static void make_frame(real f[9]) {
  *     footprint the convex-convex penetration (MuJoCo mjc_Convex, one contact per pair without
  *     multiccd) has the face normal +z, depth = -(lowest vertex z - top), and witness points at that
  *     vertex and its projection on the face: pos = their midpoint.  The lowest vertex is the first in
- *     hull order among ties; vertices outside the top face's x-y footprint are not counted. */
+ *     hull order among ties; vertices outside the top face's x-y footprint are not counted;
+ *   pairs 23..97  (box | hull, hull k) through MPR (below);
+ *   pairs 98..105 (finger pad i, table): pad_table below, one contact per pair;
+ *   pairs 106..145 (finger pad i, bin box j) box-box, like the cube's pairs.  The kernel appends the pad
+ *     contacts after the MPR contacts in the same pair order. */
 static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
   if (d->ncon >= SO100_MAXCON) { d->ncon_dropped++; return; }
   so100o_contact* con = &d->con[d->ncon++];
@@ -894,22 +898,59 @@ static int mpr_broadphase(const mpr_obj* o, const real hb[3], const real hh[3]) 
   return 1;
 }
 
+/* one box-box pair (bounding-sphere broadphase, then box_box); pairs 0..13 and the pad-bin pairs */
+static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
+  int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+  real A[3], B[3];
+  load3(A, m->geom_size[g1]);
+  load3(B, m->geom_size[g2]);
+  real dp[3] = {d->geom_xpos[g2][0] - d->geom_xpos[g1][0], d->geom_xpos[g2][1] - d->geom_xpos[g1][1],
+                d->geom_xpos[g2][2] - d->geom_xpos[g1][2]};
+  real margin = (real)m->pair_margin[p];
+  if (norm3(dp) > norm3(A) + norm3(B) + margin) return;
+  so100o_contact tmp[SO100_MAXCONPAIR];
+  int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin, tmp);
+  for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
+}
+
+/* (pad i, table), pairs 98..105: the hull-table rule applied to the pad's 8 corners (corner k: signs of
+ * the half sizes from bits 0, 1, 2 of k, minus first).  The corners inside the top face's x-y footprint
+ * and below the top (+ margin) count; one contact (MuJoCo collides the table mesh through its convex
+ * collider, one contact per pair) at the deepest corner's distance, positioned at the counted corners'
+ * x-y centroid (the face centre when a pad lies flat, where the corners' depths tie) and midway in z
+ * between the deepest corner and the top.  Normal from the pad (geom1) into the table: -z. */
+static void pad_table(const so100_model* m, so100o_data* d, int p) {
+  const int g = m->pair_geom1[p];
+  const real top = (real)m->table_top, margin = (real)m->pair_margin[p];
+  const real lo0 = (real)m->table_lo[0], lo1 = (real)m->table_lo[1];
+  const real hi0 = (real)m->table_hi[0], hi1 = (real)m->table_hi[1];
+  real sx = 0, sy = 0, zmin = 0;
+  int cnt = 0;
+  for (int k = 0; k < 8; k++) {
+    real l[3], w[3];
+    for (int t = 0; t < 3; t++) l[t] = ((k >> t) & 1 ? (real)1 : (real)-1) * (real)m->geom_size[g][t];
+    mulmv3(w, d->geom_xmat[g], l);
+    for (int t = 0; t < 3; t++) w[t] += d->geom_xpos[g][t];
+    if (w[0] < lo0 || w[0] > hi0 || w[1] < lo1 || w[1] > hi1) continue;
+    if (!(w[2] - top < margin)) continue;
+    sx += w[0];
+    sy += w[1];
+    if (cnt == 0 || w[2] < zmin) zmin = w[2];
+    cnt++;
+  }
+  if (cnt == 0) return;
+  so100o_contact con;
+  memset(&con, 0, sizeof(con));
+  con.pos[0] = sx / (real)cnt; con.pos[1] = sy / (real)cnt; con.pos[2] = (real)0.5 * (zmin + top);
+  con.frame[0] = 0; con.frame[1] = 0; con.frame[2] = -1;
+  con.dist = zmin - top;
+  add_contact(d, &con, p);
+}
+
 static void collision(const so100_model* m, so100o_data* d) {
   d->ncon = 0;
   d->ncon_dropped = 0;
-  for (int p = 0; p < SO100_NPAIR_BOX; p++) {
-    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
-    real A[3], B[3];
-    load3(A, m->geom_size[g1]);
-    load3(B, m->geom_size[g2]);
-    real dp[3] = {d->geom_xpos[g2][0] - d->geom_xpos[g1][0], d->geom_xpos[g2][1] - d->geom_xpos[g1][1],
-                  d->geom_xpos[g2][2] - d->geom_xpos[g1][2]};
-    real margin = (real)m->pair_margin[p];
-    if (norm3(dp) > norm3(A) + norm3(B) + margin) continue;
-    so100o_contact tmp[SO100_MAXCONPAIR];
-    int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin, tmp);
-    for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
-  }
+  for (int p = 0; p < SO100_NPAIR_BOX; p++) collide_box_pair(m, d, p);
   const real top = (real)m->table_top;
   const real lo0 = (real)m->table_lo[0], lo1 = (real)m->table_lo[1];
   const real hi0 = (real)m->table_hi[0], hi1 = (real)m->table_hi[1];
@@ -944,7 +985,7 @@ static void collision(const so100_model* m, so100o_data* d) {
   }
   /* pairs 23..97 through the MPR convex collider, in H = the body frame of hull k (geom2):
    *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links */
-  for (int p = SO100_PAIR_MPR0; p < SO100_NPAIR; p++) {
+  for (int p = SO100_PAIR_MPR0; p < SO100_PAIR_PAD0; p++) {
     const int k = -1 - m->pair_geom2[p], g = m->pair_geom1[p], b = m->hull_body[k];
     const real* RH = d->xmat[b];
     mpr_obj o;
@@ -990,6 +1031,9 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = -depth;
     add_contact(d, &con, p);
   }
+  /* pairs 98..145: the finger pads vs the table (98..105), then vs the bin boxes (box-box) */
+  for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_PADBIN0; p++) pad_table(m, d, p);
+  for (int p = SO100_PAIR_PADBIN0; p < SO100_NPAIR; p++) collide_box_pair(m, d, p);
 }
 
 uint32_t so100o_contact_bits(const so100o_data* d) {

@@ -378,7 +378,7 @@ def test_hull_table_parity(solver, oracle64, oracle32):
     """Arm/jaw hulls resting on the table (pairs 14..22, condim 3): states made by the
     fp64 oracle driving the arm down onto the table, then teacher-forced GPU steps against it."""
     from gym_so100 import SO100VecEnv
-    from gym_so100.model import NPAIR_BOX, build_model
+    from gym_so100.model import NPAIR_BOX, PAIR_MPR0, build_model
     model = build_model(solver=solver)
     n = 24
     rng = np.random.default_rng(11)
@@ -386,7 +386,8 @@ def test_hull_table_parity(solver, oracle64, oracle32):
     states, targets = [], []
     lo, hi = np.array(model.action_lo[:]), np.array(model.action_hi[:])
     for i in range(n):
-        oracle64.reset(model, d, np.array([0.4, 0.95, 0.6, 1, 0, 0, 0]))          # cube out of reach
+        oracle64.reset(model, d, np.array([2.0, 0.95, 0.6, 1, 0, 0, 0]))          # cube off the table: it falls
+        # clear, so no cube resting at dist ~ 0 (its contacts flip between precisions)
         target = np.array([rng.uniform(-0.6, 0.6), rng.uniform(0.6, 1.2), rng.uniform(-1.2, -0.6),
                            rng.uniform(0.8, 1.5), rng.uniform(-1.5, 1.5), rng.uniform(-0.17, 1.0)])
         for k in range(6):
@@ -401,7 +402,7 @@ def test_hull_table_parity(solver, oracle64, oracle32):
     env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
                   np.array([s[2] for s in states], np.float32))
     d64, d32 = oracle64.new_data(), oracle32.new_data()
-    qv_err, qv_floor, hull_con, bit_bad = [], [], [], 0
+    qv_err, qv_floor, hull_con, bit_bad, same = [], [], [], 0, []
     for step in range(4):
         q0 = env.qpos.cpu().numpy().astype(np.float64)
         v0 = env.qvel.cpu().numpy().astype(np.float64)
@@ -414,25 +415,101 @@ def test_hull_table_parity(solver, oracle64, oracle32):
         gb = info["contact_bits"].cpu().numpy().astype(np.uint32)
         for i in range(n):
             pairs = dbg[i, 48:48 + int(dbg[i, 0])]
-            hull_con.append(int((pairs >= NPAIR_BOX).sum()))
+            hull_con.append(int(((pairs >= NPAIR_BOX) & (pairs < PAIR_MPR0)).sum()))
             oracle64.set_state(d64, q0[i], v0[i], w0[i])
             oracle32.set_state(d32, q0[i], v0[i], w0[i])
             oracle64.env_step(model, d64, 0, act[i])
             oracle32.env_step(model, d32, 0, act[i])
+            same.append(sorted(pairs.astype(int).tolist()) == sorted(d64.con[c].pair for c in range(d64.ncon)))
             ov = oracle64.get_state(d64)[1]
             qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
             qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
             bit_bad += oracle64.contact_bits(d64) != gb[i]
-    qv_err, qv_floor, hull_con = np.array(qv_err), np.array(qv_floor), np.array(hull_con)
+    qv_err, qv_floor, hull_con, same = np.array(qv_err), np.array(qv_floor), np.array(hull_con), np.array(same)
     print(f"\n[{solver}] hull-table: GPU hull contacts per env mean {hull_con.mean():.2f} (envs with any: "
           f"{(hull_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
           f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
-          f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e} | contact-bit mismatches {bit_bad}")
+          f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e} | contact-bit mismatches {bit_bad} | "
+          f"contact-set flips {(~same).sum()} of {len(same)} (same-set p90 GPU {np.quantile(qv_err[same], .9):.2e}, "
+          f"floor {np.quantile(qv_floor[same], .9):.2e})")
     assert (hull_con > 0).mean() > 0.5                 # the arm really rests on the table
+    # a contact at dist ~ 0 can be in one precision's set and not the other's; PGS, unconverged at 100
+    # sweeps on resting contacts, amplifies such a flip, so the tail bar applies to the states whose GPU
+    # and oracle contact sets agree, and flips must stay rare
+    assert (~same).mean() <= 0.1
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.quantile(qv_err[same], 0.9) <= 2 * np.quantile(qv_floor[same], 0.9) + 1e-4
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    assert bit_bad <= max(2, 0.05 * len(qv_err))
+    env.close()
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_pad_contact_parity(solver, oracle64, oracle32):
+    """Finger pads against the table and the bin boxes (pairs 98..145, box-box, condim 3):
+    states made by the fp64 oracle pressing the gripper onto the table top (two thirds of the envs) and
+    into the bin (the rest), then teacher-forced GPU steps against it, with the pad contacts counted."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import PAIR_PAD0, build_model
+    model = build_model(solver=solver)
+    n = 24
+    rng = np.random.default_rng(13)
+    d = oracle64.new_data()
+    over_bin = np.array([[0.72, -0.89, 2.15, -1.24, -1.38, -0.05], [0.7, -0.91, 1.85, -0.39, -0.2, 0.33]])
+    states, targets = [], []
+    lo, hi = np.array(model.action_lo[:]), np.array(model.action_hi[:])
+    for i in range(n):
+        oracle64.reset(model, d, np.array([0.4, 0.95, 0.6, 1, 0, 0, 0]))          # cube out of reach
+        if i % 3 < 2:
+            target = np.array([rng.uniform(-0.6, 0.6), rng.uniform(0.2, 1.3), rng.uniform(-1.4, -0.2),
+                               rng.uniform(0.6, 1.6), rng.uniform(-1.5, 1.5), rng.uniform(-0.17, 1.5)])
+        else:
+            target = over_bin[i % 2] + rng.normal(0, 0.12, 6) + np.array([0, 0.15, 0, 0, 0, 0])
+        target = np.clip(target, lo, hi)
+        for k in range(6):
+            d.ctrl[k] = target[k]
+        for _ in range(400):
+            oracle64.call("so100o_substep", model, d)
+        q, v, w, _ = oracle64.get_state(d)
+        states.append((q, v, w))
+        targets.append((target - lo) / (hi - lo) * 2 - 1)      # keep pressing: the same targets as actions
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
+    env.reset(seed=3)
+    env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
+                  np.array([s[2] for s in states], np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, pad_gpu, pad_ora = [], [], [], []
+    for step in range(4):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = (np.array(targets) + rng.normal(0, 0.02, (n, 6))).astype(np.float32)
+        _, _, _, _, info = env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        dbg = env.debug.cpu().numpy()
+        for i in range(n):
+            pairs = dbg[i, 48:48 + int(dbg[i, 0])]
+            pad_gpu.append(int((pairs >= PAIR_PAD0).sum()))
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(model, d64, 0, act[i])
+            oracle32.env_step(model, d32, 0, act[i])
+            pad_ora.append(sum(d64.con[c].pair >= PAIR_PAD0 for c in range(d64.ncon)))
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+    qv_err, qv_floor = np.array(qv_err), np.array(qv_floor)
+    pad_gpu, pad_ora = np.array(pad_gpu), np.array(pad_ora)
+    print(f"\n[{solver}] pads: GPU pad contacts per env mean {pad_gpu.mean():.2f} (envs with any: "
+          f"{(pad_gpu > 0).mean():.2f}; oracle {pad_ora.mean():.2f}, count mismatches {(pad_gpu != pad_ora).sum()}) "
+          f"| qvel rel GPU median {np.median(qv_err):.2e} p90 {np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} "
+          f"| fp32 floor median {np.median(qv_floor):.2e} p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
+    assert (pad_gpu > 0).sum() >= 10                    # the pads really touch the table / bin
+    assert (pad_gpu != pad_ora).mean() <= 0.05           # the same pad contact sets (fp32 flips at dist ~ 0 aside)
     assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
     assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
-    assert bit_bad <= max(2, 0.05 * len(qv_err))
     env.close()
 
 
@@ -442,7 +519,7 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
     arm/jaw hulls): states from fp64-oracle random-action rollouts that hold such
     contacts, then teacher-forced GPU steps against the oracle at the fp32 floor."""
     from gym_so100 import SO100VecEnv
-    from gym_so100.model import PAIR_MPR0, NHULL, build_model
+    from gym_so100.model import PAIR_MPR0, PAIR_PAD0, NHULL, build_model
     model = build_model(solver=solver)
     rng = np.random.default_rng(21)
     d = oracle64.new_data()
@@ -452,7 +529,7 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
         for _ in range(200):
             oracle64.env_step(model, d, 0, rng.uniform(-1, 1, 6).astype(np.float32))
             pairs = [d.con[i].pair for i in range(d.ncon)]
-            mp = [p for p in pairs if p >= PAIR_MPR0]
+            mp = [p for p in pairs if PAIR_MPR0 <= p < PAIR_PAD0]
             if mp and not d.ncon_dropped:
                 q, v, w, _ = oracle64.get_state(d)
                 states.append((q, v, w))
@@ -479,7 +556,7 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
         dbg = env.debug.cpu().numpy()
         for i in range(n):
             pairs = dbg[i, 48:48 + int(dbg[i, 0])]
-            mpr_con.append(int((pairs >= PAIR_MPR0).sum()))
+            mpr_con.append(int(((pairs >= PAIR_MPR0) & (pairs < PAIR_PAD0)).sum()))
             oracle64.set_state(d64, q0[i], v0[i], w0[i])
             oracle32.set_state(d32, q0[i], v0[i], w0[i])
             oracle64.env_step(model, d64, 0, act[i])
@@ -609,7 +686,7 @@ def test_self_collision_parity(solver, oracle64, oracle32):
     """Hull-hull self-collision (pairs 77..97): random arm configurations whose
     non-adjacent links overlap, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
     from gym_so100 import SO100VecEnv
-    from gym_so100.model import PAIR_SELF0, build_model
+    from gym_so100.model import PAIR_SELF0, PAIR_PAD0, build_model
     model = build_model(solver=solver)
     rng = np.random.default_rng(17)
     lo_j = np.array([r[0] for r in model.jnt_range]); hi_j = np.array([r[1] for r in model.jnt_range])
@@ -622,7 +699,7 @@ def test_self_collision_parity(solver, oracle64, oracle32):
         for k in range(6):
             d.qpos[k] = arm[k]
         oracle64.call("so100o_fwd_position", model, d)
-        if any(d.con[i].pair >= PAIR_SELF0 for i in range(d.ncon)) and not d.ncon_dropped:
+        if any(PAIR_SELF0 <= d.con[i].pair < PAIR_PAD0 for i in range(d.ncon)) and not d.ncon_dropped:
             q, v, w, _ = oracle64.get_state(d)
             states.append((q, v * 0, w * 0))
             targets.append(np.clip((arm - lo) / (hi - lo) * 2 - 1, -1, 1))
@@ -644,7 +721,7 @@ def test_self_collision_parity(solver, oracle64, oracle32):
         dbg = env.debug.cpu().numpy()
         for i in range(n):
             pairs = dbg[i, 48:48 + int(dbg[i, 0])]
-            self_con.append(int((pairs >= PAIR_SELF0).sum()))
+            self_con.append(int(((pairs >= PAIR_SELF0) & (pairs < PAIR_PAD0)).sum()))
             oracle64.set_state(d64, q0[i], v0[i], w0[i])
             oracle32.set_state(d32, q0[i], v0[i], w0[i])
             oracle64.env_step(model, d64, 0, act[i])

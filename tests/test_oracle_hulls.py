@@ -94,11 +94,12 @@ def test_hull_contacts_are_condim3_rows_on_arm_dofs(model, oracle64):
 
 def test_contacts_stop_the_arm_at_the_table(model, oracle64):
     """Drive the arm down into the table: with the hull contacts the lowest hull vertex stays within
-    about a centimetre of the top (soft contacts, default solref 0.02, against the actuators' 3.5 N m);
-    with the table moved out of reach it sinks far below."""
+    about a centimetre of the top (soft contacts, default solref 0.02, against the actuators' 3.5 N m),
+    the finger pads' table contacts helping; with the table moved out of reach it sinks far below."""
     hulls = _hulls(model)
     no_table = copy.copy(model)
     no_table.table_top = -10.0
+    no_table.geom_pos[0][2] -= 10.0          # the table geom too (the pads' box-box pairs, 98 + 6 i)
 
     def lowest(d):
         z = []
@@ -121,3 +122,42 @@ def test_contacts_stop_the_arm_at_the_table(model, oracle64):
         runs[name] = zmin
     assert runs["no_table"] < -0.02, runs                      # the target really is below the table
     assert runs["contacts"] > -0.015, runs
+
+
+def test_pad_contacts_match_independent_geometry(model, oracle64):
+    """Finger pads vs the table (pairs 98..105), against an independent numpy statement of
+    the rule: over random arm poses, a pad gets one table contact exactly when one of its 8 corners lies
+    inside the top face's footprint and below the top; distance = the deepest such corner's height, x-y =
+    those corners' centroid, z midway between the deepest corner and the top, normal from the pad
+    (geom1) down into the table."""
+    from gym_so100.model import PAIR_PAD0, PAIR_PADBIN0
+    top = model.table_top
+    lo, hi = np.array(model.table_lo[:]), np.array(model.table_hi[:])
+    jlo = np.array([r[0] for r in model.jnt_range]); jhi = np.array([r[1] for r in model.jnt_range])
+    rng = np.random.default_rng(4)
+    signs = np.array([[1 if k & 1 else -1, 1 if k & 2 else -1, 1 if k & 4 else -1] for k in range(8)], float)
+    touched = 0
+    for _ in range(400):
+        d = _state(oracle64, model, rng.uniform(jlo, jhi))
+        if d.ncon_dropped:
+            continue                         # contact set truncated at SO100_MAXCON: not this test's subject
+        got = {}
+        for i in range(d.ncon):
+            p = d.con[i].pair
+            if PAIR_PAD0 <= p < PAIR_PADBIN0:
+                got.setdefault(p, []).append(d.con[i])
+        for pad in range(8):
+            g = model.pair_geom1[PAIR_PAD0 + pad]
+            R = np.array(d.geom_xmat[g][:]).reshape(3, 3)
+            w = (signs * np.array(model.geom_size[g][:])) @ R.T + np.array(d.geom_xpos[g][:])
+            sel = ((w[:, :2] >= lo) & (w[:, :2] <= hi)).all(1) & (w[:, 2] < top)
+            cons = got.get(PAIR_PAD0 + pad, [])
+            assert len(cons) == int(sel.any()), (pad, len(cons), sel)
+            if not cons:
+                continue
+            touched += 1
+            c, zmin = cons[0], w[sel, 2].min()
+            np.testing.assert_allclose(c.frame[:3], [0, 0, -1], atol=0)
+            assert abs(c.dist - (zmin - top)) < 1e-12
+            np.testing.assert_allclose(c.pos[:], [*w[sel, :2].mean(0), 0.5 * (zmin + top)], atol=1e-12)
+    assert touched >= 20

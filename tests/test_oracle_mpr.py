@@ -15,7 +15,7 @@ import copy
 import numpy as np
 from scipy.spatial import ConvexHull
 
-from gym_so100.model import NHULL, PAIR_MPR0
+from gym_so100.model import NHULL, PAIR_MPR0, PAIR_PAD0
 
 NV = 12
 CUBE_HALF = 0.02
@@ -189,7 +189,7 @@ def test_mpr_contact_rows(model, oracle64):
         oracle64.reset(model, d, oracle64.spawn_pose(1000 + e))
         for _ in range(150):
             oracle64.env_step(model, d, 0, rng.uniform(-1, 1, 6).astype(np.float32))
-            if not any(d.con[i].pair >= PAIR_MPR0 for i in range(d.ncon)):
+            if not any(PAIR_MPR0 <= d.con[i].pair < PAIR_PAD0 for i in range(d.ncon)):
                 continue
             oracle64.call("so100o_fwd_position", model, d)
             oracle64.call("so100o_fwd_velocity", model, d)
@@ -198,7 +198,7 @@ def test_mpr_contact_rows(model, oracle64):
                 if d.efc_type[i] != 2 or d.efc_dim[i] == 0:
                     continue
                 p = d.con[d.efc_id[i]].pair
-                if p < PAIR_MPR0:
+                if not PAIR_MPR0 <= p < PAIR_PAD0:
                     continue
                 cube = p < PAIR_MPR0 + NHULL
                 dim = d.efc_dim[i]
@@ -219,7 +219,7 @@ def _self_configs(model, o, n, seed):
     while len(hit) < n or len(miss) < n:
         arm = rng.uniform(lo, hi)
         d = _state(o, model, arm, (0.4, 0.95, 0.6, 1, 0, 0, 0))
-        pairs = [d.con[i].pair for i in range(d.ncon) if d.con[i].pair >= PAIR_SELF0]
+        pairs = [d.con[i].pair for i in range(d.ncon) if PAIR_SELF0 <= d.con[i].pair < PAIR_PAD0]
         (hit if pairs else miss).append(arm)
     return hit[:n], miss[:n]
 
@@ -229,7 +229,7 @@ def test_self_collision_contacts_are_real_overlaps(model, oracle64):
     intersect (an LP finds a common interior point of their H-representations), with the overlap along the
     normal at least the reported depth; arms whose hulls an LP proves disjoint get no such contact."""
     from scipy.optimize import linprog
-    from gym_so100.model import PAIR_SELF0, NPAIR
+    from gym_so100.model import PAIR_SELF0, PAIR_PAD0
     hit, miss = _self_configs(model, oracle64, 30, seed=8)
 
     def world(d, k):
@@ -250,7 +250,7 @@ def test_self_collision_contacts_are_real_overlaps(model, oracle64):
         d = _state(oracle64, model, arm, (0.4, 0.95, 0.6, 1, 0, 0, 0))
         for i in range(d.ncon):
             p = d.con[i].pair
-            if p < PAIR_SELF0:
+            if not PAIR_SELF0 <= p < PAIR_PAD0:
                 continue
             k1, k2 = -1 - model.pair_geom1[p], -1 - model.pair_geom2[p]
             V1, V2 = world(d, k1), world(d, k2)
@@ -261,7 +261,7 @@ def test_self_collision_contacts_are_real_overlaps(model, oracle64):
     assert checked >= 30
     for arm in miss:
         d = _state(oracle64, model, arm, (0.4, 0.95, 0.6, 1, 0, 0, 0))
-        for p in range(PAIR_SELF0, NPAIR):
+        for p in range(PAIR_SELF0, PAIR_PAD0):
             k1, k2 = -1 - model.pair_geom1[p], -1 - model.pair_geom2[p]
             if model.hull_body[k1] == model.hull_body[k2]:
                 continue
