@@ -366,6 +366,18 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->geom_rbound[g] = (float)sqrt(s->geom_size[g][0] * s->geom_size[g][0] + s->geom_size[g][1] * s->geom_size[g][1] +
                                     s->geom_size[g][2] * s->geom_size[g][2]);
   }
+  for (int k = 0; k < 3; k++) { d->bin_lo[k] = 1e30f; d->bin_hi[k] = -1e30f; }
+  for (int g = SO100_CUBE_GEOM + 1; g < SO100_CUBE_GEOM + 1 + SO100_NBINBOX; g++) {
+    double q[4], gm[9];
+    normq(s->geom_quat[g], q);
+    quat2mat(q, gm);
+    for (int k = 0; k < 3; k++) {
+      const double r = fabs(gm[3 * k]) * s->geom_size[g][0] + fabs(gm[3 * k + 1]) * s->geom_size[g][1] +
+                       fabs(gm[3 * k + 2]) * s->geom_size[g][2];
+      d->bin_lo[k] = fminf(d->bin_lo[k], (float)(s->geom_pos[g][k] - r));
+      d->bin_hi[k] = fmaxf(d->bin_hi[k], (float)(s->geom_pos[g][k] + r));
+    }
+  }
   for (int p = 0; p < SO100_NPAIR; p++) {
     d->pair_g1[p] = s->pair_geom1[p];
     d->pair_g2[p] = s->pair_geom2[p];

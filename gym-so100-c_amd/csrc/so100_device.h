@@ -62,6 +62,7 @@ struct DevModel {
   float geom_mat[SO100_NGEOM][9];
   float geom_size[SO100_NGEOM][3];
   float geom_rbound[SO100_NGEOM];   // |half sizes| (box bounding sphere)
+  float bin_lo[3], bin_hi[3];       // world AABB of the 5 bin boxes (pad-bin prefilter)
 
   // pairs (0..13 box-box, 14..22 table-hull, 23..76 (cube | bin box, hull) through MPR)
   int pair_g1[SO100_NPAIR], pair_g2[SO100_NPAIR];

@@ -1643,7 +1643,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
   return tot;                             // A/B diagnostic builds only (tests/_build_variant.sh)
 #endif
   // ---- pad-table (lanes 0..7)
-  bool tfound = false;
+  bool tfound = false, nearbin = false;
   float tx = 0.f, ty = 0.f, tz = 0.f;
   if (valid && lane < SO100_NPAD) {
     const int p = SO100_PAIR_PAD0 + lane, g = m->pair_g1[p];
@@ -1651,8 +1651,24 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
     const float* bm = sh.jaw_mat[b - 6];
     const float* gm = m->geom_mat[g];
     const float top = m->table_top, margin = m->pair_margin[p];
-    // broadphase: the pad's lowest point (centre z minus its half-extent along world z)
-    const float cz = sh.jaw_pos[b - 6][2] + bm[6] * m->geom_pos[g][0] + bm[7] * m->geom_pos[g][1] + bm[8] * m->geom_pos[g][2];
+    float pc[3];
+    mulmv3(pc, bm, m->geom_pos[g]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) pc[k] += sh.jaw_pos[b - 6][k];
+    // pad-bin prefilter: the pad's bounding sphere against the bin's AABB
+    float bmarg = 0.f;
+#pragma unroll
+    for (int j = 0; j < SO100_NBINBOX; j++) bmarg = fmaxf(bmarg, m->pair_margin[SO100_PAIR_PADBIN0 + SO100_NBINBOX * lane + j]);
+    float ex2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float u = fmaxf(m->bin_lo[k] - pc[k], pc[k] - m->bin_hi[k]);
+      ex2 += u > 0.f ? u * u : 0.f;
+    }
+    const float rb = m->geom_rbound[g] + bmarg;
+    nearbin = ex2 <= rb * rb;
+    // table broadphase: the pad's lowest point (centre z minus its half-extent along world z)
+    const float cz = pc[2];
     float ext = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; k++) ext += fabsf(bm[6] * gm[k] + bm[7] * gm[3 + k] + bm[8] * gm[6 + k]) * m->geom_size[g][k];
@@ -1697,7 +1713,8 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
     }
   }
   tot += __popc(trow);
-  // ---- pad-bin candidates (3 pairs per lane)
+  // ---- pad-bin candidates (3 pairs per lane); the whole wave skips them when no pad is near the bin
+  if (__ballot(nearbin) == 0ull) return tot;
   uint64_t cm = 0ull;
 #pragma unroll
   for (int r = 0; r < 3; r++) {
