@@ -273,8 +273,24 @@ int build_device_model(const so100_model* s, DevModel* d) {
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: MPR pairs must have condim 3 or 4");
     if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
   }
+  // the static Base hull: (cube, Base hull) then (Base hull, link hull k), all through MPR
+  if (s->hull_body[SO100_HULL_BASE] != 1) return fail("model: hull 9 must be the Base's");
+  if (s->hull_start[SO100_HULL_BASE] < 0 || s->hull_count[SO100_HULL_BASE] < 1 ||
+      s->hull_start[SO100_HULL_BASE] + s->hull_count[SO100_HULL_BASE] > SO100_HULL_NVERT)
+    return fail("model: Base hull vertex range out of bounds");
+  if (s->body_parent[1] != 0) return fail("model: the Base must hang off the world");
+  for (int p = SO100_PAIR_BASE0; p < SO100_PAIR_PAD0; p++) {
+    const int g1 = s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
+    if (p == SO100_PAIR_BASE0) {
+      if (g1 != SO100_CUBE_GEOM || k2 != SO100_HULL_BASE) return fail("model: pair 98 must be (cube, Base hull)");
+    } else if (g1 != -1 - SO100_HULL_BASE || k2 < 0 || k2 >= SO100_NHULL) {
+      return fail("model: Base pairs must be (Base hull, link hull k)");
+    }
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: Base pairs must have condim 3 or 4");
+    if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
+  }
   // hull-hull self-collision pairs: two hulls on different arm links
-  for (int p = SO100_PAIR_SELF0; p < SO100_PAIR_PAD0; p++) {
+  for (int p = SO100_PAIR_SELF0; p < SO100_PAIR_BASE0; p++) {
     const int k1 = -1 - s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
     if (k1 < 0 || k1 >= SO100_NHULL || k2 < 0 || k2 >= SO100_NHULL) return fail("model: self pair must be two hulls");
     if (s->pair_body1[p] != s->hull_body[k1] || s->pair_body2[p] != s->hull_body[k2] || k1 == k2)
@@ -299,6 +315,13 @@ int build_device_model(const so100_model* s, DevModel* d) {
     if (!(b == 0 || b == 6 || b == 7 || b == SO100_CUBE_BODY)) return fail("model: geoms must be static, on the jaws or the cube");
   }
 
+  {
+    double bq[4], bm[9];
+    normq(s->body_quat[1], bq);
+    quat2mat(bq, bm);
+    for (int k = 0; k < 9; k++) d->base_xmat[k] = (float)bm[k];
+    for (int k = 0; k < 3; k++) d->base_xpos[k] = (float)s->body_pos[1][k];
+  }
   d->timestep = (float)s->timestep;
   d->nsubstep = s->nsubstep;
   d->iterations = s->iterations;
@@ -398,7 +421,7 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->pair_tran[p] = (float)(s->body_invweight0[b1][0] + s->body_invweight0[b2][0]);
     d->pair_rot[p] = (float)(s->body_invweight0[b1][1] + s->body_invweight0[b2][1]);
   }
-  for (int k = 0; k < SO100_NHULL; k++) {
+  for (int k = 0; k < SO100_NHULL_ALL; k++) {
     d->hull_body[k] = s->hull_body[k];
     d->hull_start[k] = s->hull_start[k];
     d->hull_count[k] = s->hull_count[k];

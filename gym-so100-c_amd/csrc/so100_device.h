@@ -63,6 +63,7 @@ struct DevModel {
   float geom_size[SO100_NGEOM][3];
   float geom_rbound[SO100_NGEOM];   // |half sizes| (box bounding sphere)
   float bin_lo[3], bin_hi[3];       // world AABB of the 5 bin boxes (pad-bin prefilter)
+  float base_xmat[9], base_xpos[3]; // the static Base's world frame (the Base hull's frame, MPR)
 
   // pairs (0..13 box-box, 14..22 table-hull, 23..76 (cube | bin box, hull) through MPR)
   int pair_g1[SO100_NPAIR], pair_g2[SO100_NPAIR];
@@ -77,9 +78,9 @@ struct DevModel {
   float pair_tran[SO100_NPAIR], pair_rot[SO100_NPAIR];   // diagApprox (body invweight sums)
 
   // arm/jaw collision hulls vs the table top (body-frame vertices and bounding box: center, half extents)
-  int hull_body[SO100_NHULL], hull_start[SO100_NHULL], hull_count[SO100_NHULL];
-  float4_t hull_center[SO100_NHULL], hull_half[SO100_NHULL];   // hull_half.w = |half extents|
-  float4_t hull_centroid[SO100_NHULL];   // MPR portal centre (mesh volume centroid), body frame
+  int hull_body[SO100_NHULL_ALL], hull_start[SO100_NHULL_ALL], hull_count[SO100_NHULL_ALL];
+  float4_t hull_center[SO100_NHULL_ALL], hull_half[SO100_NHULL_ALL];   // hull_half.w = |half extents|
+  float4_t hull_centroid[SO100_NHULL_ALL];   // MPR portal centre (mesh volume centroid), body frame
   float4_t hull_vert[SO100_HULL_NVERT];
   float table_top, table_lo[2], table_hi[2];
 

@@ -1224,13 +1224,29 @@ DEV bool mpr_penetration(const DevModel* __restrict__ m, const MprObj& o, float&
   return true;
 }
 
-// Convex pair p (23..97): obj1 = box geom (cube, bin box) or hull k1 (self-collision), obj2 = hull k, both
+// world frame of a hull's body: an arm link (bodies 2..7, fk_stage's frames in LDS) or the static Base
+// (body 1, hull SO100_HULL_BASE)
+DEV void hull_frame(const DevModel* __restrict__ m, const EnvShared& sh, int b, float* R, float* P) {
+  if (b == 1) {
+#pragma unroll
+    for (int t = 0; t < 9; t++) R[t] = m->base_xmat[t];
+#pragma unroll
+    for (int t = 0; t < 3; t++) P[t] = m->base_xpos[t];
+  } else {
+    const int a = b - 2;
+#pragma unroll
+    for (int t = 0; t < 9; t++) R[t] = sh.ser.xm[a][t];
+#pragma unroll
+    for (int t = 0; t < 3; t++) P[t] = sh.ser.xp[a][t];
+  }
+}
+
+// Convex pair p (23..106): obj1 = box geom (cube, bin box) or hull k1 (self-collision, the Base), obj2 = hull k, both
 // in hull k's body frame H.  Oracle collision().
 DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int p, MprObj& o) {
   const int g = m->pair_g1[p], k = -1 - m->pair_g2[p];
-  const int a = m->hull_body[k] - 2;
-  const float* RH = sh.ser.xm[a];
-  const float* pH = sh.ser.xp[a];
+  float RH[9], pH[3];
+  hull_frame(m, sh, m->hull_body[k], RH, pH);
   float pb[3], Rb[9];
   if (g == SO100_CUBE_GEOM) {
 #pragma unroll
@@ -1243,11 +1259,7 @@ DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int 
 #pragma unroll
     for (int t = 0; t < 9; t++) Rb[t] = m->geom_mat[g][t];
   } else {
-    const int a1 = m->hull_body[-1 - g] - 2;
-#pragma unroll
-    for (int t = 0; t < 3; t++) pb[t] = sh.ser.xp[a1][t];
-#pragma unroll
-    for (int t = 0; t < 9; t++) Rb[t] = sh.ser.xm[a1][t];
+    hull_frame(m, sh, m->hull_body[-1 - g], Rb, pb);
   }
   float dp[3];
   sub3(dp, pb, pH);
@@ -1286,11 +1298,12 @@ DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int 
 // |half sizes| of a box)
 DEV bool mpr_sphere(const DevModel* __restrict__ m, const EnvShared& sh, int p) {
   const int g = m->pair_g1[p], k = -1 - m->pair_g2[p];
-  const int a = m->hull_body[k] - 2;
+  float RH[9], pH[3];
+  hull_frame(m, sh, m->hull_body[k], RH, pH);
   const float4 hb4 = reinterpret_cast<const float4*>(m->hull_center)[k];
   const float hb[3] = {hb4.x, hb4.y, hb4.z};
   float w[3], c1[3], r1;
-  mulmv3(w, sh.ser.xm[a], hb);
+  mulmv3(w, RH, hb);
   if (g == SO100_CUBE_GEOM) {
 #pragma unroll
     for (int t = 0; t < 3; t++) c1[t] = sh.cube_pos[t];
@@ -1300,18 +1313,20 @@ DEV bool mpr_sphere(const DevModel* __restrict__ m, const EnvShared& sh, int p) 
     for (int t = 0; t < 3; t++) c1[t] = m->geom_pos[g][t];
     r1 = m->geom_rbound[g];
   } else {
-    const int k1 = -1 - g, a1 = m->hull_body[k1] - 2;
+    const int k1 = -1 - g;
+    float R1[9], P1[3];
+    hull_frame(m, sh, m->hull_body[k1], R1, P1);
     const float4 b4 = reinterpret_cast<const float4*>(m->hull_center)[k1];
     const float bl[3] = {b4.x, b4.y, b4.z};
     float t1[3];
-    mulmv3(t1, sh.ser.xm[a1], bl);
+    mulmv3(t1, R1, bl);
 #pragma unroll
-    for (int t = 0; t < 3; t++) c1[t] = t1[t] + sh.ser.xp[a1][t];
+    for (int t = 0; t < 3; t++) c1[t] = t1[t] + P1[t];
     r1 = reinterpret_cast<const float4*>(m->hull_half)[k1].w;
   }
   float T[3];
 #pragma unroll
-  for (int t = 0; t < 3; t++) T[t] = c1[t] - (w[t] + sh.ser.xp[a][t]);
+  for (int t = 0; t < 3; t++) T[t] = c1[t] - (w[t] + pH[t]);
   const float rs = reinterpret_cast<const float4*>(m->hull_half)[k].w + r1;
   return dot3(T, T) <= rs * rs;
 }
@@ -1348,8 +1363,9 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
   return true;
 }
 
-// The (cube | bin box, hull) pairs 23..76 of one substep, contacts staged in sh.mpr in pair order.
-//  * broadphase, lane-parallel: lane l of the env's row tests pairs l, l+16, l+32, l+48 (< 54);
+// The MPR pairs 23..106 of one substep ((cube | bin box, hull), hull-hull self-collision, the Base hull),
+// contacts staged in sh.mpr in pair order.
+//  * broadphase, lane-parallel: lane l of the env's row tests pairs 23 + l + 16 r (r < 6);
 //  * narrowphase: the wave walks the union of its 4 envs' candidate pairs in ascending order; each env
 //    holding the pair runs MPR on its whole row.
 // Returns the env's number of staged contacts (uniform across its row, capped at kMaxCon).
@@ -1357,7 +1373,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
 #ifdef SO100_EXPERIMENT_NO_MPR
   return 0;   // timing experiment only: box-hull contacts off
 #endif
-  constexpr int kRounds = (SO100_NPAIR_CONVEX + kLanes - 1) / kLanes;   // 5
+  constexpr int kRounds = (SO100_NPAIR_CONVEX + kLanes - 1) / kLanes;   // 6
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
   uint64_t env_cand[2] = {0ull, 0ull}, wave_cand[2] = {0ull, 0ull};
 #pragma unroll
@@ -1389,13 +1405,13 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
       float depth, dir[3], pos[3];
       if (mpr_penetration(m, o, depth, dir, pos, lane)) {
         if (ns < kMaxCon && lane == 0) {
-          const int a = m->hull_body[k] - 2;
-          float wn[3], wp[3];
-          mulmv3(wn, sh.ser.xm[a], dir);
-          mulmv3(wp, sh.ser.xm[a], pos);
+          float RH[9], pH[3], wn[3], wp[3];
+          hull_frame(m, sh, m->hull_body[k], RH, pH);
+          mulmv3(wn, RH, dir);
+          mulmv3(wp, RH, pos);
           MprStage& st = sh.mpr[ns];
-          st.pos[0] = wp[0] + sh.ser.xp[a][0]; st.pos[1] = wp[1] + sh.ser.xp[a][1];
-          st.pos[2] = wp[2] + sh.ser.xp[a][2]; st.pos[3] = -depth;
+          st.pos[0] = wp[0] + pH[0]; st.pos[1] = wp[1] + pH[1];
+          st.pos[2] = wp[2] + pH[2]; st.pos[3] = -depth;
           st.nrm[0] = wn[0]; st.nrm[1] = wn[1]; st.nrm[2] = wn[2];
           st.nrm[3] = __int_as_float(p);
         }

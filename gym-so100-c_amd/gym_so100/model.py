@@ -19,11 +19,13 @@ NBODY, NHINGE, NQ, NV, NU, NGEOM = 9, 6, 13, 12, 6, 15
 NPAIR_BOX, NHULL, HULL_NVERT, NBINBOX = 14, 9, 2560, 5
 PAIR_MPR0 = NPAIR_BOX + NHULL                  # (box, hull) pairs of the MPR convex collider start here
 PAIR_SELF0 = PAIR_MPR0 + (1 + NBINBOX) * NHULL  # 77: hull-hull self-collision pairs
+NHULL_ALL, HULL_BASE = NHULL + 1, NHULL          # hull arrays hold the static Base's hull at index 9
 NPAIR_SELF = 21
-PAIR_PAD0 = PAIR_SELF0 + NPAIR_SELF              # 98: (pad i, table) pairs 98..105
-PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 106: (pad i, bin box j) at 106 + 5 i + j, box-box
+PAIR_BASE0 = PAIR_SELF0 + NPAIR_SELF             # 98: (cube, Base hull), 99..106 (Base hull, hull k = 1..8)
+PAIR_PAD0 = PAIR_BASE0 + 9                       # 107: (pad i, table) pairs 107..114
+PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 115: (pad i, bin box j) at 115 + 5 i + j, box-box
 NPAIR_PAD = 8 * (1 + NBINBOX)                    # 48
-NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 146
+NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 155
 NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
 MAXCON, CONDIM, NOBS = 16, 4, 15
 NEFC_MAX = NV + NHINGE + MAXCON * CONDIM
@@ -59,9 +61,9 @@ class SO100Model(ctypes.Structure):
         ("pair_body1", _arr(_i, NPAIR)), ("pair_body2", _arr(_i, NPAIR)), ("pair_condim", _arr(_i, NPAIR)),
         ("pair_friction", _arr(_d, NPAIR, 3)), ("pair_solref", _arr(_d, NPAIR, 2)),
         ("pair_solimp", _arr(_d, NPAIR, 5)), ("pair_margin", _arr(_d, NPAIR)),
-        ("hull_body", _arr(_i, NHULL)), ("hull_start", _arr(_i, NHULL)), ("hull_count", _arr(_i, NHULL)),
-        ("hull_center", _arr(_d, NHULL, 3)), ("hull_half", _arr(_d, NHULL, 3)),
-        ("hull_centroid", _arr(_d, NHULL, 3)),
+        ("hull_body", _arr(_i, NHULL_ALL)), ("hull_start", _arr(_i, NHULL_ALL)), ("hull_count", _arr(_i, NHULL_ALL)),
+        ("hull_center", _arr(_d, NHULL_ALL, 3)), ("hull_half", _arr(_d, NHULL_ALL, 3)),
+        ("hull_centroid", _arr(_d, NHULL_ALL, 3)),
         ("hull_vert", _arr(_d, HULL_NVERT, 3)),
         ("table_top", _d), ("table_lo", _arr(_d, 2)), ("table_hi", _arr(_d, 2)),
         ("site_cube_body", _i), ("site_cube_pos", _arr(_d, 3)), ("site_ee_body", _i), ("site_ee_pos", _arr(_d, 3)),
@@ -146,7 +148,7 @@ def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton", var
     _set(m, "pair_body1", np.asarray([x["body1"] for x in p], dtype=np.int64))
     _set(m, "pair_body2", np.asarray([x["body2"] for x in p], dtype=np.int64))
     h = d["hulls"]
-    assert len(h) == NHULL and len(p) == NPAIR
+    assert len(h) == NHULL_ALL and len(p) == NPAIR
     counts = [len(x["verts"]) for x in h]
     starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
     verts = np.zeros((HULL_NVERT, 3))

@@ -353,7 +353,7 @@ def compile_model():
     # ---- arm/jaw collision hulls (convex hulls of the class="collision" meshes of the moving bodies) ----
     from scipy.spatial import ConvexHull
     hulls = []
-    for bname in ARM_BODIES[1:]:
+    for bname in ARM_BODIES[1:] + ARM_BODIES[:1]:      # the 9 link hulls, then the static Base's (hull 9)
         for g in bodies[bname]["geoms"]:
             if g.get("type") != "mesh" or g.get("group") != "3" or g.get("contype", "1") == "0":
                 continue
@@ -402,17 +402,17 @@ def compile_model():
         pairs.append(dict(g1=gid[n1], g2=gid[n2], body1=g1["body"], body2=g2["body"], name1=n1, name2=n2,
                           **mixed(g1, g2)))
     # (table, hull k): geom1 = the table (world geom, lower id), normal from the table to the hull
-    for k, h in enumerate(hulls):
+    for k, h in enumerate(hulls[:9]):
         pairs.append(dict(g1=gid["table"], g2=-1 - k, body1=0, body2=h["body"], name1="table", name2=h["name"],
                           hull=k, **mixed(tbl, h)))
     # (box, hull k) through the general convex collider (MPR): geom1 = the box (MuJoCo orders a pair by
     # geom type, box < mesh), normal from the box to the hull.  Pairs 23..31: the cube against every
-    # arm/jaw hull; pairs 32..76: bin box j (walls, floor) against hull k at 32 + 9 j + k.  Not in scope:
-    # the static Base hull (far from every spawn), hull-hull self-collision, pads vs table/bin.
+    # arm/jaw hull; pairs 32..76: bin box j (walls, floor) against hull k at 32 + 9 j + k (the static
+    # Base hull against the static bin boxes is a static-static pair, filtered).
     boxes = ["red_box"] + ["bin_wall", "bin_wall2", "bin_wall3", "bin_wall4", "bin_floor"]
     for n1 in boxes:
         g1 = geoms[gid[n1]]
-        for k, h in enumerate(hulls):
+        for k, h in enumerate(hulls[:9]):
             pairs.append(dict(g1=gid[n1], g2=-1 - k, body1=g1["body"], body2=h["body"], name1=n1,
                               name2=h["name"], hull=k, **mixed(g1, h)))
     # Pairs 77..97: hull-hull self-collision of the arm, through the same collider.  MuJoCo filters only
@@ -420,15 +420,28 @@ def compile_model():
     # geom1 = the hull on the body nearer the root, normal from it to the other.
     parent = {bid[n]: bid[bodies[n]["parent"]] if bodies[n]["parent"] in bid else 0 for n in ARM_BODIES}
     excl = {frozenset((bid[a], bid[b])) for a, b in excludes}
-    for k1, h1 in enumerate(hulls):
-        for k2, h2 in enumerate(hulls):
+    for k1, h1 in enumerate(hulls[:9]):
+        for k2, h2 in enumerate(hulls[:9]):
             b1, b2 = h1["body"], h2["body"]
             if not b1 < b2 or parent[b2] == b1 or frozenset((b1, b2)) in excl:
                 continue
             pairs.append(dict(g1=-1 - k1, g2=-1 - k2, body1=b1, body2=b2, name1=h1["name"], name2=h2["name"],
                               hull=k2, hull1=k1, **mixed(h1, h2)))
 
-    # Pairs 98..105: the 8 finger pads against the table; 106..145: against the 5 bin boxes (106 + 5 i + j).
+    # Pairs 98..106: the static Base's hull (hull 9).  The Base has no joint, so MuJoCo's parent filter
+    # (which skips world-welded bodies) does not apply; the model's exclude removes Rotation_Pitch, and the
+    # static-static rule the table and the bin.  (red_box, Base): box < mesh, geom1 = the cube; (Base, hull
+    # k): the Base's geom has the lower id, geom1 = the Base hull.
+    assert len(hulls) == 10 and hulls[9]["body"] == bid["Base"]
+    pairs.append(dict(g1=gid["red_box"], g2=-1 - 9, body1=geoms[gid["red_box"]]["body"], body2=bid["Base"],
+                      name1="red_box", name2=hulls[9]["name"], hull=9, **mixed(geoms[gid["red_box"]], hulls[9])))
+    for k, h in enumerate(hulls[:9]):
+        if frozenset((bid["Base"], h["body"])) in excl:
+            continue
+        pairs.append(dict(g1=-1 - 9, g2=-1 - k, body1=bid["Base"], body2=h["body"], name1=hulls[9]["name"],
+                          name2=h["name"], hull=k, hull1=9, **mixed(hulls[9], h)))
+    assert len(pairs) == 107
+    # Pairs 107..114: the 8 finger pads against the table; 115..154: against the 5 bin boxes (115 + 5 i + j).
     # geom1 = the pad: the table is a mesh (box < mesh) and the bin boxes come after the arm in the model
     # (so100_transfer_cube.xml includes the arm before the bin), so the normal points from the pad to the
     # table / bin box.  Pad-table contacts follow the hull-table rule (one per pair); pad-bin pairs are
@@ -440,7 +453,7 @@ def compile_model():
         g1, g2 = geoms[gid[n1]], geoms[gid[n2]]
         pairs.append(dict(g1=gid[n1], g2=gid[n2], body1=g1["body"], body2=g2["body"], name1=n1, name2=n2,
                           **mixed(g1, g2)))
-    assert len(pairs) == 146
+    assert len(pairs) == 155
 
     # ---- EE / mocap variant (so100_transfer_cube_ee.xml: the same scene with trs_so_arm100/so_arm100_ee.xml,
     # whose only differences are the mocap body at :155 and the weld equality at :171-173) ----

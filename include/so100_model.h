@@ -17,6 +17,8 @@
  *          23..31 (red_box, hull k) | 32..76 (bin box j, hull k) at 32 + 9 j + k, j = bin_wall,
  *          bin_wall2..4, bin_floor: box vs convex hull through the MPR convex collider
  *          77..97 (hull k1, hull k2): self-collision of hulls on non-adjacent arm links (MPR)
+ *          98..106 (red_box, Base hull) and (Base hull, hull k), k = 1..8: the static Base (MPR)
+ *          107..114 (finger pad i, table); 115..154 (finger pad i, bin box j) at 115 + 5 i + j
  *   hulls  0 Rotation_Pitch | 1 Upper_Arm | 2 Lower_Arm | 3 Wrist_Pitch_Roll |
  *          4..5 Fixed_Jaw_Collision_1..2 | 6..8 Moving_Jaw_Collision_1..3
  */
@@ -30,19 +32,23 @@
 #define SO100_NU 6
 #define SO100_NGEOM 15
 #define SO100_NPAIR_BOX 14         /* box-box pairs 0..13 */
-#define SO100_NHULL 9               /* arm/jaw collision hulls */
+#define SO100_NHULL 9               /* arm/jaw collision hulls (moving links) */
+#define SO100_HULL_BASE 9           /* hull 9: the static Base's collision hull */
+#define SO100_NHULL_ALL 10          /* hull arrays: the 9 link hulls + the Base hull */
 #define SO100_NBINBOX 5             /* bin walls + floor (geoms 10..14) */
 #define SO100_PAIR_MPR0 (SO100_NPAIR_BOX + SO100_NHULL)     /* 23: first (box, hull) MPR pair */
 #define SO100_NPAIR_MPR ((1 + SO100_NBINBOX) * SO100_NHULL) /* 54: (cube | bin box j, hull k) */
 #define SO100_PAIR_SELF0 (SO100_PAIR_MPR0 + SO100_NPAIR_MPR)  /* 77: first hull-hull self-collision pair */
 #define SO100_NPAIR_SELF 21                                 /* hulls on non-adjacent arm links */
-#define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF)  /* 75 pairs through the MPR collider */
-#define SO100_PAIR_PAD0 (SO100_PAIR_SELF0 + SO100_NPAIR_SELF)  /* 98: first (pad, table | bin box) pair */
+#define SO100_PAIR_BASE0 (SO100_PAIR_SELF0 + SO100_NPAIR_SELF)  /* 98: (cube, Base hull), then (Base hull, hull k) */
+#define SO100_NPAIR_BASE 9                                  /* 99..106: hull k = 1..8 (Rotation_Pitch excluded) */
+#define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF + SO100_NPAIR_BASE)  /* 84 pairs through MPR */
+#define SO100_PAIR_PAD0 (SO100_PAIR_BASE0 + SO100_NPAIR_BASE)  /* 107: first (pad, table | bin box) pair */
 #define SO100_NPAD 8                                        /* finger pads: geoms 1..8 */
-#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 106: (pad i, bin box j) at 106 + 5 i + j */
+#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 115: (pad i, bin box j) at 115 + 5 i + j */
 #define SO100_NPAIR_PADBIN (SO100_NPAD * SO100_NBINBOX)     /* 40, box-box */
-#define SO100_NPAIR_PAD (SO100_NPAD + SO100_NPAIR_PADBIN)   /* 48: 98..105 (pad i, table), then pad-bin */
-#define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 146 */
+#define SO100_NPAIR_PAD (SO100_NPAD + SO100_NPAIR_PADBIN)   /* 48: 107..114 (pad i, table), then pad-bin */
+#define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 155 */
 #define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_CUBE_BODY 8
@@ -123,12 +129,12 @@ typedef struct so100_model {
   /* arm/jaw collision hulls: convex hulls of the collision meshes, vertices in the body frame,
    * body-frame bounding box (center, half extents) for the broadphase; the table's top face (z, x-y
    * footprint) */
-  int    hull_body[SO100_NHULL];
-  int    hull_start[SO100_NHULL];
-  int    hull_count[SO100_NHULL];
-  double hull_center[SO100_NHULL][3];
-  double hull_half[SO100_NHULL][3];
-  double hull_centroid[SO100_NHULL][3];   /* mesh volume centroid = the mesh geom's frame origin */
+  int    hull_body[SO100_NHULL_ALL];
+  int    hull_start[SO100_NHULL_ALL];
+  int    hull_count[SO100_NHULL_ALL];
+  double hull_center[SO100_NHULL_ALL][3];
+  double hull_half[SO100_NHULL_ALL][3];
+  double hull_centroid[SO100_NHULL_ALL][3];   /* mesh volume centroid = the mesh geom's frame origin */
   double hull_vert[SO100_HULL_NVERT][3];
   double table_top;
   double table_lo[2];

@@ -681,14 +681,14 @@ def test_domain_randomization_config4_shard(solver):
     shard.close()
 
 
-@pytest.mark.parametrize("solver", ["newton", "pgs"])
-def test_self_collision_parity(solver, oracle64, oracle32):
-    """Hull-hull self-collision (pairs 77..97, SURVEY §8 f.2): random arm configurations whose
-    non-adjacent links overlap, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
+def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed):
+    """random arm configurations with a contact in pairs [p0, p1), the actuators holding them;
+    teacher-forced GPU steps at the fp32 floor"""
     from gym_so100 import SO100VecEnv
-    from gym_so100.model import PAIR_SELF0, PAIR_PAD0, build_model
+    from gym_so100.model import build_model
+    PAIR_SELF0, PAIR_BASE0 = p0, p1
     model = build_model(solver=solver)
-    rng = np.random.default_rng(17)
+    rng = np.random.default_rng(seed)
     lo_j = np.array([r[0] for r in model.jnt_range]); hi_j = np.array([r[1] for r in model.jnt_range])
     lo, hi = np.array(model.action_lo[:]), np.array(model.action_hi[:])
     d = oracle64.new_data()
@@ -699,7 +699,7 @@ def test_self_collision_parity(solver, oracle64, oracle32):
         for k in range(6):
             d.qpos[k] = arm[k]
         oracle64.call("so100o_fwd_position", model, d)
-        if any(PAIR_SELF0 <= d.con[i].pair < PAIR_PAD0 for i in range(d.ncon)) and not d.ncon_dropped:
+        if any(PAIR_SELF0 <= d.con[i].pair < PAIR_BASE0 for i in range(d.ncon)) and not d.ncon_dropped:
             q, v, w, _ = oracle64.get_state(d)
             states.append((q, v * 0, w * 0))
             targets.append(np.clip((arm - lo) / (hi - lo) * 2 - 1, -1, 1))
@@ -721,7 +721,7 @@ def test_self_collision_parity(solver, oracle64, oracle32):
         dbg = env.debug.cpu().numpy()
         for i in range(n):
             pairs = dbg[i, 48:48 + int(dbg[i, 0])]
-            self_con.append(int(((pairs >= PAIR_SELF0) & (pairs < PAIR_PAD0)).sum()))
+            self_con.append(int(((pairs >= PAIR_SELF0) & (pairs < PAIR_BASE0)).sum()))
             oracle64.set_state(d64, q0[i], v0[i], w0[i])
             oracle32.set_state(d32, q0[i], v0[i], w0[i])
             oracle64.env_step(model, d64, 0, act[i])
@@ -730,7 +730,7 @@ def test_self_collision_parity(solver, oracle64, oracle32):
             qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
             qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
     qv_err, qv_floor, self_con = np.array(qv_err), np.array(qv_floor), np.array(self_con)
-    print(f"\n[{solver}] self-collision: GPU self contacts per env mean {self_con.mean():.2f} (envs with any: "
+    print(f"\n[{solver}] {label}: GPU {label} contacts per env mean {self_con.mean():.2f} (envs with any: "
           f"{(self_con > 0).mean():.2f}) | qvel rel GPU median {np.median(qv_err):.2e} p90 "
           f"{np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor median {np.median(qv_floor):.2e} "
           f"p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
@@ -739,6 +739,22 @@ def test_self_collision_parity(solver, oracle64, oracle32):
     assert np.mean(qv_err > 1e-4) <= 1.5 * np.mean(qv_floor > 1e-4) + 0.05    # tail mass (MPR: see above)
     assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
     env.close()
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_self_collision_parity(solver, oracle64, oracle32):
+    """Hull-hull self-collision (pairs 77..97, SURVEY §8 f.2): random arm configurations whose
+    non-adjacent links overlap, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
+    from gym_so100.model import PAIR_SELF0, PAIR_BASE0
+    _arm_contact_parity(solver, oracle64, oracle32, PAIR_SELF0, PAIR_BASE0, "self-collision", 17)
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_base_contact_parity(solver, oracle64, oracle32):
+    """Link hulls against the static Base's hull (pairs 99..106 through MPR): random arm
+    configurations folded into the Base, the actuators holding them; teacher-forced GPU steps."""
+    from gym_so100.model import PAIR_BASE0, PAIR_PAD0
+    _arm_contact_parity(solver, oracle64, oracle32, PAIR_BASE0, PAIR_PAD0, "Base", 19)
 
 
 def test_step_graph_replay_matches_eager(monkeypatch):
