@@ -1373,14 +1373,19 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
 #ifdef SO100_EXPERIMENT_NO_MPR
   return 0;   // timing experiment only: box-hull contacts off
 #endif
-  constexpr int kRounds = (SO100_NPAIR_CONVEX + kLanes - 1) / kLanes;   // 6
+#ifdef SO100_NO_BASE
+  constexpr int kConvex = SO100_NPAIR_CONVEX - SO100_NPAIR_BASE;   // A/B diagnostic builds only
+#else
+  constexpr int kConvex = SO100_NPAIR_CONVEX;
+#endif
+  constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 6
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
   uint64_t env_cand[2] = {0ull, 0ull}, wave_cand[2] = {0ull, 0ull};
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
     const int q = lane + kLanes * r;
     bool cand = false;
-    if (valid && q < SO100_NPAIR_CONVEX && mpr_sphere(m, sh, SO100_PAIR_MPR0 + q)) {
+    if (valid && q < kConvex && mpr_sphere(m, sh, SO100_PAIR_MPR0 + q)) {
       MprObj o;
       mpr_obj_setup(m, sh, SO100_PAIR_MPR0 + q, o);
       cand = mpr_broadphase(m, o, -1 - m->pair_g2[SO100_PAIR_MPR0 + q]);
