@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 6   /* 6: pad-vs-table/bin pairs (SO100_NPAIR 146); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 6   /* 6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
