@@ -757,6 +757,62 @@ def test_base_contact_parity(solver, oracle64, oracle32):
     _arm_contact_parity(solver, oracle64, oracle32, PAIR_BASE0, PAIR_PAD0, "Base", 19)
 
 
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_cube_on_base_parity(solver, oracle64, oracle32):
+    """The cube resting on the static Base (pair 98, box vs the Base hull through MPR, one contact):
+    states made by the fp64 oracle dropping the cube onto the Base top, then teacher-forced GPU steps."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import PAIR_BASE0, build_model
+    model = build_model(solver=solver)
+    rng = np.random.default_rng(23)
+    d = oracle64.new_data()
+    states = []
+    for i in range(16):
+        dx, dy = rng.uniform(-0.02, 0.02, 2)
+        q = np.array([1, 0, 0, rng.uniform(-0.3, 0.3)])
+        oracle64.reset(model, d, np.array([-0.469 + dx, 0.5 + dy, 0.12, *(q / np.linalg.norm(q))]))
+        for _ in range(300):
+            oracle64.call("so100o_substep", model, d)
+        states.append(oracle64.get_state(d)[:3])
+    n = len(states)
+    start = np.array([-1.0 + 2.0 * (model.start_qpos[k] - model.action_lo[k]) / (model.action_hi[k] - model.action_lo[k])
+                      for k in range(6)], np.float32)
+    env = SO100VecEnv(n, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver)
+    env.reset(seed=3)
+    env.set_state(np.array([s[0] for s in states], np.float32), np.array([s[1] for s in states], np.float32),
+                  np.array([s[2] for s in states], np.float32))
+    d64, d32 = oracle64.new_data(), oracle32.new_data()
+    qv_err, qv_floor, base_con = [], [], []
+    for step in range(4):
+        q0 = env.qpos.cpu().numpy().astype(np.float64)
+        v0 = env.qvel.cpu().numpy().astype(np.float64)
+        w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
+        act = np.tile(start, (n, 1))
+        env.step(torch.from_numpy(act).cuda())
+        torch.cuda.synchronize()
+        gv = env.qvel.cpu().numpy()
+        dbg = env.debug.cpu().numpy()
+        for i in range(n):
+            pairs = dbg[i, 48:48 + int(dbg[i, 0])]
+            base_con.append(int((pairs == PAIR_BASE0).sum()))
+            oracle64.set_state(d64, q0[i], v0[i], w0[i])
+            oracle32.set_state(d32, q0[i], v0[i], w0[i])
+            oracle64.env_step(model, d64, 0, act[i])
+            oracle32.env_step(model, d32, 0, act[i])
+            ov = oracle64.get_state(d64)[1]
+            qv_err.append((np.abs(ov - gv[i]) / (1 + np.abs(ov))).max())
+            qv_floor.append((np.abs(ov - oracle32.get_state(d32)[1]) / (1 + np.abs(ov))).max())
+    qv_err, qv_floor, base_con = np.array(qv_err), np.array(qv_floor), np.array(base_con)
+    print(f"\n[{solver}] cube on Base: GPU cube-Base contacts per env mean {base_con.mean():.2f} | qvel rel GPU "
+          f"median {np.median(qv_err):.2e} p90 {np.quantile(qv_err, .9):.2e} max {qv_err.max():.2e} | fp32 floor "
+          f"median {np.median(qv_floor):.2e} p90 {np.quantile(qv_floor, .9):.2e} max {qv_floor.max():.2e}")
+    assert (base_con > 0).mean() > 0.8                     # the cube really rests on the Base
+    assert np.median(qv_err) <= 2 * np.median(qv_floor) + 1e-5
+    assert np.quantile(qv_err, 0.9) <= 2 * np.quantile(qv_floor, 0.9) + 1e-4
+    assert qv_err.max() <= 2 * qv_floor.max() + 1e-3
+    env.close()
+
+
 def test_step_graph_replay_matches_eager(monkeypatch):
     """so100_step replays a captured hipGraph of the step (chunk fork/join included); SO100_GRAPH=0 launches
     eagerly.  Both must give bit-identical trajectories, across re-captures (new action buffer, flags)."""
