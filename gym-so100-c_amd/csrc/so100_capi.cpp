@@ -176,6 +176,8 @@ static so100_buffers offset_buffers(const so100_buffers& b, int s) {
   o.total_steps = off(b.total_steps, 1);
   o.dr_params = off(b.dr_params, 4);
   o.debug = off(b.debug, SO100_DBG_STRIDE);
+  o.mocap = off(b.mocap, 7);
+  o.reward64 = off(b.reward64, 1);
   return o;
 }
 

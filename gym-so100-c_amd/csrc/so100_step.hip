@@ -2288,6 +2288,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
   if (valid) {
     if (lane == 0) {
       if (B.reward) B.reward[env] = (float)reward;
+      if (B.reward64) B.reward64[env] = reward;
       if (B.terminated) B.terminated[env] = terminated;
       if (B.truncated) B.truncated[env] = truncated;
       if (B.success) B.success[env] = success;

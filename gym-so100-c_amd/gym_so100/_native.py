@@ -22,7 +22,7 @@ class SO100Buffers(ctypes.Structure):
     _fields_ = [(n, _P) for n in (
         "qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "action",
         "obs", "reward", "terminated", "truncated", "success", "final_obs", "diverged", "contact_bits",
-        "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug", "mocap")]
+        "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64")]
 
 
 SO100_MAX_LIGHTS = 4
@@ -44,7 +44,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 6          # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 7          # include/so100.h SO100_ABI_VERSION
 
 
 def load():

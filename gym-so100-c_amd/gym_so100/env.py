@@ -30,10 +30,19 @@ except ImportError:          # gymnasium is optional here
 class SO100Env(_Base):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
 
-    def __init__(self, task, obs_type="so100_state", render_mode="rgb_array", observation_width=640,
+    def __init__(self, task, obs_type="pixels", render_mode="rgb_array", observation_width=640,
                  observation_height=480, visualization_width=640, visualization_height=480, device="cuda:0",
                  max_episode_steps=0, solver="newton"):
+        """Same signature and default as the reference (env.py:28-38).  Its default obs_type "pixels" is
+        one the reference's own code does not handle: no observation_space is set (env.py:50-73) and
+        _format_raw_obs leaves `obs` unbound (env.py:130-146), so its first reset fails.  Here that default
+        fails at construction, with the two obs types the reference does serve named; the registered ids
+        (gym_so100/__init__.py:4-32) pass so100_pixels_agent_pos, as in the reference."""
         super().__init__()
+        if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
+            raise ValueError(f"obs_type={obs_type!r} is not served (the reference's default 'pixels' fails "
+                             "in its own _format_raw_obs, env.py:130-146): pass obs_type="
+                             "'so100_pixels_agent_pos' (the registered envs') or 'so100_state'")
         self.task = task
         self.obs_type = obs_type
         self.render_mode = render_mode
@@ -42,7 +51,8 @@ class SO100Env(_Base):
         # TimeLimit is applied by the gymnasium registry wrapper (as in the reference); 0 = none here
         self._venv = SO100VecEnv(1, task=task, obs_type=obs_type, device=device, autoreset=False,
                                  max_episode_steps=max_episode_steps, solver=solver,
-                                 observation_width=observation_width, observation_height=observation_height)
+                                 observation_width=observation_width, observation_height=observation_height,
+                                 reward64=True)
         self._vis = None
         if obs_type == "so100_pixels_agent_pos":                          # env.py:50-66
             self.observation_space = spaces.Dict({
@@ -68,7 +78,7 @@ class SO100Env(_Base):
         action = np.asarray(action, dtype=np.float32)
         assert action.ndim == 1                                          # env.py:173
         obs, reward, terminated, truncated, info = self._venv.step(action[None, :6])
-        r = float(reward[0].item())
+        r = float(self._venv.reward64[0].item())                       # float64, as the reference
         is_success = bool(info["is_success"][0].item())
         return self._np_obs(obs), r, bool(terminated[0].item()), False, {"is_success": is_success}
 
@@ -99,7 +109,7 @@ class SO100GoalEnv(_Base):
         self.visualization_width, self.visualization_height = visualization_width, visualization_height
         self._venv = SO100VecEnv(1, task="so100_goal", device=device, autoreset=False, solver=solver,
                                  obs_type=obs_type, observation_width=observation_width,
-                                 observation_height=observation_height)
+                                 observation_height=observation_height, reward64=True)
         self._vis = None
         self.distance_threshold = GOAL_DISTANCE_THRESHOLD                # env.py:252
         size = observation_height * observation_width * 3 + len(SO100_JOINTS) \
@@ -146,7 +156,7 @@ class SO100GoalEnv(_Base):
         inf = {"is_success": success}
         if trunc:
             inf["TimeLimit.truncated"] = True
-        return out, float(reward[0].item()), bool(terminated[0].item()), trunc, inf
+        return out, float(self._venv.reward64[0].item()), bool(terminated[0].item()), trunc, inf
 
     def render(self):
         """Top camera at the visualization size (env.py:256-265), uint8 [H, W, 3]."""

@@ -84,12 +84,14 @@ class SO100VecEnv:
         solver: "newton" (default: MuJoCo's default solver, which the reference's model runs; the
             unique minimiser of the constraint problem) or "pgs" (north_star's projected Gauss-Seidel).
         debug: allocate the [N, 96] diagnostics buffer (contacts, forces, solver iterations).
+        reward64: also keep the reward in float64 (``self.reward64``), as the reference returns it; the
+            float32 ``reward`` rounds the dense TouchCube shaping (the other ladders are exact in float32).
     """
 
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
                  iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480,
-                 variant="joint"):
+                 variant="joint", reward64=False):
         torch = _torch()
         if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
             raise NotImplementedError(f"obs_type={obs_type!r}: 'so100_state' or 'so100_pixels_agent_pos'")
@@ -136,6 +138,7 @@ class SO100VecEnv:
         self.desired_goal = torch.zeros(n, 3, dtype=f32, device=d) if self.is_goal else None
         self.total_steps = torch.zeros(n, dtype=i32, device=d) if self.is_goal else None
         self.debug = torch.zeros(n, _native.SO100_DBG_STRIDE, dtype=f32, device=d) if debug else None
+        self.reward64 = torch.zeros(n, dtype=torch.float64, device=d) if reward64 else None
         self.mocap = None
         if variant == "ee":          # mj_resetData's mocap pose: the mocap body's (so_arm100_ee.xml:155)
             m0 = list(self.model.mocap_pos0) + list(self.model.mocap_quat0)
@@ -161,7 +164,7 @@ class SO100VecEnv:
         b = self._buf
         for name in ("qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "obs", "reward", "terminated",
                      "truncated", "success", "final_obs", "diverged", "contact_bits", "achieved_goal",
-                     "desired_goal", "total_steps", "dr_params", "debug", "mocap"):
+                     "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64"):
             setattr(b, name, P(getattr(self, name)))
         b.action = P(self.actions)
 

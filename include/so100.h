@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 6   /* 6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 7   /* 7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -67,6 +67,10 @@ typedef struct so100_buffers {
    * target the weld equality pulls ee_site to (teleop_ee.py:52-98 drives data.mocap_pos/quat); NULL =
    * the model's default pose */
   const float* mocap;
+  /* [N] the reward in float64, as the reference returns it (task_reward computes in double; `reward`
+   * holds its float32 rounding, exact for the CubeToBin / sparse / GoalEnv ladders, rounded for the dense
+   * TouchCube shaping); NULL = not written */
+  double*   reward64;
 } so100_buffers;
 
 #define SO100_DBG_STRIDE 96  /* ncon, solver_iter, improvement, nefc, qacc[12], contact(dist,fn)[16], ... */

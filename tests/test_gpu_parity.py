@@ -239,12 +239,15 @@ def test_sharding_invariance():
     assert torch.equal(full.obs, torch.cat([a0.obs, a1.obs]))
 
 
-def test_chunking_invariance(monkeypatch):
+@pytest.mark.parametrize("variant", ["joint", "ee"])
+def test_chunking_invariance(monkeypatch, variant):
     """The env-range chunks of a step (concurrent streams, so100_capi.cpp) change nothing: 4 ragged
-    chunks == 1 chunk, bitwise, through auto-resets and the solver's debug record."""
+    chunks == 1 chunk, bitwise, through auto-resets and the solver's debug record.  The EE variant gives
+    every env its own mocap target, so a chunk reading another chunk's targets (a per-env pointer left
+    unshifted by offset_buffers) shows up as a mismatch."""
     from gym_so100 import SO100VecEnv
     n = 4160
-    kw = dict(device="cuda:0", seed=4, max_episode_steps=5, debug=True)
+    kw = dict(device="cuda:0", seed=4, max_episode_steps=5, debug=True, variant=variant)
     monkeypatch.setenv("SO100_CHUNKS", "1")
     one = SO100VecEnv(n, **kw)
     monkeypatch.setenv("SO100_CHUNKS", "4")
@@ -254,6 +257,12 @@ def test_chunking_invariance(monkeypatch):
     assert k == 4 and n0 < n
     for e in (one, four):
         e.reset()
+    if variant == "ee":
+        gm = torch.Generator(device="cuda").manual_seed(3)
+        pos = one.mocap[:, :3] + (torch.rand(n, 3, generator=gm, device="cuda") - 0.5) * 0.08
+        for e in (one, four):
+            e.set_mocap(pos)
+        assert pos[:, 0].unique().numel() > n // 2          # distinct per-env targets
     g = torch.Generator(device="cuda").manual_seed(2)
     for _ in range(12):
         a = torch.rand(n, 6, generator=g, device="cuda") * 2 - 1
@@ -307,7 +316,9 @@ def test_domain_randomization_changes_dynamics_deterministically():
 
 def test_single_env_api():
     from gym_so100 import SO100Env, SO100GoalEnv
-    env = SO100Env("so100_cube_to_bin")
+    with pytest.raises(ValueError):
+        SO100Env("so100_cube_to_bin")                  # the reference's default obs_type "pixels"
+    env = SO100Env("so100_cube_to_bin", obs_type="so100_state")
     obs, info = env.reset(seed=0)
     assert obs.shape == (15,) and obs.dtype == np.float32 and info == {"is_success": False}
     obs, r, term, trunc, info = env.step(np.zeros(6, np.float32))
@@ -319,6 +330,32 @@ def test_single_env_api():
     assert r in (0.0, -1.0)
     rb = g.compute_reward(np.zeros((4, 3)), np.zeros((4, 3)) + 0.001, {})
     assert rb.dtype == np.float32 and (rb == 0).all()
+
+
+def test_reward64_is_the_double_ladder(oracle64):
+    """reward64 holds the reward in float64 as the reference returns it (env.py:174-182 passes the task's
+    python float through); reward is its float32 rounding.  Dense TouchCube shaping (single_arm.py:149-215)
+    is not representable in float32, so the two differ there; the float64 value equals the oracle's."""
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import build_model
+    n = 64
+    venv = SO100VecEnv(n, task="so100_touch_cube", device="cuda:0", autoreset=False, max_episode_steps=0,
+                       reward64=True)
+    venv.reset(seed=300)
+    torch.cuda.synchronize()
+    q0 = venv.qpos.cpu().numpy().astype(np.float64)
+    a = np.random.default_rng(1).uniform(-1, 1, size=(n, 6)).astype(np.float32)
+    venv.step(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    r32, r64 = venv.reward.cpu().numpy(), venv.reward64.cpu().numpy()
+    assert np.array_equal(r64.astype(np.float32), r32)
+    assert (r64 != r32.astype(np.float64)).any()           # the dense shaping needs float64
+    model, d = build_model(), oracle64.new_data()
+    for i in range(n):
+        oracle64.set_state(d, q0[i], np.zeros(12), np.zeros(12))
+        _, r, _ = oracle64.env_step(model, d, 1, a[i])
+        assert abs(r64[i] - r) <= 1e-5
+    venv.close()
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
