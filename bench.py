@@ -8,8 +8,10 @@
 One "step" = one batched env step of every env on every GPU: action prologue, 10 physics substeps
 (kinematics, CRBA/RNE, box-box / hull / MPR contacts, the constraint solve -- primal Newton, MuJoCo's
 default and so the reference's, or --solver pgs -- and semi-implicit Euler), the final position stage,
-reward/obs epilogue, TimeLimit + in-kernel auto-reset — 21 HIP launches per GPU per step (per substep a
-stage kernel and a solver kernel, then the final stage kernel).
+reward/obs epilogue, TimeLimit + in-kernel auto-reset.  With Newton at up to 24,576 envs per GPU (the 2-, 4-
+and 8-GPU shards) the step is ONE fused kernel launch (so100_fused_kernel: every wave runs its envs through
+all substeps with the state in registers); above that (the 1-GPU shard) and with PGS it is 21 launches per
+env chunk (per substep a stage kernel and a solver kernel, then the final stage kernel).
 Envs are sharded contiguously (global ids drive the seeds); there is no collective on the data path:
 only the barrier + max-over-ranks timing reduction around the timed region.
 Rank 0 prints ONE JSON line.  See DESIGN.md §6 for the roofline bytes and the CPU baseline.
@@ -37,6 +39,8 @@ SOLVER_BYTES_PER_CONTACT = 160 + 192
 # block + 48 of J read
 NEWTON_BYTES_PER_ENV = 4 * 100 + 48
 NEWTON_BYTES_PER_CONTACT = 4 * (12 + 48)
+# fused kernel: the boundary bytes of the env step (state/action in, state/outputs out) + the contact count
+FUSED_BYTES_PER_ENV = BYTES_PER_ENV_STEP + 4
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 CLOCK_HZ = 2.4e9             # MI355X peak engine clock (valu_busy uses it: a lower real clock only raises the share)
 SIMDS = 1024                 # 256 CUs x 4 SIMDs
@@ -97,11 +101,12 @@ def cpu_baseline(seconds, solver="newton"):
                       f"{cores} threads, {t_used:.1f}s)"}
 
 
-def load_traffic(n_envs, solver="pgs"):
+def load_traffic(n_envs, solver="pgs", fused=False):
     """(HBM bytes per solver launch of n_envs envs, VALU wave-instructions per env step) from the
     committed rocprofv3 PMC passes (profiles/pmc_traffic[_newton].json, tests/_pmc_traffic.py), or
     (None, None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if solver == "pgs" else f"pmc_traffic_{solver}.json")
+    name = "pmc_traffic_fused.json" if fused else ("pmc_traffic.json" if solver == "pgs" else f"pmc_traffic_{solver}.json")
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None, None
     try:
@@ -193,13 +198,18 @@ def main(argv=None):
     if rank == 0:
         env_steps = total * args.steps
         value = env_steps / elapsed
-        # the timed launches are chunk 0's (n0 envs), concurrent with the other chunks' (so100_chunk_info)
+        # the timed launches are chunk 0's (n0 envs), concurrent with the other chunks' (so100_chunk_info);
+        # fused: the one launch over all envs
+        fused = env.fused
         nchunks, n0 = env.chunk_info()
-        per_env, per_con = ((SOLVER_BYTES_PER_ENV, SOLVER_BYTES_PER_CONTACT) if args.solver == "pgs" else
-                            (NEWTON_BYTES_PER_ENV, NEWTON_BYTES_PER_CONTACT))
-        solver_bytes = n0 * (per_env + per_con * contacts_per_env)
+        if fused:
+            solver_bytes = n0 * FUSED_BYTES_PER_ENV
+        else:
+            per_env, per_con = ((SOLVER_BYTES_PER_ENV, SOLVER_BYTES_PER_CONTACT) if args.solver == "pgs" else
+                                (NEWTON_BYTES_PER_ENV, NEWTON_BYTES_PER_CONTACT))
+            solver_bytes = n0 * (per_env + per_con * contacts_per_env)
         achieved = solver_bytes / (solver_ms * 1e-3)
-        traffic, valu_insts = load_traffic(n0, args.solver)
+        traffic, valu_insts = load_traffic(n0, args.solver, fused)
         # VALU issue share of the timed run: insts x 2 cyc (wave64 on SIMD-32) / (step x 2.4 GHz x 1024 SIMDs)
         valu_busy = valu_insts * 2.0 / (step_ms * 1e-3 * CLOCK_HZ * SIMDS) if valu_insts else None
         line = {
@@ -210,21 +220,28 @@ def main(argv=None):
                                     f"({count} per GPU), joint-space ctrl, fp32 state, CubeToBin reward, "
                                     "auto-reset"),
                        "envs_total": total, "envs_per_gpu": count, "task": args.task, "substeps": 10,
-                       "solver": args.solver, "solver_iterations": env.model.iterations, "parallelism": f"env-sharded x{world}, no collectives",
+                       "solver": args.solver, "solver_iterations": env.model.iterations,
+                       "step_mode": "fused" if fused else "split",
+                       "parallelism": f"env-sharded x{world}, no collectives",
                        "actions": "U[-1,1]^6 pool resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic, "valu_busy": valu_busy,
-                         "kernel": f"so100_{args.solver}_kernel", "kernel_ms": solver_ms,
+                         "kernel": "so100_fused_kernel" if fused else f"so100_{args.solver}_kernel", "kernel_ms": solver_ms,
                          "bytes_per_launch": solver_bytes, "envs_per_launch": n0, "concurrent_chunks": nchunks,
                          "contacts_per_env": contacts_per_env,
                          "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
                          "boundary_bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "note": ((f"solver = primal Newton ({args.solver}): per env a 12x12 Hessian, its Cholesky "
+                         "note": (("fused step kernel: the whole env step per wave (10 x (kinematics, CRBA/RNE, "
+                                   "collision, constraint rows, primal Newton) + epilogue), state in registers, the "
+                                   "Newton rows handed over in registers, so its algorithmic HBM bytes are the "
+                                   "boundary's 412 B per env step; "
+                                   if fused else
+                                   f"solver = primal Newton ({args.solver}): per env a 12x12 Hessian, its Cholesky "
                                    "factor and an exact line search on 16 lanes, 2-3 Newton steps per substep; "
                                    if args.solver == "newton" else
                                    "solver = serial Gauss-Seidel chains per env, 100 sweeps; ") +
                                   "issue/latency-bound, not HBM-bound (DESIGN.md §3.5); traffic = measured PMC bytes per "
-                                  "solver launch; valu_busy = PMC SQ_INSTS_VALU per step x 2 cyc / (step time x 2.4 GHz x "
+                                  "launch of that kernel; valu_busy = PMC SQ_INSTS_VALU per step x 2 cyc / (step time x 2.4 GHz x "
                                   "1024 SIMDs): VALU issue share beside the HBM share (SURVEY §8d)")},
             "cpu_baseline": None,
         }

@@ -16,8 +16,8 @@
 #include "so100_device.h"
 
 namespace so100 {
-hipError_t launch_step(const DevModel*, int, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t, int,
-                       hipStream_t, hipEvent_t*);
+hipError_t launch_step(const DevModel*, int, int, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t,
+                       int, hipStream_t, hipEvent_t*);
 hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
 hipError_t launch_render(const DevModel*, const float4*, const int*, const uint32_t*, int, const float*,
                          const uint8_t*, const so100_camera&, int, int, int, uint8_t*, hipStream_t);
@@ -60,6 +60,10 @@ struct so100_env {
   DevModel* d_model;
   int nsubstep;
   int solver;                   // SO100_SOLVER_* of the model
+  int fused;                    // step mode: 1 fused, 0 split, -1 auto (fused up to fused_max envs; Newton only)
+  int fused_max;                // auto mode: the largest env count that runs fused
+  Workspace fws{};              // fused launches: the record header (contact counts) of all n envs, lazily
+  bool last_fused = false;      // the mode of the last step (so100_contact_count reads its record)
   std::vector<Chunk> chunks;
   hipEvent_t fork = nullptr;
   int task;
@@ -71,9 +75,9 @@ struct so100_env {
   int* r_body = nullptr;
   uint32_t* r_rgb = nullptr;
   int r_ntri = 0;
-  // profiling (so100_profile_enable): events[step][2 nsubstep + 2]
+  // profiling (so100_profile_enable): events[step][prof_per] (2 nsubstep + 2 split, 2 fused)
   std::vector<hipEvent_t> prof_ev;
-  int prof_cap = 0, prof_used = 0;
+  int prof_cap = 0, prof_used = 0, prof_per = 0;
   // step graphs: the 21 launches per chunk, the chunk fork and join, captured once per (buffers, flags,
   // substep parity) and replayed with one hipGraphLaunch when SO100_GRAPH=1.  A small LRU cache serves
   // callers that rotate a few action buffers (bench.py's pool of 16).  Off by default: the step is not
@@ -95,6 +99,16 @@ static void graph_destroy(StepGraph& g) {
 static void graph_free(so100_env* env) {
   for (StepGraph& g : env->graphs) graph_destroy(g);
   env->graphs.clear();
+}
+
+// The fused kernel implements the Newton solver only: PGS always takes the split launches.  Auto mode runs
+// fused up to fused_max envs per GPU: there every wave is resident at once and the split path's 21
+// chip-wide launch barriers cost most; at larger shards the split path's shorter launches pack the chip
+// better (measured crossover between 16,384 and 32,768 envs).
+constexpr int kFusedAutoMax = 24576;
+static bool step_is_fused(const so100_env* env) {
+  if (env->solver != SO100_SOLVER_NEWTON) return false;
+  return env->fused < 0 ? env->n <= env->fused_max : env->fused != 0;
 }
 
 static hipError_t free_chunks(so100_env* env) {
@@ -512,10 +526,18 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (e != hipSuccess) { fail_hip("so100_create: hipMalloc", e); return nullptr; }
   e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
-  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, h.solver, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
+  so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, h.solver, -1, kFusedAutoMax, {}, false, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
   if (const char* v = getenv("SO100_GRAPH")) env->use_graph = atoi(v) != 0;
+  if (const char* v = getenv("SO100_FUSED")) env->fused = atoi(v) < 0 ? -1 : atoi(v) != 0;   // A/B: 0 split, 1 fused
+  if (const char* v = getenv("SO100_FUSED_MAX")) env->fused_max = atoi(v);
   e = make_chunks(env, default_chunks(n_envs));
+  if (e == hipSuccess && env->solver == SO100_SOLVER_NEWTON) {
+    // the fused launches' record: only the header's contact count is used (640 B per env)
+    e = hipMalloc(&env->fws.hdr, (size_t)n_envs * so100::kHdrEnv * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(env->fws.hdr, 0, (size_t)n_envs * so100::kHdrEnv * sizeof(float));
+  }
   if (e != hipSuccess) {
+    if (env->fws.hdr) (void)hipFree(env->fws.hdr);
     (void)free_chunks(env);
     (void)hipFree(dm);
     delete env;
@@ -537,6 +559,7 @@ int so100_destroy(so100_env* env) {
   hipError_t e = hipFree(env->d_model);
   hipError_t e2 = free_chunks(env);
   if (e == hipSuccess) e = e2;
+  if (env->fws.hdr) (void)hipFree(env->fws.hdr);
   delete env;
   return e == hipSuccess ? 0 : fail_hip("so100_destroy", e);
 }
@@ -574,9 +597,15 @@ int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, con
 // The launches of one env step on stream s: chunk 0 on s, chunks 1.. on their own streams forked from s
 // and joined back to it.  The profiling events (if any) ride on chunk 0.
 static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags, hipStream_t s, hipEvent_t* ev) {
+  env->last_fused = step_is_fused(env);
+  if (env->last_fused) {
+    // one launch over all n envs (every wave runs its whole env step: no chunks needed to fill the gaps)
+    return so100::launch_step(env->d_model, env->nsubstep, env->solver, 1, env->fws, *b, env->n, env->task, flags,
+                              env->max_steps, env->base_seed, env->env_offset, s, ev);
+  }
   if (env->chunks.size() == 1) {
     Chunk& c = env->chunks[0];
-    return so100::launch_step(env->d_model, env->nsubstep, env->solver, c.ws, *b, c.count, env->task, flags, env->max_steps,
+    return so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, c.ws, *b, c.count, env->task, flags, env->max_steps,
                               env->base_seed, env->env_offset, s, ev);
   }
   hipError_t e = hipEventRecord(env->fork, s);
@@ -584,13 +613,13 @@ static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags
     Chunk& c = env->chunks[k];
     e = hipStreamWaitEvent(c.s, env->fork, 0);
     if (e == hipSuccess)
-      e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
+      e = so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
                              env->max_steps, env->base_seed, env->env_offset + c.start, c.s, nullptr);
     if (e == hipSuccess) e = hipEventRecord(c.done, c.s);
   }
   Chunk& c0 = env->chunks[0];
   if (e == hipSuccess)
-    e = so100::launch_step(env->d_model, env->nsubstep, env->solver, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
+    e = so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
                            env->base_seed, env->env_offset, s, ev);
   for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) e = hipStreamWaitEvent(s, env->chunks[k].done, 0);
   return e;
@@ -657,8 +686,7 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
   if ((flags & SO100_FLAG_AUTORESET) && !b->episode) return fail("so100_step: FLAG_AUTORESET needs episode");
   DeviceGuard g(env->device);
   hipEvent_t* ev = nullptr;
-  const int per = 2 * env->nsubstep + 2;
-  if (env->prof_used < env->prof_cap) ev = env->prof_ev.data() + (size_t)(env->prof_used++) * per;
+  if (env->prof_used < env->prof_cap) ev = env->prof_ev.data() + (size_t)(env->prof_used++) * env->prof_per;
   const hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   if (env->use_graph && !ev) {
@@ -674,7 +702,8 @@ int so100_profile_enable(so100_env* env, int max_steps) {
   if (max_steps < 0) return fail("so100_profile_enable: max_steps < 0");
   DeviceGuard g(env->device);
   profile_free(env);
-  const size_t count = (size_t)max_steps * (2 * env->nsubstep + 2);
+  env->prof_per = step_is_fused(env) ? 2 : 2 * env->nsubstep + 2;
+  const size_t count = (size_t)max_steps * env->prof_per;
   env->prof_ev.resize(count);
   for (size_t i = 0; i < count; i++) {
     hipError_t e = hipEventCreate(&env->prof_ev[i]);
@@ -689,13 +718,21 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
   DeviceGuard g(env->device);
   *solver_ms = *stage_ms = 0.0;
   *solver_launches = *stage_launches = 0;
-  const int per = 2 * env->nsubstep + 2;
+  const int per = env->prof_per;
   if (env->prof_used > 0) {
     hipError_t e = hipEventSynchronize(env->prof_ev[(size_t)env->prof_used * per - 1]);
     if (e != hipSuccess) return fail_hip("so100_profile_read", e);
   }
   for (int st = 0; st < env->prof_used; st++) {
     const hipEvent_t* ev = env->prof_ev.data() + (size_t)st * per;
+    if (per == 2) {                        // fused: the one launch contains the solves
+      float ms = 0.f;
+      hipError_t e = hipEventElapsedTime(&ms, ev[0], ev[1]);
+      if (e != hipSuccess) return fail_hip("so100_profile_read", e);
+      *solver_ms += ms;
+      (*solver_launches)++;
+      continue;
+    }
     for (int k = 0; k + 1 < per; k++) {   // launch order: stage, solver, stage, solver, ..., final stage
       float ms = 0.f;
       hipError_t e = hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
@@ -707,9 +744,29 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
   return 0;
 }
 
+int so100_set_step_mode(so100_env* env, int fused) {
+  if (!env) return fail("so100_set_step_mode: env is NULL");
+  if (fused < -1 || fused > 1) return fail("so100_set_step_mode: mode must be -1 (auto), 0 (split) or 1 (fused)");
+  if (env->prof_cap > 0) return fail("so100_set_step_mode: disable profiling first");
+  DeviceGuard g(env->device);
+  graph_free(env);                     // captured graphs hold the other mode's launches
+  env->fused = fused;
+  return 0;
+}
+
+int so100_step_mode(const so100_env* env) {
+  if (!env) return fail("so100_step_mode: env is NULL");
+  return step_is_fused(env) ? 1 : 0;
+}
+
 int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs) {
   if (!env) return fail("so100_chunk_info: env is NULL");
   if (nchunks) *nchunks = (int)env->chunks.size();
+  if (step_is_fused(env)) {     // one launch over all envs
+    if (nchunks) *nchunks = 1;
+    if (profiled_envs) *profiled_envs = env->n;
+    return 0;
+  }
   if (profiled_envs) *profiled_envs = env->chunks.empty() ? 0 : env->chunks[0].count;
   return 0;
 }
@@ -718,8 +775,12 @@ int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
   if (!env || !accum) return fail("so100_contact_count: bad arguments");
   DeviceGuard g(env->device);
   hipError_t e = hipSuccess;
-  for (const Chunk& c : env->chunks)
-    if (e == hipSuccess) e = so100::launch_contact_count(c.ws, c.count, accum, (hipStream_t)stream);
+  if (env->last_fused) {
+    if (env->fws.hdr) e = so100::launch_contact_count(env->fws, env->n, accum, (hipStream_t)stream);
+  } else {
+    for (const Chunk& c : env->chunks)
+      if (e == hipSuccess) e = so100::launch_contact_count(c.ws, c.count, accum, (hipStream_t)stream);
+  }
   return e == hipSuccess ? 0 : fail_hip("so100_contact_count", e);
 }
 

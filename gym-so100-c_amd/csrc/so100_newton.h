@@ -1,0 +1,463 @@
+// so100_newton.h — the constraint solve of one substep by MuJoCo's default solver: primal Newton
+// (engine_solver.c mj_solNewton; the reference's model sets no solver, so_arm100.xml:4), restated as
+// oracle/so100_oracle.c sol_newton (internal).
+//
+// Minimises c(a) = 1/2 (a - a_smooth)' M (a - a_smooth) + sum_rows s(J a - aref) over qacc a
+// (frictionloss: Huber; limits: one-sided quadratic; elliptic contacts: three cone zones), with the
+// Newton direction from the Cholesky factor of H = M + J' H_rows J and an exact line search.  Unlike PGS
+// the result does not depend on the sweep order or an iteration cap: it is the problem's unique
+// minimiser, reached in 2-6 iterations.
+//
+// Layout: one wave64 = 4 envs x 16 lanes (a DPP row per env, as the stage kernel).
+//   * lane d < 12 owns dof d: qacc, qacc_smooth, the search direction, row d of H and of its Cholesky
+//     factor (plus column d, collected during the factorisation for the back substitution), the
+//     frictionloss row of dof d and, for d < 6, the joint-limit row;
+//   * lane c owns contact c's block: jar, force, the 4x4 cone Hessian; the per-row scalar work of a
+//     cost/gradient/Hessian evaluation runs once per row, in parallel over the rows;
+//   * every dof lane holds J of its dof for contacts 0..kJReg-1 (one float4 per contact), so J x is a DPP
+//     row reduction and J' f, J' H J come from DPP row broadcasts.  Contacts kJReg.. (rare: 0.4 % of envs
+//     have more than 4) keep J in LDS (NewtonRows.jx) and take rolled loops with LDS broadcast reads and
+//     ds_bpermute row shuffles: 32 fewer VGPRs, which the fused kernel needs for 3 waves per SIMD.
+//
+// The problem arrives as NewtonRows, one lane's share of it.  The fused step kernel (so100_step.hip
+// so100_fused_kernel) hands it over in registers from the assembly of the same wave; the split path
+// stores it in the HBM record (so100_device.h NewtonHdr) and so100_newton_kernel loads it back.
+#pragma once
+#include "so100_common.h"
+
+namespace so100 {
+
+// One lane's share of a substep's Newton problem (its rows of the record).
+constexpr int kJReg = 8;                // contacts whose J rows stay in VGPRs
+constexpr int kJLds = kMaxCon - kJReg;  // the others' J rows: LDS [kJLds][SO100_NV] float4 per env
+struct NewtonRows {
+  float qs, warm, fr_aref;              // dof lanes: qacc_smooth, warmstart, frictionloss aref
+  float lim_s, lim_aref, lim_R;         // lanes < 6: joint-limit side (+-1, 0 = inactive), aref, R
+  float mrow[6];                        // lanes < 6: row of the arm's M (incl. armature)
+  float mcd;                            // lanes 6..11: the cube's diagonal mass
+  int ncon;                             // the env's contact count
+  float4 J[kJReg];                      // dof lanes: J of this dof, contact c's 4 rows (0 beyond ncon)
+  float4* jx;                           // LDS: J of contacts kJReg + i at jx[i * SO100_NV + dof] (0 beyond ncon)
+  float4 c_aref, c_R, c_mu;             // lane c < ncon: contact c's aref, R, (cone mu, friction0, friction1)
+};
+
+// MuJoCo mj_constraintUpdate (primal), elliptic contact block at jar: cost, force f = -dc/djar, and the
+// cost Hessian (upper triangle 00 01 02 03 11 12 13 22 23 33).  Oracle block_eval.
+DEV void cone_eval(const float* jar, const float* D, float mu, float fr0, float fr1, float& cost, float* f,
+                   float* h) {
+  const float fr[4] = {mu, fr0, fr0, fr1};
+  float U[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) U[k] = jar[k] * fr[k];
+  const float T = sqrtf(U[1] * U[1] + U[2] * U[2] + U[3] * U[3]);
+  const float N = U[0];
+  cost = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; k++) f[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 10; k++) h[k] = 0.f;
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) return;                          // top zone: no force
+  if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {                            // bottom zone: quadratic
+#pragma unroll
+    for (int k = 0; k < 4; k++) { f[k] = -D[k] * jar[k]; cost += 0.5f * D[k] * jar[k] * jar[k]; }
+    h[0] = D[0]; h[4] = D[1]; h[7] = D[2]; h[9] = D[3];
+    return;
+  }
+  // middle zone: c = 1/2 Dm (N - mu T)^2, g = d(N - mu T)/djar
+  const float Dm = D[0] / (mu * mu * (1.f + mu * mu)), NmT = N - mu * T, invT = 1.f / T;
+  float g[4];
+  g[0] = mu;
+#pragma unroll
+  for (int k = 1; k < 4; k++) g[k] = -mu * U[k] * fr[k] * invT;
+  cost = 0.5f * Dm * NmT * NmT;
+#pragma unroll
+  for (int k = 0; k < 4; k++) f[k] = -Dm * NmT * g[k];
+  const float c2 = -Dm * NmT * mu, invT3 = invT * invT * invT;
+  int q = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int l = k; l < 4; l++, q++) {
+      float v = Dm * g[k] * g[l];
+      if (k >= 1) v += c2 * fr[k] * fr[l] * ((k == l ? invT : 0.f) - U[k] * U[l] * invT3);
+      h[q] = v;
+    }
+}
+// frictionloss row (Huber) and joint-limit row (one-sided quadratic) at jar x
+DEV void fr_eval(float x, float fl, float R, float D, float& cost, float& f, float& h) {
+  if (x >= R * fl) { f = -fl; cost = fl * x - 0.5f * R * fl * fl; h = 0.f; }
+  else if (x <= -R * fl) { f = fl; cost = -fl * x - 0.5f * R * fl * fl; h = 0.f; }
+  else { f = -D * x; cost = 0.5f * D * x * x; h = D; }
+}
+DEV void lim_eval(float x, bool on, float D, float& cost, float& f, float& h) {
+  const bool act = on && x < 0.f;
+  f = act ? -D * x : 0.f;
+  cost = act ? 0.5f * D * x * x : 0.f;
+  h = act ? D : 0.f;
+}
+// h (upper triangle) times v
+DEV float4 sym4(const float* h, float4 v) {
+  return make_float4(h[0] * v.x + h[1] * v.y + h[2] * v.z + h[3] * v.w, h[1] * v.x + h[4] * v.y + h[5] * v.z + h[6] * v.w,
+                     h[2] * v.x + h[5] * v.y + h[7] * v.z + h[8] * v.w, h[3] * v.x + h[6] * v.y + h[8] * v.z + h[9] * v.w);
+}
+DEV float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+// (M x)[dof]: the dense arm block by row broadcasts, the cube's diagonal masses
+DEV float mul_m(const float* mrow, float mcd, float x) {
+  float acc = mcd * x;
+#pragma unroll
+  for (int j = 0; j < 6; j++) acc += mrow[j] * bcast_row(x, j);
+  return acc;
+}
+// J of contact c >= kJReg for this lane's dof (LDS; 0 on the non-dof lanes)
+DEV float4 jx_own(const NewtonRows& r, int c, int lane) {
+  return lane < SO100_NV ? r.jx[(c - kJReg) * SO100_NV + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// lane src of this lane's 16-lane row, src not a compile-time constant (ds_bpermute)
+DEV float4 shfl_row4(float4 v, int src) {
+  return make_float4(__shfl(v.x, src, kLanes), __shfl(v.y, src, kLanes), __shfl(v.z, src, kLanes), __shfl(v.w, src, kLanes));
+}
+// contact c's J x (4 rows) on lane c (the contacts present anywhere in the wave)
+DEV float4 contact_rows(const NewtonRows& rw, float x, int lane, int ncon_max) {
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int c = 0; c < kJReg; c++) {
+    if (c < ncon_max) {
+      const float4* J = rw.J;
+      const float v0 = rowsum16(J[c].x * x), v1 = rowsum16(J[c].y * x), v2 = rowsum16(J[c].z * x);
+      const float v3 = rowsum16(J[c].w * x);
+      if (lane == c) r = make_float4(v0, v1, v2, v3);
+    }
+  }
+  for (int c = kJReg; c < ncon_max; c++) {
+    const float4 j = jx_own(rw, c, lane);
+    const float v0 = rowsum16(j.x * x), v1 = rowsum16(j.y * x), v2 = rowsum16(j.z * x), v3 = rowsum16(j.w * x);
+    if (lane == c) r = make_float4(v0, v1, v2, v3);
+  }
+  return r;
+}
+
+// The split path's HBM record (so100_device.h NewtonHdr): the stage kernel stores a lane's rows, the
+// Newton kernel loads them back.  J is stored by the stage as it is computed (so100_step.hip).
+// (M goes first, as soon as the CRBA has it: the stage reuses its LDS for collision.)
+DEV void newton_mass_store(const Workspace& w, int e, int lane, const NewtonRows& r) {
+  float* hd = w.hdr + (size_t)e * kHdrEnv;
+  if (lane < 6) {
+#pragma unroll
+    for (int j = 0; j < 6; j++) hd[N_M + 6 * lane + j] = r.mrow[j];
+  } else if (lane < SO100_NV) {
+    hd[N_MC + lane - 6] = r.mcd;
+  }
+}
+DEV void newton_rows_store(const Workspace& w, int e, int lane, const NewtonRows& r) {
+  float* hd = w.hdr + (size_t)e * kHdrEnv;
+  float* crec = w.con + (size_t)e * kMaxCon * kConRec;
+  if (lane < r.ncon) {
+    float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
+    cs[0] = r.c_aref;
+    cs[1] = r.c_R;
+    cs[2] = r.c_mu;
+  }
+  if (lane < SO100_NV) { hd[N_QS + lane] = r.qs; hd[N_WARM + lane] = r.warm; hd[N_FRAREF + lane] = r.fr_aref; }
+  if (lane < 6) { hd[N_LIMS + lane] = r.lim_s; hd[N_LIMAREF + lane] = r.lim_aref; hd[N_LIMR + lane] = r.lim_R; }
+  if (lane == 0) hd[H_NCON] = __int_as_float(r.ncon);
+}
+
+// jx: the env's LDS area for the J rows of contacts kJReg.. (a barrier must follow before the solve)
+DEV void newton_rows_load(const Workspace& w, int e, int lane, bool valid, float4* jx, NewtonRows& r) {
+  const bool dof = lane < SO100_NV;
+  const float* __restrict__ hd = w.hdr + (size_t)e * kHdrEnv;
+  r.qs = dof ? hd[N_QS + lane] : 0.f;
+  r.warm = dof ? hd[N_WARM + lane] : 0.f;
+  r.fr_aref = dof ? hd[N_FRAREF + lane] : 0.f;
+  r.lim_s = 0.f; r.lim_aref = 0.f; r.lim_R = 1.f;
+  if (lane < 6) {
+    r.lim_s = hd[N_LIMS + lane];
+    r.lim_aref = hd[N_LIMAREF + lane];
+    r.lim_R = hd[N_LIMR + lane];
+  }
+#pragma unroll
+  for (int j = 0; j < 6; j++) r.mrow[j] = lane < 6 ? hd[N_M + 6 * lane + j] : 0.f;
+  r.mcd = (lane >= 6 && dof) ? hd[N_MC + lane - 6] : 0.f;
+  r.ncon = valid ? __float_as_int(hd[H_NCON]) : 0;
+  int ncon_max = r.ncon;
+  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
+  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
+  ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
+  const float* __restrict__ crec = w.con + (size_t)e * kMaxCon * kConRec;
+#pragma unroll
+  for (int c = 0; c < kJReg; c++) {
+    r.J[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < ncon_max && c < r.ncon && dof) r.J[c] = reinterpret_cast<const float4*>(crec + c * kConRec + kJOff)[lane];
+  }
+  for (int c = kJReg; c < ncon_max; c++) {
+    float4 j = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < r.ncon && dof) j = reinterpret_cast<const float4*>(crec + c * kConRec + kJOff)[lane];
+    if (dof) jx[(c - kJReg) * SO100_NV + lane] = j;
+  }
+  r.jx = jx;
+  r.c_aref = make_float4(0.f, 0.f, 0.f, 0.f);
+  r.c_R = make_float4(1.f, 1.f, 1.f, 1.f);
+  r.c_mu = make_float4(1.f, 1.f, 1.f, 0.f);
+  if (lane < r.ncon) {
+    const float4* cb = reinterpret_cast<const float4*>(crec + lane * kConRec);
+    r.c_aref = cb[0];
+    r.c_R = cb[1];
+    r.c_mu = cb[2];
+  }
+}
+
+// Solve one env's substep problem (its 16 lanes); returns qacc on the dof lanes.  dbg (the env's debug
+// row, or nullptr): the last substep writes qacc, frictionloss and contact normal forces, iterations.
+DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, float* dbg) {
+  const bool dof = lane < SO100_NV;
+  STAMP_DECL
+  STAMP(-1);
+  const float qs = r.qs, warm = r.warm, fr_aref = r.fr_aref;
+  const float fr_fl = dof ? m->fr_floss[lane] : 0.f;
+  const float fr_R = dof ? m->fr_R[lane] : 1.f;
+  const float fr_D = 1.f / fr_R;
+  const float lim_s = lane < 6 ? r.lim_s : 0.f, lim_aref = lane < 6 ? r.lim_aref : 0.f;
+  const float lim_D = lane < 6 ? 1.f / r.lim_R : 0.f;
+  const bool lim_on = lim_s != 0.f;
+  const float* mrow = r.mrow;
+  const float mcd = r.mcd;
+  const int ncon = r.ncon;
+  int ncon_max = ncon;
+  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
+  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
+  ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
+  const float4* J = r.J;                  // contacts < kJReg; the others: r.jx (LDS)
+  const bool own = lane < ncon;                   // lane c owns contact c
+  float c_aref[4] = {0.f, 0.f, 0.f, 0.f}, c_D[4] = {1.f, 1.f, 1.f, 1.f}, c_mu = 1.f, c_fr0 = 1.f, c_fr1 = 1.f;
+  if (own) {
+    c_aref[0] = r.c_aref.x; c_aref[1] = r.c_aref.y; c_aref[2] = r.c_aref.z; c_aref[3] = r.c_aref.w;
+    c_D[0] = 1.f / r.c_R.x; c_D[1] = 1.f / r.c_R.y; c_D[2] = 1.f / r.c_R.z; c_D[3] = 1.f / r.c_R.w;
+    c_mu = r.c_mu.x; c_fr0 = r.c_mu.y; c_fr1 = r.c_mu.z;
+  }
+
+  // cost of the rows this lane owns at (frictionloss / limit jar of its dof, contact jar)
+  auto rows_cost = [&](float xfr, float xlim, const float* xc) {
+    float cost = 0.f, f, h, cc, fc[4], hc[10];
+    if (dof) { fr_eval(xfr, fr_fl, fr_R, fr_D, cc, f, h); cost += cc; }
+    lim_eval(xlim, lim_on, lim_D, cc, f, h);
+    cost += cc;
+    if (own) { cone_eval(xc, c_D, c_mu, c_fr0, c_fr1, cc, fc, hc); cost += cc; }
+    return cost;
+  };
+
+  STAMP(0);
+  // ---------------- start: the warmstart if its cost is below qacc_smooth's (mj_fwdConstraint)
+  float qacc, jc[4];
+  {
+    const float4 jw = contact_rows(r, warm, lane, ncon_max), js = contact_rows(r, qs, lane, ncon_max);
+    const float xw[4] = {jw.x - c_aref[0], jw.y - c_aref[1], jw.z - c_aref[2], jw.w - c_aref[3]};
+    const float xs[4] = {js.x - c_aref[0], js.y - c_aref[1], js.z - c_aref[2], js.w - c_aref[3]};
+    const float ew = warm - qs;
+    const float gw = 0.5f * rowsum16(dof ? ew * mul_m(mrow, mcd, ew) : 0.f);
+    const float cw = gw + rowsum16(rows_cost(warm - fr_aref, lim_s * warm - lim_aref, xw));
+    const float cs = rowsum16(rows_cost(qs - fr_aref, lim_s * qs - lim_aref, xs));
+    const bool use_w = cw < cs;
+    qacc = use_w ? warm : qs;
+#pragma unroll
+    for (int k = 0; k < 4; k++) jc[k] = use_w ? xw[k] : xs[k];
+  }
+  float ev = qacc - qs;                                   // a - a_smooth
+  float Me = mul_m(mrow, mcd, ev);
+  float jfr = qacc - fr_aref, jlim = lim_s * qacc - lim_aref;
+  float gauss = 0.5f * rowsum16(dof ? ev * Me : 0.f);
+  float cost = gauss + rowsum16(rows_cost(jfr, jlim, jc));
+  const float scale = m->pgs_scale, tolerance = m->tolerance;
+  STAMP(1);
+
+  bool done = !valid;
+  int iters = 0;
+  float last_impr = 0.f;
+  for (int it = 0; it < m->iterations; it++) {
+    if (__ballot(!done) == 0ull) break;
+    if (!done) {
+      // ---- rows at the current point: forces and Hessians
+      float c0, f_fr = 0.f, h_fr = 0.f, f_lim, h_lim, fc[4], hc[10];
+      if (dof) fr_eval(jfr, fr_fl, fr_R, fr_D, c0, f_fr, h_fr);
+      lim_eval(jlim, lim_on, lim_D, c0, f_lim, h_lim);
+      cone_eval(jc, c_D, c_mu, c_fr0, c_fr1, c0, fc, hc);
+      if (!own) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) fc[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 10; k++) hc[k] = 0.f;
+      }
+      // ---- gradient M (a - a_smooth) - J' f
+      float grad = Me - f_fr - lim_s * f_lim;
+#pragma unroll
+      for (int c = 0; c < kJReg; c++) {
+        if (c < ncon_max) grad -= dot4(J[c], bcast_row4(make_float4(fc[0], fc[1], fc[2], fc[3]), c));
+      }
+      for (int c = kJReg; c < ncon_max; c++)
+        grad -= dot4(jx_own(r, c, lane), shfl_row4(make_float4(fc[0], fc[1], fc[2], fc[3]), c));
+      grad = dof ? grad : 0.f;
+      const float gn = sqrtf(rowsum16(grad * grad));
+      STAMP(2);
+      if (scale * gn < tolerance) {
+        done = true;
+      } else {
+        // ---- Hessian row `lane`: M + diag(frictionloss, limit) + sum_c J_c' H_c J_c
+        float H[SO100_NV];
+#pragma unroll
+        for (int j = 0; j < SO100_NV; j++) {
+          H[j] = j < 6 ? mrow[j] : 0.f;
+          if (lane == j) H[j] += mcd + h_fr + h_lim;
+        }
+#pragma unroll
+        for (int c = 0; c < kJReg; c++) {
+          // (skipping contacts whose Hessian is zero in every env of the wave, or zero J columns, measured
+          // 2% slower: the uniform branches cost more than the DPP/FMA they save)
+          if (c < ncon_max) {
+            float hb[10];
+#pragma unroll
+            for (int k = 0; k < 10; k++) hb[k] = bcast_row(hc[k], c);
+            const float4 w = sym4(hb, J[c]);
+#pragma unroll
+            for (int j = 0; j < SO100_NV; j++) H[j] += dot4(w, bcast_row4(J[c], j));
+          }
+        }
+        for (int c = kJReg; c < ncon_max; c++) {       // J from LDS: one broadcast read per dof
+          float hb[10];
+#pragma unroll
+          for (int k = 0; k < 10; k++) hb[k] = __shfl(hc[k], c, kLanes);
+          const float4* jc_l = r.jx + (c - kJReg) * SO100_NV;
+          const float4 w = sym4(hb, jx_own(r, c, lane));
+#pragma unroll
+          for (int j = 0; j < SO100_NV; j++) H[j] += dot4(w, jc_l[j]);
+        }
+        STAMP(3);
+        // ---- Cholesky H = L L' (lane i: row i of L; lc: column i, gathered from the broadcasts)
+        float lc[SO100_NV], dinv = 1.f;
+#pragma unroll
+        for (int k = 0; k < SO100_NV; k++) {
+          const float dkk = bcast_row(H[k], k);
+          const float Lkk = sqrtf(fmaxf(dkk, kMinVal));
+          const float inv = 1.f / Lkk;
+          const float lik = H[k] * inv;
+          if (lane >= k) H[k] = lik;
+          if (lane == k) dinv = inv;
+#pragma unroll
+          for (int j = k + 1; j < SO100_NV; j++) {
+            const float ljk = bcast_row(lik, j);
+            if (lane > k) H[j] -= lik * ljk;
+            if (lane == k) lc[j] = ljk;
+          }
+        }
+        // ---- search direction s = -H^-1 grad: L y = -grad, L' s = y
+        float y = -grad;
+#pragma unroll
+        for (int k = 0; k < SO100_NV; k++) {
+          const float yk = bcast_row(y * dinv, k);
+          if (lane == k) y = yk;
+          else if (lane > k) y -= H[k] * yk;
+        }
+        float sv = y;
+#pragma unroll
+        for (int k = SO100_NV - 1; k >= 0; k--) {
+          const float xk = bcast_row(sv * dinv, k);
+          if (lane == k) sv = xk;
+          else if (lane < k) sv -= lc[k] * xk;
+        }
+        sv = dof ? sv : 0.f;
+        STAMP(4);
+        // ---- exact line search on c(a + alpha s): safeguarded 1-D Newton on c'(alpha) (oracle line_search)
+        const float Ms = mul_m(mrow, mcd, sv);
+        const float A1 = rowsum16(dof ? Ms * ev : 0.f), A2 = rowsum16(dof ? Ms * sv : 0.f);
+        const float4 js4 = contact_rows(r, sv, lane, ncon_max);
+        const float jsc[4] = {js4.x, js4.y, js4.z, js4.w};
+        const float sfr = sv, slim = lim_s * sv;
+        auto derivs = [&](float al, float& d1, float& d2) {
+          float l1 = 0.f, l2 = 0.f, cc, f, h;
+          if (dof) { fr_eval(jfr + al * sfr, fr_fl, fr_R, fr_D, cc, f, h); l1 -= f * sfr; l2 += h * sfr * sfr; }
+          lim_eval(jlim + al * slim, lim_on, lim_D, cc, f, h);
+          l1 -= f * slim; l2 += h * slim * slim;
+          if (own) {
+            float x[4], fcc[4], hcc[10];
+#pragma unroll
+            for (int k = 0; k < 4; k++) x[k] = jc[k] + al * jsc[k];
+            cone_eval(x, c_D, c_mu, c_fr0, c_fr1, cc, fcc, hcc);
+            const float4 v = make_float4(jsc[0], jsc[1], jsc[2], jsc[3]);
+            l1 -= fcc[0] * jsc[0] + fcc[1] * jsc[1] + fcc[2] * jsc[2] + fcc[3] * jsc[3];
+            l2 += dot4(v, sym4(hcc, v));
+          }
+          d1 = rowsum16(l1) + A1 + al * A2;
+          d2 = rowsum16(l2) + A2;
+        };
+        // c'(0) from the forces already evaluated at the current point (= derivs(0)'s d1)
+        float d10;
+        {
+          float l1 = 0.f;
+          l1 -= f_fr * sfr;
+          l1 -= f_lim * slim;
+          l1 -= fc[0] * jsc[0] + fc[1] * jsc[1] + fc[2] * jsc[2] + fc[3] * jsc[3];
+          d10 = rowsum16(l1) + A1;
+        }
+        float alpha = 0.f;
+        if (d10 < 0.f) {
+          // fp32 stops (oracle LS_TOL / LS_STEP): MuJoCo's ls_tolerance 0.01 on |c'|, or a relative step 1e-4
+          const float tol_ls = 1e-2f * -d10;
+          float lo = 0.f, hi = -1.f;
+          alpha = 1.f;
+          for (int ls = 0; ls < 50; ls++) {
+            float d1, d2;
+            derivs(alpha, d1, d2);
+            if (fabsf(d1) <= tol_ls) break;
+            if (d1 < 0.f) lo = alpha; else hi = alpha;
+            float nxt = d2 > 0.f ? alpha - d1 / d2 : -1.f;
+            if (hi >= 0.f) { if (!(nxt > lo && nxt < hi)) nxt = 0.5f * (lo + hi); }
+            else if (!(nxt > lo)) nxt = 2.f * alpha;
+            if (nxt == alpha) break;
+            if (fabsf(nxt - alpha) <= 1e-4f * fabsf(alpha)) { alpha = nxt; break; }
+            alpha = nxt;
+          }
+        }
+        iters = it + 1;
+        STAMP(5);
+        if (alpha == 0.f) {
+          done = true;
+        } else {
+          // ---- move; the new cost gives MuJoCo's improvement test
+          qacc += alpha * sv;
+          ev += alpha * sv;
+          Me += alpha * Ms;
+          jfr += alpha * sfr;
+          jlim += alpha * slim;
+#pragma unroll
+          for (int k = 0; k < 4; k++) jc[k] += alpha * jsc[k];
+          gauss += alpha * A1 + 0.5f * alpha * alpha * A2;
+          const float nc = gauss + rowsum16(rows_cost(jfr, jlim, jc));
+          const float improvement = scale * (cost - nc);
+          cost = nc;
+          last_impr = improvement;
+          // MuJoCo's test, and the fp32 relative one (oracle NEWTON_RELTOL): 1e-8 is below fp32 resolution
+          if (improvement < tolerance || improvement < 1e-6f * scale * fabsf(cost)) done = true;
+        }
+        STAMP(6);
+      }
+    }
+  }
+
+  STAMP(7);
+  if (valid && dbg) {
+#ifdef SO100_STAMPS
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) dbg[88 + k] = (float)st_acc_[k];
+    }
+#endif
+    float cc, f_fr, h, fc[4], hc[10];
+    fr_eval(jfr, fr_fl, fr_R, fr_D, cc, f_fr, h);
+    cone_eval(jc, c_D, c_mu, c_fr0, c_fr1, cc, fc, hc);
+    if (dof) { dbg[4 + lane] = qacc; dbg[76 + lane] = f_fr; }
+    if (lane < kMaxCon) dbg[32 + lane] = own ? fc[0] : 0.f;
+    if (lane == 0) { dbg[1] = (float)iters; dbg[2] = last_impr; }
+  }
+  return qacc;
+}
+
+}  // namespace so100

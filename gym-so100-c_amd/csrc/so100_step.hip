@@ -20,6 +20,7 @@
 #include "so100.h"
 #include "so100_common.h"
 #include "so100_kin.h"
+#include "so100_newton.h"
 
 namespace so100 {
 
@@ -1793,53 +1794,50 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
 #ifndef SO100_STAGE_WAVES
 #define SO100_STAGE_WAVES 3      // waves per SIMD the stage kernel's register budget is sized for
 #endif
-// Substep stage kernel (one wave = 4 envs x 16 lanes).
-//   kMode 0: substep 0 — position/velocity stages and constraint assembly on the stored state;
-//   kMode 1: Euler with the previous substep's solver output, then the same assembly;
-//   kMode 2: Euler, then the mj_step1 position stage and the task epilogue (reward, obs, autoreset).
-// Assembly writes the solver's per-env record (Workspace) that so100_pgs_kernel consumes.
-template <int kMode, int kSolver>
-__global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kernel(StageArgs args) {
-  __shared__ EnvShared shm[kEnvsPerBlock];
-  const DevModel* __restrict__ m = args.m;
-  const int tid = threadIdx.x;
-  const int grp = tid >> 4;
-  const int lane = tid & 15;
-  const int env = blockIdx.x * kEnvsPerBlock + grp;
-  const bool valid = env < args.n;
-  const int e = valid ? env : 0;          // clamp loads for the tail group; stores are guarded
-  EnvShared& sh = shm[grp];
-  const so100_buffers& B = args.b;
 
-  // ---------------- prologue: state -> registers
-  float qpos_r = (lane < SO100_NQ) ? B.qpos[(size_t)e * SO100_NQ + lane] : 0.f;
-  float qvel_r = (lane < SO100_NV) ? B.qvel[(size_t)e * SO100_NV + lane] : 0.f;
-  float warm_r = (lane < SO100_NV) ? B.qacc_warmstart[(size_t)e * SO100_NV + lane] : 0.f;
-  float mscale = 1.f, fscale = 1.f, sigma = 0.f;
+// prologue: the env's state -> registers (lane k: qpos[k], qvel[k], warmstart[k]), DR parameters, counters
+DEV void load_state(const StageArgs& args, int lane, int e, float& qpos_r, float& qvel_r, float& warm_r, float& mscale,
+                    float& fscale, float& sigma, int& elapsed0, uint32_t& episode0) {
+  const so100_buffers& B = args.b;
+  qpos_r = (lane < SO100_NQ) ? B.qpos[(size_t)e * SO100_NQ + lane] : 0.f;
+  qvel_r = (lane < SO100_NV) ? B.qvel[(size_t)e * SO100_NV + lane] : 0.f;
+  warm_r = (lane < SO100_NV) ? B.qacc_warmstart[(size_t)e * SO100_NV + lane] : 0.f;
+  mscale = 1.f; fscale = 1.f; sigma = 0.f;
   if ((args.flags & SO100_FLAG_DR) && B.dr_params) {
     mscale = B.dr_params[(size_t)e * 4 + 0];
     fscale = B.dr_params[(size_t)e * 4 + 1];
     sigma = B.dr_params[(size_t)e * 4 + 2];
   }
-  const int elapsed0 = B.elapsed ? B.elapsed[e] : 0;
-  const uint32_t episode0 = B.episode ? B.episode[e] : 0u;
-  const float h = m->timestep;
+  elapsed0 = B.elapsed ? B.elapsed[e] : 0;
+  episode0 = B.episode ? B.episode[e] : 0u;
+}
+
+// control (the same every substep of the env step: elapsed/episode only change in the epilogue): the
+// action (+ DR noise) un-normalised into sh.ctrl; the EE variant's mocap pose into sh.mocap
+DEV void set_controls(const StageArgs& args, EnvShared& sh, int lane, int e, float sigma, int elapsed0, uint32_t episode0) {
+  const DevModel* __restrict__ m = args.m;
+  const so100_buffers& B = args.b;
+  if (lane < 6) {
+    float a = B.action[(size_t)e * 6 + lane];
+    if (sigma > 0.f)
+      a += sigma * hash_normal(splitmix64(args.base_seed ^ ((uint64_t)(e + args.env_offset) << 40) ^
+                                          ((uint64_t)episode0 << 20) ^ (uint64_t)(elapsed0 * 8 + lane)));
+    sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
+  }
+  if (m->ee && lane < 7) sh.mocap[lane] = B.mocap ? B.mocap[(size_t)e * 7 + lane] : m->mocap0[lane];
+}
+
+// One substep's position/velocity stages and constraint assembly on the state in registers (after the
+// previous substep's Euler): kinematics, CRBA/RNE, actuation, collision, the frictionloss / limit /
+// contact rows.  Newton: the rows go to nr (kFused: kept in registers for newton_solve; split: stored to the
+// HBM record); PGS: the solver record of so100_pgs_kernel.
+template <int kSolver, bool kFused>
+DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int env, int e, bool valid, float qpos_r,
+                  float qvel_r, float warm_r, float mscale, float fscale, int sub, NewtonRows& nr) {
+  const DevModel* __restrict__ m = args.m;
+  const so100_buffers& B = args.b;
   SSTAMP_DECL
   SSTAMP(-1);
-
-  if (kMode != 0) euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
-  SSTAMP(0);
-
-  if (kMode != 2) {
-    // control (the same every substep of the env step: elapsed/episode only change in the epilogue)
-    if (lane < 6) {
-      float a = B.action[(size_t)e * 6 + lane];
-      if (sigma > 0.f)
-        a += sigma * hash_normal(splitmix64(args.base_seed ^ ((uint64_t)(e + args.env_offset) << 40) ^
-                                            ((uint64_t)episode0 << 20) ^ (uint64_t)(elapsed0 * 8 + lane)));
-      sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
-    }
-    if (m->ee && lane < 7) sh.mocap[lane] = B.mocap ? B.mocap[(size_t)e * 7 + lane] : m->mocap0[lane];
     // ---------------- S1: stage state in LDS
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
     if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
@@ -1851,18 +1849,15 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     __syncthreads();
     dynamics_par(m, sh, lane, mscale);
     __syncthreads();
-    if (kSolver == SO100_SOLVER_NEWTON && valid) {
+    if constexpr (kSolver == SO100_SOLVER_NEWTON) {
       // the Newton solver works with M itself: arm rows from the CRBA scratch (which collision reuses),
       // the cube's diagonal masses
-      float* hd = args.w.hdr + (size_t)e * kHdrEnv;
-      if (lane < 6) {
 #pragma unroll
-        for (int j = 0; j < 6; j++) hd[N_M + 6 * lane + j] = sh.ser.M[lane][j];
-      } else if (lane < 9) {
-        hd[N_MC + lane - 6] = m->cube_mass * mscale;
-      } else if (lane < SO100_NV) {
-        hd[N_MC + lane - 6] = m->cube_inertia[lane - 9] * mscale;
-      }
+      for (int j = 0; j < 6; j++) nr.mrow[j] = lane < 6 ? sh.ser.M[lane][j] : 0.f;
+      nr.mcd = 0.f;
+      if (lane >= 6 && lane < 9) nr.mcd = m->cube_mass * mscale;
+      else if (lane >= 9 && lane < SO100_NV) nr.mcd = m->cube_inertia[lane - 9] * mscale;
+      if (!kFused && valid) newton_mass_store(args.w, e, lane, nr);   // split path: the record, now
     }
     SSTAMP(1);
     // ---------------- S3: collision: hulls vs the table (lane k = hull k), box-hull pairs by MPR
@@ -1973,17 +1968,24 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
     if (lim_on) cost_part += 0.5f * lim_R * lim_f * lim_f + lim_f * (lim_s * qs_r - lim_aref);
 
     if constexpr (kSolver == SO100_SOLVER_NEWTON) {
-      // ---------------- Newton record (so100_newton.hip builds its gradients and Hessians from it):
-      // J rows (-> HBM) and J qvel (lane c keeps contact c's), per contact aref, R and the cone
-      // coefficients, the header with qacc_smooth, the warmstart, the frictionloss and limit rows
+      // ---------------- Newton rows (so100_newton.h): J (lane = dof) and J qvel (lane c keeps contact c's),
+      // per contact aref, R and the cone coefficients, qacc_smooth, the warmstart, the frictionloss and
+      // limit rows.  Fused: handed to newton_solve in registers; split: stored to the HBM record.
       float cVn[4] = {0.f, 0.f, 0.f, 0.f};
+      float4 jhi[kJLds];          // fused: J of contacts kJReg.., to LDS once every contact_jac has run
 #pragma unroll
       for (int c = 0; c < kMaxCon; c++) {
+        if (c < kJReg) nr.J[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        else jhi[c - kJReg] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c < ncon_max) {
           float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
           if (c < ncon && lane < SO100_NV) {
             J = contact_jac(m, sh, c, lane);
-            reinterpret_cast<float4*>(crec + c * kConRec + kJOff)[lane] = J;
+            if constexpr (!kFused) reinterpret_cast<float4*>(crec + c * kConRec + kJOff)[lane] = J;
+          }
+          if constexpr (kFused) {
+            if (c < kJReg) nr.J[c] = J;
+            else jhi[c - kJReg] = J;
           }
           const bool mine = lane == c;
           const float v0 = rowsum16(J.x * qvel_r), v1 = rowsum16(J.y * qvel_r);
@@ -1992,7 +1994,23 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
           cVn[2] = mine ? v2 : cVn[2]; cVn[3] = mine ? v3 : cVn[3];
         }
       }
+      if constexpr (kFused) {
+        // the J rows of contacts kJReg.. go to the contact-geometry area of LDS, dead from here to the next
+        // substep's collision (ConArea is exactly kJLds x 12 float4)
+        float4* jx = reinterpret_cast<float4*>(&sh.con[0]);
+        if (kJReg < ncon_max) {
+          __syncthreads();
+#pragma unroll
+          for (int c = kJReg; c < kMaxCon; c++)
+            if (c < ncon_max && lane < SO100_NV) jx[(c - kJReg) * SO100_NV + lane] = jhi[c - kJReg];
+          __syncthreads();
+        }
+        nr.jx = jx;
+      }
       SSTAMP(3);
+      nr.c_aref = make_float4(0.f, 0.f, 0.f, 0.f);
+      nr.c_R = make_float4(1.f, 1.f, 1.f, 1.f);
+      nr.c_mu = make_float4(1.f, 1.f, 1.f, 0.f);
       if (lane < ncon) {
         const int p = sh.con_pair[lane];
         const float dist = sh.con_dist[lane];
@@ -2005,29 +2023,33 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
         R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
         R[2] = R[1];
         R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
-        float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
-        cs[0] = make_float4(-Bd * cVn[0] - K * imp * (dist - m->pair_margin[p]), -Bd * cVn[1], -Bd * cVn[2], -Bd * cVn[3]);
-        cs[1] = make_float4(R[0], R[1], R[2], R[3]);
-        cs[2] = make_float4(mu0 * sqrtf(R[1] / R[0]), mu0, mu1, 0.f);
+        nr.c_aref = make_float4(-Bd * cVn[0] - K * imp * (dist - m->pair_margin[p]), -Bd * cVn[1], -Bd * cVn[2], -Bd * cVn[3]);
+        nr.c_R = make_float4(R[0], R[1], R[2], R[3]);
+        nr.c_mu = make_float4(mu0 * sqrtf(R[1] / R[0]), mu0, mu1, 0.f);
       }
       SSTAMP(4);
+      nr.qs = lane < SO100_NV ? qs_r : 0.f;
+      nr.warm = lane < SO100_NV ? warm_r : 0.f;
+      nr.fr_aref = lane < SO100_NV ? fr_aref : 0.f;
+      nr.lim_s = lim_on ? lim_s : 0.f;
+      nr.lim_aref = lim_aref;
+      nr.lim_R = lim_R;
+      nr.ncon = ncon;
       if (valid) {
-        float* hd = args.w.hdr + (size_t)e * kHdrEnv;
-        if (lane < SO100_NV) { hd[N_QS + lane] = qs_r; hd[N_WARM + lane] = warm_r; hd[N_FRAREF + lane] = fr_aref; }
-        if (lane < 6) { hd[N_LIMS + lane] = lim_on ? lim_s : 0.f; hd[N_LIMAREF + lane] = lim_aref; hd[N_LIMR + lane] = lim_R; }
-        if (lane == 0) hd[H_NCON] = __int_as_float(ncon);
-        if (kMode == 1) {
-          if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
-          if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
+        if constexpr (!kFused) {
+          newton_rows_store(args.w, e, lane, nr);
+        } else {
+          // the contact counter (so100_contact_count) reads the last substep's count from the record
+          if (lane == 0 && sub == m->nsubstep - 1) args.w.hdr[(size_t)e * kHdrEnv + H_NCON] = __int_as_float(ncon);
         }
         SSTAMP(5);
 #ifdef SO100_STAGE_STAMPS
-        if (B.debug && args.sub == m->nsubstep - 1 && lane == 0) {
+        if (B.debug && sub == m->nsubstep - 1 && lane == 0) {
 #pragma unroll
           for (int k = 0; k < 8; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
         }
 #endif
-        if (B.debug && args.sub == m->nsubstep - 1) {
+        if (B.debug && sub == m->nsubstep - 1) {
           float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
           if (lane < kMaxCon) {
             dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
@@ -2209,19 +2231,15 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
         }
         if (k == 0) hd[H_NCON] = __int_as_float(ncon);
       }
-      if (kMode == 1) {
-        if (lane < SO100_NQ) B.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
-        if (lane < SO100_NV) B.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
-      }
       SSTAMP(5);
 #ifdef SO100_STAGE_STAMPS
-      if (B.debug && args.sub == m->nsubstep - 1 && lane == 0) {
+      if (B.debug && sub == m->nsubstep - 1 && lane == 0) {
 #pragma unroll
         for (int k = 0; k < 8; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
       }
 #endif
       // debug: contact set of the last substep (forces / iterations come from the solver kernel)
-      if (B.debug && args.sub == m->nsubstep - 1) {
+      if (B.debug && sub == m->nsubstep - 1) {
         float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
         if (lane < kMaxCon) {
           dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
@@ -2234,9 +2252,14 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
         }
       }
     }
-    return;
-  }
+}
 
+// The env step's epilogue (kMode 2 / the fused kernel's tail): the mj_step1 position stage (sites, contact
+// set), reward, obs, TimeLimit, divergence, auto-reset, and the state store.
+DEV void final_stage(const StageArgs& args, EnvShared& sh, int lane, int grp, int env, int e, bool valid, float qpos_r,
+                     float qvel_r, float warm_r, int elapsed0, uint32_t episode0) {
+  const DevModel* __restrict__ m = args.m;
+  const so100_buffers& B = args.b;
   // ---------------- final position stage (mj_step1): sites + contact set for reward / obs
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
@@ -2359,6 +2382,142 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
   }
 }
 
+
+// Substep stage kernel of the split path (one wave = 4 envs x 16 lanes).
+//   kMode 0: substep 0 — position/velocity stages and constraint assembly on the stored state;
+//   kMode 1: Euler with the previous substep's solver output, then the same assembly;
+//   kMode 2: Euler, then the mj_step1 position stage and the task epilogue (reward, obs, autoreset).
+// Assembly writes the solver's per-env record (Workspace) that so100_pgs_kernel / so100_newton_kernel consume.
+template <int kMode, int kSolver>
+__global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kernel(StageArgs args) {
+  __shared__ EnvShared shm[kEnvsPerBlock];
+  const int tid = threadIdx.x;
+  const int grp = tid >> 4;
+  const int lane = tid & 15;
+  const int env = blockIdx.x * kEnvsPerBlock + grp;
+  const bool valid = env < args.n;
+  const int e = valid ? env : 0;          // clamp loads for the tail group; stores are guarded
+  EnvShared& sh = shm[grp];
+  float qpos_r, qvel_r, warm_r, mscale, fscale, sigma;
+  int elapsed0;
+  uint32_t episode0;
+  load_state(args, lane, e, qpos_r, qvel_r, warm_r, mscale, fscale, sigma, elapsed0, episode0);
+  if (kMode != 0) euler_update(sh, lane, args.m->timestep, warm_r, qpos_r, qvel_r);
+  if constexpr (kMode != 2) {
+    set_controls(args, sh, lane, e, sigma, elapsed0, episode0);
+    NewtonRows nr;
+    assemble<kSolver, false>(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale, fscale, args.sub, nr);
+    if (kMode == 1 && valid) {
+      if (lane < SO100_NQ) args.b.qpos[(size_t)env * SO100_NQ + lane] = qpos_r;
+      if (lane < SO100_NV) args.b.qvel[(size_t)env * SO100_NV + lane] = qvel_r;
+    }
+  } else {
+    final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+  }
+}
+
+#ifndef SO100_LAUNDER
+#define SO100_LAUNDER 2
+#endif
+#ifndef SO100_LAUNDER_IDS
+#define SO100_LAUNDER_IDS 1
+#endif
+#ifndef SO100_FUSED_WAVES
+#define SO100_FUSED_WAVES 3
+#endif
+// The whole env step in one launch (Newton solver, the default): each wave runs its 4 envs through the 10
+// substeps — Euler, assembly, the Newton solve with the rows handed over in registers (no HBM record) —
+// and the epilogue, with the state in registers throughout.  The split path's 21 launches end every
+// substep at the slowest wave of the chip; here a wave only waits for itself.
+// Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
+// functions on the same values.
+__global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kernel(const DevModel* __restrict__ model,
+                                                                                  StageArgs args) {
+  // the model as a noalias kernel argument: no store of the step can clobber it, so its uniform loads stay
+  // scalar (s_load) after the substeps' global stores (through args.m they became vector loads)
+  args.m = model;
+#ifdef SO100_TIMELINE
+  // diagnostic build: wave start / end (s_memrealtime) and shader cycles in assembly / Newton / epilogue
+  const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t tl_acc[3] = {0, 0, 0}, tl_prev = 0;
+#define TL_MARK(slot)                                                                            \
+  do {                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if ((slot) >= 0) tl_acc[(slot)] += t_ - tl_prev;                                             \
+    tl_prev = t_;                                                                                \
+  } while (0)
+#else
+#define TL_MARK(slot) do {} while (0)
+#endif
+  __shared__ EnvShared shm[kEnvsPerBlock];
+  const int tid = threadIdx.x;
+  const int grp0 = tid >> 4;
+  const int lane0 = tid & 15;
+  const int env0 = blockIdx.x * kEnvsPerBlock + grp0;
+  const int e0 = env0 < args.n ? env0 : 0;
+  {
+  const int grp = grp0, lane = lane0, env = env0, e = e0;
+  const bool valid = env < args.n;
+  EnvShared& sh = shm[grp];
+  float qpos_r, qvel_r, warm_r, mscale, fscale, sigma;
+  int elapsed0;
+  uint32_t episode0;
+  load_state(args, lane, e, qpos_r, qvel_r, warm_r, mscale, fscale, sigma, elapsed0, episode0);
+  set_controls(args, sh, lane, e, sigma, elapsed0, episode0);
+  const int nsub = args.m->nsubstep;
+  const float h = args.m->timestep;
+  for (int sub = 0; sub < nsub; sub++) {
+#if SO100_LAUNDER_IDS
+    // the lane / env ids laundered per substep too: what derives from them (masks, addresses, per-lane
+    // model values) is recomputed in each substep instead of hoisted and held live across the loop
+    int lane = lane0, grp = grp0, env = env0, e = e0;
+    asm volatile("" : "+v"(lane), "+v"(grp), "+v"(env), "+v"(e));
+    const bool valid = env < args.n;
+    EnvShared& sh = shm[grp];
+#endif
+    TL_MARK(-1);
+    if (sub > 0) euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
+    // the model pointer laundered per substep: the model loads (uniform, ~1 KB) must not be hoisted out of
+    // the substep loop, where they would stay live across it (register spills)
+    StageArgs sa = args;
+#if SO100_LAUNDER == 1
+    asm volatile("" : "+s"(sa.m));
+#elif SO100_LAUNDER == 2
+    {
+      int zero;
+      asm volatile("s_mov_b32 %0, 0" : "=s"(zero));
+      sa.m = reinterpret_cast<const DevModel*>(reinterpret_cast<const char*>(args.m) + zero);
+    }
+#endif
+    NewtonRows nr;
+    assemble<SO100_SOLVER_NEWTON, true>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale, fscale,
+                                        sub, nr);
+    float* dbg = (args.b.debug && sub == nsub - 1) ? args.b.debug + (size_t)env * SO100_DBG_STRIDE : nullptr;
+    TL_MARK(0);
+    const float qacc = newton_solve(sa.m, nr, lane, valid, dbg);
+    warm_r = lane < SO100_NV ? qacc : 0.f;
+    TL_MARK(1);
+  }
+  TL_MARK(-1);
+  euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
+  final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+  TL_MARK(2);
+#ifdef SO100_TIMELINE
+  if (args.b.debug && valid && lane == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    float* dbg = args.b.debug + (size_t)env * SO100_DBG_STRIDE;
+    dbg[88] = __uint_as_float((uint32_t)tl_t0); dbg[89] = __uint_as_float((uint32_t)(tl_t0 >> 32));
+    dbg[90] = __uint_as_float((uint32_t)t1); dbg[91] = __uint_as_float((uint32_t)(t1 >> 32));
+    dbg[92] = (float)tl_acc[0];
+    dbg[93] = (float)tl_acc[1];
+    dbg[94] = (float)tl_acc[2];
+  }
+#endif
+  }
+}
+
 // ------------------------------------------------------------------ reset kernel
 struct ResetArgs {
   const DevModel* m;
@@ -2462,18 +2621,28 @@ hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, fl
                       hipStream_t s);
 
 
-// One env step = nsubstep x (stage, solve) + the final stage: 2 * nsubstep + 1 launches on one stream.
-// ev (optional, profiling): 2 nsubstep + 2 events, recorded before the first launch and after each.
+// One env step = nsubstep x (stage, solve) + the final stage: 2 * nsubstep + 1 launches on one stream (split
+// path), or one fused launch.  ev (optional, profiling): 2 nsubstep + 2 events (split) or 2 (fused), recorded
+// before the first launch and after each.
 hipError_t launch_newton(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
                          hipStream_t s);
 
-hipError_t launch_step(const DevModel* m, int nsubstep, int solver, Workspace& w, const so100_buffers& b, int n,
-                       int task, int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s,
+// fused (Newton only): the whole env step as one so100_fused_kernel launch; ev then takes 2 events.
+hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, Workspace& w, const so100_buffers& b,
+                       int n, int task, int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s,
                        hipEvent_t* ev) {
   StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0, 0};
   const dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
   int k = 0;
   if (ev) (void)hipEventRecord(ev[k++], s);
+  if (fused && solver == SO100_SOLVER_NEWTON) {
+    hipLaunchKernelGGL(so100_fused_kernel, grid, dim3(kThreads), 0, s, m, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (ev) (void)hipEventRecord(ev[k++], s);
+    w.sub_count += (uint32_t)nsubstep;
+    return hipSuccess;
+  }
   for (int sub = 0; sub <= nsubstep; sub++) {
     a.sub = sub;
     a.par = (int)(w.sub_count & 1u);

@@ -44,7 +44,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 7          # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 8          # include/so100.h SO100_ABI_VERSION
 
 
 def load():
@@ -74,12 +74,14 @@ def load():
     lib.so100_profile_read.argtypes = [_P, _P, _P, _P, _P]
     lib.so100_contact_count.argtypes = [_P, _P, _P]
     lib.so100_chunk_info.argtypes = [_P, _P, _P]
+    lib.so100_set_step_mode.argtypes = [_P, ctypes.c_int]
+    lib.so100_step_mode.argtypes = [_P]
     lib.so100_render_mesh.argtypes = [_P, _P, _P, _P, ctypes.c_int]
     lib.so100_render.argtypes = [_P, _P, _P, ctypes.POINTER(SO100Camera), ctypes.c_int, ctypes.c_int, _P, _P]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
                "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info",
-               "so100_render_mesh", "so100_render"):
+               "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
     lib.so100_struct_sizes.restype = ctypes.c_int
@@ -98,7 +100,8 @@ def load():
 EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
-                    "so100_contact_count", "so100_chunk_info", "so100_render_mesh", "so100_render")
+                    "so100_contact_count", "so100_chunk_info", "so100_render_mesh", "so100_render",
+                    "so100_set_step_mode", "so100_step_mode")
 
 
 def check(rc, what):

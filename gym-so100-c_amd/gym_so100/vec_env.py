@@ -382,6 +382,18 @@ class SO100VecEnv:
                                                   ctypes.byref(tm), ctypes.byref(tn)), "so100_profile_read")
         return sm.value, sn.value, tm.value, tn.value
 
+    @property
+    def fused(self):
+        """True when a step is one fused kernel launch (Newton solver); False: the split stage/solver
+        launches (always for PGS).  Set True / False to force a mode, None for auto (the default: fused up
+        to 24,576 envs, include/so100.h so100_set_step_mode)."""
+        return bool(self.lib.so100_step_mode(self._handle))
+
+    @fused.setter
+    def fused(self, on):
+        mode = -1 if on is None else (1 if on else 0)
+        _native.check(self.lib.so100_set_step_mode(self._handle, mode), "so100_set_step_mode")
+
     def chunk_info(self):
         """(chunks, envs of chunk 0): the env split of a step; profile_read times chunk 0's launches."""
         k, n0 = ctypes.c_int(0), ctypes.c_int(0)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 7   /* 7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 8   /* 8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -112,6 +112,16 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream);
 int so100_profile_enable(so100_env* env, int max_steps);
 int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms,
                        int* stage_launches);
+
+/* Step mode (Newton solver): 1 = the whole env step as ONE fused kernel launch over all N envs, the
+ * substep's constraint rows handed from the assembly to the solve in registers; 0 = the split path, per
+ * substep a stage kernel and a solver kernel exchanging an HBM record (2 nsubstep + 1 launches per env
+ * chunk); -1 = auto (default): fused for N <= 24,576 (SO100_FUSED_MAX overrides), split above.  Both give
+ * the same results bit for bit.  The PGS solver always runs split.  so100_step_mode returns the mode in
+ * effect (0/1).  In fused mode so100_profile_read reports the fused launches as the solver launches
+ * (stage: 0) and so100_chunk_info reports 1 chunk of N envs. */
+int so100_set_step_mode(so100_env* env, int fused);
+int so100_step_mode(const so100_env* env);
 
 /* Number of env chunks and the env count of chunk 0 (the launches so100_profile_read times). */
 int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs);

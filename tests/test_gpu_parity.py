@@ -252,6 +252,8 @@ def test_chunking_invariance(monkeypatch, variant):
     one = SO100VecEnv(n, **kw)
     monkeypatch.setenv("SO100_CHUNKS", "4")
     four = SO100VecEnv(n, **kw)
+    for e in (one, four):
+        e.fused = False                  # chunks belong to the split path (a fused step is one launch)
     assert one.chunk_info() == (1, n)
     k, n0 = four.chunk_info()
     assert k == 4 and n0 < n
@@ -274,6 +276,71 @@ def test_chunking_invariance(monkeypatch, variant):
         assert torch.equal(getattr(one, name), getattr(four, name)), name
     one.close()
     four.close()
+
+
+@pytest.mark.parametrize("variant,task,dr", [("joint", "so100_cube_to_bin", False), ("ee", "so100_touch_cube", False),
+                                               ("joint", "so100_goal", True)])
+def test_fused_step_matches_split(variant, task, dr):
+    """The fused step kernel (one launch per env step, the Newton rows handed over in registers) gives the
+    split path's results (per substep a stage and a Newton launch exchanging an HBM record) bit for bit:
+    state, outputs, auto-resets and the debug record, with a ragged tail wave (n % 4 != 0)."""
+    from gym_so100 import SO100VecEnv
+    n = 1003
+    kw = dict(task=task, device="cuda:0", seed=7, max_episode_steps=6, debug=True, variant=variant,
+              domain_randomization=(dict(mass=(0.8, 1.2), friction=(0.8, 1.2), action_noise=0.05) if dr else None))
+    fused, split = SO100VecEnv(n, **kw), SO100VecEnv(n, **kw)
+    fused.fused, split.fused = True, False
+    assert fused.fused and not split.fused
+    for e in (fused, split):
+        e.reset(seed=500)
+    if variant == "ee":
+        gm = torch.Generator(device="cuda").manual_seed(3)
+        pos = fused.mocap[:, :3] + (torch.rand(n, 3, generator=gm, device="cuda") - 0.5) * 0.08
+        for e in (fused, split):
+            e.set_mocap(pos)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(14):
+        a = torch.rand(n, 6, generator=g, device="cuda") * 2 - 1
+        rf, rs = fused.step(a), split.step(a)
+        torch.cuda.synchronize()
+        for x, y in zip(rf[1:4], rs[1:4]):
+            assert torch.equal(x, y)
+    for name in ("qpos", "qvel", "qacc_warmstart", "obs", "debug", "elapsed", "episode"):
+        assert torch.equal(getattr(fused, name), getattr(split, name)), name
+    fused.close()
+    split.close()
+
+
+def test_step_mode_switch():
+    """PGS always runs split; auto mode runs fused up to 24,576 envs; the mode can be switched between steps
+    (Newton), and the contact counter reads the record of the mode that ran."""
+    from gym_so100 import SO100VecEnv
+    big = SO100VecEnv(32768, device="cuda:0")
+    assert not big.fused and big.chunk_info()[0] == 4
+    big.fused = True
+    assert big.fused and big.chunk_info() == (1, 32768)
+    big.close()
+    pgs = SO100VecEnv(8, device="cuda:0", solver="pgs")
+    assert not pgs.fused
+    pgs.fused = True
+    assert not pgs.fused
+    pgs.close()
+    env = SO100VecEnv(8, device="cuda:0", debug=True)
+    assert env.fused
+    env.reset(seed=1)
+    for _ in range(30):                                     # the cube lands on the table: contacts
+        env.step(torch.zeros(8, 6, device="cuda"))
+    counts = []
+    for mode in (True, False, True, None):
+        env.fused = mode
+        env.step(torch.zeros(8, 6, device="cuda"))
+        acc = torch.zeros(1, dtype=torch.int64, device="cuda")
+        env.contact_count(acc)
+        torch.cuda.synchronize()
+        assert int(acc) == int(env.debug[:, 0].sum())      # the last substep's contact count
+        counts.append(int(acc))
+    assert torch.isfinite(env.qpos).all() and counts[0] > 0
+    env.close()
 
 
 def test_goal_env_semantics():
@@ -850,9 +917,11 @@ def test_cube_on_base_parity(solver, oracle64, oracle32):
     env.close()
 
 
-def test_step_graph_replay_matches_eager(monkeypatch):
-    """so100_step replays a captured hipGraph of the step (chunk fork/join included); SO100_GRAPH=0 launches
-    eagerly.  Both must give bit-identical trajectories, across re-captures (new action buffer, flags)."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_step_graph_replay_matches_eager(monkeypatch, fused):
+    """so100_step replays a captured hipGraph of the step (split: the chunk fork/join included; fused: the
+    one launch); SO100_GRAPH=0 launches eagerly.  Both must give bit-identical trajectories, across
+    re-captures (new action buffer, flags)."""
     import torch
     from gym_so100 import SO100VecEnv
     n = 4096                                        # 4 chunks: the forked streams are captured too
@@ -860,7 +929,9 @@ def test_step_graph_replay_matches_eager(monkeypatch):
     eager = SO100VecEnv(n, max_episode_steps=7, seed=3)
     monkeypatch.setenv("SO100_GRAPH", "1")
     graph = SO100VecEnv(n, max_episode_steps=7, seed=3)
-    assert eager.chunk_info()[0] == 4
+    for e in (eager, graph):
+        e.fused = fused
+    assert eager.chunk_info()[0] == (1 if fused else 4)
     eager.reset(seed=9)
     graph.reset(seed=9)
     g = torch.Generator().manual_seed(1)
