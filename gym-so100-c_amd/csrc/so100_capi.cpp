@@ -22,6 +22,7 @@ hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
 hipError_t launch_render(const DevModel*, const float4*, const int*, const uint32_t*, int, const float*,
                          const uint8_t*, const so100_camera&, int, int, int, uint8_t*, hipStream_t);
 hipError_t alloc_workspace(int, Workspace*);
+hipError_t alloc_fused_workspace(int, Workspace*);
 hipError_t free_workspace(Workspace*);
 hipError_t launch_reset(const DevModel*, const so100_buffers&, int, int, uint64_t, int, const uint8_t*, const uint32_t*,
                         hipStream_t);
@@ -62,7 +63,7 @@ struct so100_env {
   int solver;                   // SO100_SOLVER_* of the model
   int fused;                    // step mode: 1 fused, 0 split, -1 auto (fused up to fused_max envs; Newton only)
   int fused_max;                // auto mode: the largest env count that runs fused
-  Workspace fws{};              // fused launches: the record header (contact counts) of all n envs, lazily
+  Workspace fws{};              // fused launches: record header (contact counts) of all n envs, wave order
   bool last_fused = false;      // the mode of the last step (so100_contact_count reads its record)
   std::vector<Chunk> chunks;
   hipEvent_t fork = nullptr;
@@ -102,10 +103,9 @@ static void graph_free(so100_env* env) {
 }
 
 // The fused kernel implements the Newton solver only: PGS always takes the split launches.  Auto mode runs
-// fused up to fused_max envs per GPU: there every wave is resident at once and the split path's 21
-// chip-wide launch barriers cost most; at larger shards the split path's shorter launches pack the chip
-// better (measured crossover between 16,384 and 32,768 envs).
-constexpr int kFusedAutoMax = 24576;
+// fused up to fused_max envs per GPU (SO100_FUSED_MAX; default: every size, since with the heavy-first wave
+// order the fused step is at least as fast as the split one at every measured shard size).
+constexpr int kFusedAutoMax = 1 << 30;    // measured: fused >= split at every shard size
 static bool step_is_fused(const so100_env* env) {
   if (env->solver != SO100_SOLVER_NEWTON) return false;
   return env->fused < 0 ? env->n <= env->fused_max : env->fused != 0;
@@ -532,12 +532,10 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (const char* v = getenv("SO100_FUSED_MAX")) env->fused_max = atoi(v);
   e = make_chunks(env, default_chunks(n_envs));
   if (e == hipSuccess && env->solver == SO100_SOLVER_NEWTON) {
-    // the fused launches' record: only the header's contact count is used (640 B per env)
-    e = hipMalloc(&env->fws.hdr, (size_t)n_envs * so100::kHdrEnv * sizeof(float));
-    if (e == hipSuccess) e = hipMemset(env->fws.hdr, 0, (size_t)n_envs * so100::kHdrEnv * sizeof(float));
+    // the fused launches: the record header (only its contact counts are written) and the wave order
+    e = so100::alloc_fused_workspace(n_envs, &env->fws);
   }
   if (e != hipSuccess) {
-    if (env->fws.hdr) (void)hipFree(env->fws.hdr);
     (void)free_chunks(env);
     (void)hipFree(dm);
     delete env;
@@ -559,7 +557,8 @@ int so100_destroy(so100_env* env) {
   hipError_t e = hipFree(env->d_model);
   hipError_t e2 = free_chunks(env);
   if (e == hipSuccess) e = e2;
-  if (env->fws.hdr) (void)hipFree(env->fws.hdr);
+  if (e == hipSuccess) e = so100::free_workspace(&env->fws);
+  else (void)so100::free_workspace(&env->fws);
   delete env;
   return e == hipSuccess ? 0 : fail_hip("so100_destroy", e);
 }

@@ -167,6 +167,9 @@ struct Workspace {
   int* hcount;      // [2]
   int* hlist;       // [2][kHeavyCap]
   uint32_t sub_count;   // host-side substep counter (parity)
+  // fused path (so100_fused_kernel): heavy-first wave order from the previous step's per-wave cost
+  uint32_t* gcost;  // [ngroups] shader cycles of each 4-env wave in the last fused step
+  int* order;       // [ngroups] launch order of the groups (so100_order_kernel), nullptr = natural
 };
 
 }  // namespace so100

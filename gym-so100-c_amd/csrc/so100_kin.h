@@ -44,9 +44,9 @@ struct __attribute__((aligned(16))) EnvShared {
     float vec[16];
     int cnt[16];                 // S3 compaction counts (vec is free during collision)
   };
-  float ctrl[8];
+  float ctrl[6];
   float minv[6][6];
-  float inv_mcube[8];
+  float inv_mcube[6];
   float anchor[6][4];
   float axis[6][4];
   float cube_pos[4];
@@ -56,10 +56,9 @@ struct __attribute__((aligned(16))) EnvShared {
   float site_cube[4];
   float site_ee[4];
   int ncon;
-  int nlim;
-  int misc[2];
   int con_pair[kMaxCon];
   float con_dist[kMaxCon];
+  float mocap[7];                // EE variant: mocap pose (pos, quat wxyz)
   union {
     struct {
       ConSlot con[kMaxCon];      // geometry (collision -> Jacobian)
@@ -67,10 +66,11 @@ struct __attribute__((aligned(16))) EnvShared {
     };
     SerialScratch ser;           // dynamics scratch (dead before collision) + link frames (live through it)
   };
-  float mocap[8];                // EE variant: mocap pose (pos, quat wxyz)
-  // stride = 13.25 x 256 B: the 4 envs of a wave hit different LDS bank windows for the same field
-  float bank_pad[8];
 };
+// 3,168 B per env: 4 envs = 12,672 B per wave, under the 12,800 B that lets 12 workgroups share a CU's LDS
+// (allocated in 1,280-B steps: 12,928 B held the stage and fused kernels to 11 waves per CU, measured), and
+// a stride of 12.375 x 256 B, so the 4 envs of a wave hit different LDS bank windows for the same field.
+static_assert(sizeof(EnvShared) == 3168, "EnvShared: 4 per workgroup must stay within 12,800 B");
 
 // ------------------------------------------------------------------ small math (same formulas as oracle)
 DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }

@@ -2452,10 +2452,12 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
 #define TL_MARK(slot) do {} while (0)
 #endif
   __shared__ EnvShared shm[kEnvsPerBlock];
+  const uint64_t cost_t0 = __builtin_amdgcn_s_memtime();
   const int tid = threadIdx.x;
   const int grp0 = tid >> 4;
   const int lane0 = tid & 15;
-  const int env0 = blockIdx.x * kEnvsPerBlock + grp0;
+  const int group = args.w.order ? args.w.order[blockIdx.x] : (int)blockIdx.x;   // heavy-first (so100_order_kernel)
+  const int env0 = group * kEnvsPerBlock + grp0;
   const int e0 = env0 < args.n ? env0 : 0;
   {
   const int grp = grp0, lane = lane0, env = env0, e = e0;
@@ -2504,6 +2506,7 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
   euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
   final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
   TL_MARK(2);
+  if (args.w.gcost && tid == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
 #ifdef SO100_TIMELINE
   if (args.b.debug && valid && lane == 0) {
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -2627,6 +2630,41 @@ hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, fl
 hipError_t launch_newton(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
                          hipStream_t s);
 
+// Heavy-first wave order for the fused kernel.  Its waves run a whole env step each (0.4-1.8 ms) and the
+// grid exceeds the resident slots (12 per CU) above 12,288 envs: a long wave dispatched late sets the step's
+// tail.  Wave costs persist from step to step (correlation 0.65-0.74, measured), so the groups are launched
+// in descending order of their previous step's cost: a counting sort on a 12-bit float key (exponent + 4
+// mantissa bits, 6 % buckets), one workgroup.  The order changes the schedule, never a result.
+constexpr int kOrderBuckets = 4096;
+constexpr int kOrderMinGroups = 3072;          // up to the resident capacity (12 waves x 256 CUs) all start at once
+__global__ void __launch_bounds__(1024) so100_order_kernel(const uint32_t* __restrict__ gcost, int ng,
+                                                           int* __restrict__ order) {
+  __shared__ int hist[kOrderBuckets];
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  auto key = [](uint32_t c) { return (kOrderBuckets - 1) - (int)((__float_as_uint((float)c) >> 19) & 0xFFFu); };
+  for (int b = t; b < kOrderBuckets; b += 1024) hist[b] = 0;
+  __syncthreads();
+  for (int g = t; g < ng; g += 1024) atomicAdd(&hist[key(gcost[g])], 1);
+  __syncthreads();
+  int loc[kOrderBuckets / 1024], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kOrderBuckets / 1024; k++) { loc[k] = sum; sum += hist[(kOrderBuckets / 1024) * t + k]; }
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {           // inclusive scan of the per-thread sums
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int base = part[t] - sum;
+#pragma unroll
+  for (int k = 0; k < kOrderBuckets / 1024; k++) hist[(kOrderBuckets / 1024) * t + k] = base + loc[k];
+  __syncthreads();
+  for (int g = t; g < ng; g += 1024) order[atomicAdd(&hist[key(gcost[g])], 1)] = g;
+}
+
 // fused (Newton only): the whole env step as one so100_fused_kernel launch; ev then takes 2 events.
 hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, Workspace& w, const so100_buffers& b,
                        int n, int task, int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s,
@@ -2636,6 +2674,16 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, W
   int k = 0;
   if (ev) (void)hipEventRecord(ev[k++], s);
   if (fused && solver == SO100_SOLVER_NEWTON) {
+    const int ng = (int)grid.x;
+    if (w.order && w.gcost && ng > kOrderMinGroups) {
+      if (ev) (void)hipEventRecord(ev[0], s);   // the order kernel stays outside the timed launch
+      hipLaunchKernelGGL(so100_order_kernel, dim3(1), dim3(1024), 0, s, w.gcost, ng, w.order);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      if (ev) (void)hipEventRecord(ev[0], s);
+    } else {
+      a.w.order = nullptr;
+    }
     hipLaunchKernelGGL(so100_fused_kernel, grid, dim3(kThreads), 0, s, m, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -2710,15 +2758,29 @@ hipError_t alloc_workspace(int n, Workspace* w) {
 }
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
-  for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist}) {
+  for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist, (void*)w->gcost,
+                  (void*)w->order}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
   }
   w->hdr = w->con = nullptr;
-  w->gflag = nullptr;
-  w->hcount = w->hlist = nullptr;
+  w->gflag = w->gcost = nullptr;
+  w->hcount = w->hlist = w->order = nullptr;
   return r;
+}
+// The fused path's workspace: the record header (only its contact counts are written) and the wave-order
+// buffers.
+hipError_t alloc_fused_workspace(int n, Workspace* w) {
+  *w = Workspace{};
+  const size_t ng = (size_t)(n + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&w->gcost, ng * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(w->gcost, 0, ng * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&w->order, ng * sizeof(int));
+  if (e != hipSuccess) (void)free_workspace(w);
+  return e;
 }
 hipError_t launch_reset(const DevModel* m, const so100_buffers& b, int n, int task, uint64_t base_seed,
                         int env_offset, const uint8_t* mask, const uint32_t* seeds, hipStream_t s) {
