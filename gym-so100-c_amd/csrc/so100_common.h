@@ -24,6 +24,9 @@ namespace so100 {
 #define STAMP_DECL
 #define STAMP(slot) do {} while (0)
 #endif
+// an opaque copy: the compiler can neither fold nor hoist what is computed from it (the fused kernel's
+// substep loop would otherwise keep loop-invariant results live across it, spilling)
+DEV void opaque(float& v) { asm volatile("" : "+v"(v)); }
 constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;

@@ -207,9 +207,33 @@ DEV void newton_rows_load(const Workspace& w, int e, int lane, bool valid, float
   }
 }
 
-// Solve one env's substep problem (its 16 lanes); returns qacc on the dof lanes.  dbg (the env's debug
-// row, or nullptr): the last substep writes qacc, frictionloss and contact normal forces, iterations.
-DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, float* dbg) {
+// Diagnostics of a solve (debug buffer rows): the final frictionloss force of the lane's dof, contact
+// `lane`'s normal force, the iteration count, the last cost improvement, and the phase stamps.
+struct NewtonDiag {
+  float f_fr, f_n, impr;
+  int iters;
+#ifdef SO100_STAMPS
+  unsigned long long st[8];
+#endif
+};
+DEV void newton_diag_write(float* dbg, int lane, bool valid, float qacc, const NewtonDiag& d) {
+  if (!valid) return;
+#ifdef SO100_STAMPS
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) dbg[88 + k] = (float)d.st[k];
+  }
+#endif
+  if (lane < SO100_NV) { dbg[4 + lane] = qacc; dbg[76 + lane] = d.f_fr; }
+  if (lane < kMaxCon) dbg[32 + lane] = d.f_n;
+  if (lane == 0) { dbg[1] = (float)d.iters; dbg[2] = d.impr; }
+}
+
+// Solve one env's substep problem (its 16 lanes); returns qacc on the dof lanes.  want_diag: fill diag, the
+// diagnostics for the debug row, written by the caller (the row's address is then not held live across
+// the solve).
+DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, bool want_diag,
+                       NewtonDiag& diag) {
   const bool dof = lane < SO100_NV;
   STAMP_DECL
   STAMP(-1);
@@ -443,19 +467,18 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
   }
 
   STAMP(7);
-  if (valid && dbg) {
+  if (want_diag) {
 #ifdef SO100_STAMPS
-    if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) dbg[88 + k] = (float)st_acc_[k];
-    }
+    for (int k = 0; k < 8; k++) diag.st[k] = st_acc_[k];
 #endif
     float cc, f_fr, h, fc[4], hc[10];
     fr_eval(jfr, fr_fl, fr_R, fr_D, cc, f_fr, h);
     cone_eval(jc, c_D, c_mu, c_fr0, c_fr1, cc, fc, hc);
-    if (dof) { dbg[4 + lane] = qacc; dbg[76 + lane] = f_fr; }
-    if (lane < kMaxCon) dbg[32 + lane] = own ? fc[0] : 0.f;
-    if (lane == 0) { dbg[1] = (float)iters; dbg[2] = last_impr; }
+    diag.f_fr = f_fr;
+    diag.f_n = own ? fc[0] : 0.f;
+    diag.iters = iters;
+    diag.impr = last_impr;
   }
   return qacc;
 }

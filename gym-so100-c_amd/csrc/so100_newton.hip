@@ -28,8 +28,10 @@ __global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_ker
   NewtonRows r;
   newton_rows_load(a.w, e, lane, valid, jx_sh[grp], r);
   __syncthreads();
-  float* dbg = (a.last && a.debug) ? a.debug + (size_t)env * SO100_DBG_STRIDE : nullptr;
-  const float qacc = newton_solve(a.m, r, lane, valid, dbg);
+  NewtonDiag diag;
+  const bool dbg = a.last && a.debug;
+  const float qacc = newton_solve(a.m, r, lane, valid, dbg, diag);
+  if (dbg) newton_diag_write(a.debug + (size_t)env * SO100_DBG_STRIDE, lane, valid, qacc, diag);
   // qacc -> HBM (the next stage's Euler input and the next substep's warmstart)
   if (valid && lane < SO100_NV) a.qacc_out[(size_t)env * SO100_NV + lane] = qacc;
 }

@@ -715,12 +715,21 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
     float uaub = dot3(ua, ub), q1 = dot3(ua, pq), q2 = -dot3(ub, pq);
     float den = 1.f - uaub * uaub, al = 0.f, be = 0.f;
     if (den > 1e-4f) { den = 1.f / den; al = (q1 + uaub * q2) * den; be = (uaub * q1 + q2) * den; }
+    float pc0[3];
+#pragma unroll
     for (int t = 0; t < 3; t++) {
       pa[t] += ua[t] * al;
       pb[t] += ub[t] * be;
-      out.pos[0][t] = 0.5f * (pa[t] + pb[t]);
+      pc0[t] = 0.5f * (pa[t] + pb[t]);
     }
-    out.dist[0] = -depth0;
+    // every slot, in the face path's store order (only slot 0 counts: n = 1): the compiler merges the two
+    // exits' stores, and stores to different slots became one store at a run-time slot index (scratch)
+#pragma unroll
+    for (int c = 0; c < SO100_MAXCONPAIR; c++) {
+#pragma unroll
+      for (int t = 0; t < 3; t++) out.pos[c][t] = pc0[t];
+      out.dist[c] = -depth0;
+    }
     out.n = 1;
     return;
   }
@@ -820,24 +829,24 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
     cull_points8(K, SO100_MAXCONPAIR, i0, idx);
     nout = SO100_MAXCONPAIR;
   }
+  // every slot written unconditionally (slots >= nout are never read): stores under `c < nout` were merged
+  // by the compiler into one store with a run-time slot index, which put `out` in scratch memory
 #pragma unroll
   for (int c = 0; c < SO100_MAXCONPAIR; c++) {
-    if (c < nout) {
-      float x = 0.f, y = 0.f, dp = 0.f;
+    float x = 0.f, y = 0.f, dp = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const bool w = (k == idx[c]);
-        x = w ? K.x[k] : x; y = w ? K.y[k] : y; dp = w ? D[k] : dp;
-      }
-      const float xr = x - cc1, yr = y - cc2;
-      const float s1 = i11 * xr + i12 * yr, s2 = i21 * xr + i22 * yr;
-#pragma unroll
-      for (int t = 0; t < 3; t++) {
-        const float pt = center[t] + s1 * v1[t] + s2 * v2[t];
-        out.pos[c][t] = pt + pR[t] + 0.5f * dp * nref[t];
-      }
-      out.dist[c] = -dp;
+    for (int k = 0; k < 8; k++) {
+      const bool w = (k == idx[c]);
+      x = w ? K.x[k] : x; y = w ? K.y[k] : y; dp = w ? D[k] : dp;
     }
+    const float xr = x - cc1, yr = y - cc2;
+    const float s1 = i11 * xr + i12 * yr, s2 = i21 * xr + i22 * yr;
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      const float pt = center[t] + s1 * v1[t] + s2 * v2[t];
+      out.pos[c][t] = pt + pR[t] + 0.5f * dp * nref[t];
+    }
+    out.dist[c] = -dp;
   }
   out.n = nout;
 }
@@ -1724,6 +1733,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
     const int slot = tot + __popc(trow & ((1u << lane) - 1u));
     if (tfound && slot < kMaxCon) {
       float fr[9] = {0.f, 0.f, -1.f, 0, 0, 0, 0, 0, 0};
+      opaque(fr[2]);              // a constant frame: built here, not hoisted out of the fused substep loop
       make_frame(fr);
 #pragma unroll
       for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
@@ -1882,6 +1892,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
       if (hfound && hslot < kMaxCon) {
         float fr[9] = {0.f, 0.f, 1.f, 0, 0, 0, 0, 0, 0};
+        opaque(fr[2]);            // a constant frame: built here, not hoisted out of the fused substep loop
         make_frame(fr);
 #pragma unroll
         for (int t = 0; t < 9; t++) sh.con[hslot].g.frame[t] = fr[t];
@@ -2496,9 +2507,15 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
     NewtonRows nr;
     assemble<SO100_SOLVER_NEWTON, true>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale, fscale,
                                         sub, nr);
-    float* dbg = (args.b.debug && sub == nsub - 1) ? args.b.debug + (size_t)env * SO100_DBG_STRIDE : nullptr;
     TL_MARK(0);
-    const float qacc = newton_solve(sa.m, nr, lane, valid, dbg);
+    NewtonDiag diag;
+    const bool dbg = args.b.debug && sub == nsub - 1;
+    const float qacc = newton_solve(sa.m, nr, lane, valid, dbg, diag);
+    if (dbg) {
+      int row = env;
+      asm volatile("" : "+v"(row));        // not the assembly's row address (GVN would hold that across the solve)
+      newton_diag_write(args.b.debug + (size_t)row * SO100_DBG_STRIDE, lane, valid, qacc, diag);
+    }
     warm_r = lane < SO100_NV ? qacc : 0.f;
     TL_MARK(1);
   }

@@ -1,12 +1,12 @@
 """Diagnostic: per-phase cycles of the Newton solver kernel (last substep of a step); SO100_STAMPS build via
-SO100_LIB.  usage: SO100_LIB=<stamps build> python tests/_newton_stamps_report.py"""
+SO100_LIB.  usage: SO100_LIB=<stamps build> python tests/_newton_stamps_report.py [n]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv
-n = 65536
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 env = SO100VecEnv(n, device="cuda:0", debug=True, solver="newton")
 env.reset(seed=1000)
 g = torch.Generator(device="cuda").manual_seed(0)

@@ -15,14 +15,15 @@ per-dispatch busy figure from GRBM_GUI_ACTIVE would miss the chunks' overlap; it
 valu_issue_frac_serialised for reference only.
 
 usage: python tests/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json> [chunks] [solver]
-solver: newton (so100_newton_kernel) or pgs (so100_pgs_kernel; default for old profiles).  The Newton
+solver: newton (so100_newton_kernel), pgs (so100_pgs_kernel; default for old profiles) or fused
+(so100_fused_kernel: one launch per step, chunks = 1).  The Newton
 kernel's reads mix 16-B J rows with 4-B header loads; the same x2 correction is applied (the J rows
 dominate) and it is marked uncalibrated in the JSON.
 """
 import csv, glob, json, sys
 
 SOLVER = sys.argv[5] if len(sys.argv) > 5 else "pgs"
-KERNEL = f"so100_{SOLVER}_kernel"
+KERNEL = f"so100_{SOLVER}_kernel"      # solver "fused": so100_fused_kernel, the whole step in one launch
 
 
 def per_launch(pattern, counter):
@@ -50,18 +51,24 @@ def kernel_mean(pattern, counter, name):
 
 per_kernel = {k: kernel_mean(d + "/sq*counter_collection.csv", "SQ_INSTS_VALU", k)
               for k in (KERNEL, "so100_stage_kernel<0,", "so100_stage_kernel<1,", "so100_stage_kernel<2,")}
-step_insts = chunks * (10 * per_kernel[KERNEL] + per_kernel["so100_stage_kernel<0,"] +
-                       9 * per_kernel["so100_stage_kernel<1,"] + per_kernel["so100_stage_kernel<2,"])
+if SOLVER == "fused":
+    step_insts = chunks * per_kernel[KERNEL]
+else:
+    step_insts = chunks * (10 * per_kernel[KERNEL] + per_kernel["so100_stage_kernel<0,"] +
+                           9 * per_kernel["so100_stage_kernel<1,"] + per_kernel["so100_stage_kernel<2,"])
 fetch = per_launch(d + "/fetch*counter_collection.csv", "FETCH_SIZE")
 write = per_launch(d + "/write*counter_collection.csv", "WRITE_SIZE")
+fx = 1 if SOLVER == "fused" else 2
 res = {"kernel": KERNEL, "n_envs": n, "fetch_correction": "x2 (16-B/lane reads)" if SOLVER == "pgs" else
-       "x2 (J rows 16-B/lane; 4-B header loads uncalibrated)",
+       ("none (4-B/lane state loads and scalar model loads; the x2 16-B/lane correction does not apply)"
+        if SOLVER == "fused" else "x2 (J rows 16-B/lane; 4-B header loads uncalibrated)"),
        "fetch_kb_raw": fetch, "write_kb": write,
-       "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
+       "hbm_bytes_per_launch": (fx * fetch + write) * 1024 if fetch is not None and write is not None else None,
        "sq_insts_valu": insts, "grbm_gui_active": gui, "chunks": chunks,
        "valu_insts_per_kernel": per_kernel, "valu_insts_per_step": step_insts,
        "valu_issue_frac_serialised": (insts * 2.0) / (gui / 8.0 * 1024.0) if insts and gui else None,
        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), steady state (after 60 warmup steps), "
-                 "mean of the last 20 solver dispatches; FETCH doubled per the gfx950 16-B/lane correction"}
+                 "mean of the last 20 dispatches of the kernel; FETCH doubled per the gfx950 16-B/lane correction "
+                 "(not for the fused kernel)"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
