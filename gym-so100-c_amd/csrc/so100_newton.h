@@ -28,7 +28,10 @@
 namespace so100 {
 
 // One lane's share of a substep's Newton problem (its rows of the record).
-constexpr int kJReg = 8;                // contacts whose J rows stay in VGPRs
+#ifndef SO100_JREG
+#define SO100_JREG 8
+#endif
+constexpr int kJReg = SO100_JREG;       // contacts whose J rows stay in VGPRs
 constexpr int kJLds = kMaxCon - kJReg;  // the others' J rows: LDS [kJLds][SO100_NV] float4 per env
 struct NewtonRows {
   float qs, warm, fr_aref;              // dof lanes: qacc_smooth, warmstart, frictionloss aref

@@ -1376,10 +1376,14 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
 // The MPR pairs 23..106 of one substep ((cube | bin box, hull), hull-hull self-collision, the Base hull),
 // contacts staged in sh.mpr in pair order.
 //  * broadphase, lane-parallel: lane l of the env's row tests pairs 23 + l + 16 r (r < 6);
-//  * narrowphase: the wave walks the union of its 4 envs' candidate pairs in ascending order; each env
-//    holding the pair runs MPR on its whole row.
+//  * narrowphase, shared across the wave: the 4 envs' candidates form one list (env by env, pairs ascending,
+//    in the LDS contact area of env 0, dead until the compaction); each round the 4 rows take the next 4
+//    items, whichever env they belong to, and run MPR on that env's frames.  A wave whose envs hold c_e
+//    candidates runs ceil(sum c_e / 4) rounds: the envs' own rows share a heavy env's pairs (this was one
+//    pair of the wave's union per round, on the rows holding it: 60 % of the slowest waves' assembly);
+//  * each round's hits go to their env's staging slots in list order, so each env keeps its pair order.
 // Returns the env's number of staged contacts (uniform across its row, capped at kMaxCon).
-DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, int grp, bool valid) {
+DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, int grp, bool valid) {
 #ifdef SO100_EXPERIMENT_NO_MPR
   return 0;   // timing experiment only: box-hull contacts off
 #endif
@@ -1390,7 +1394,10 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
 #endif
   constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 6
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
-  uint64_t env_cand[2] = {0ull, 0ull}, wave_cand[2] = {0ull, 0ull};
+  static_assert(kEnvsPerBlock * kConvex <= (int)sizeof(shm[0].con), "the candidate list fits the contact area");
+  const EnvShared& sh = shm[grp];
+  uint64_t env_cand[2] = {0ull, 0ull};
+  uint32_t mine = 0u;                           // bit r: this lane's pair of round r is a candidate
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
     const int q = lane + kLanes * r;
@@ -1401,40 +1408,78 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
       cand = mpr_broadphase(m, o, -1 - m->pair_g2[SO100_PAIR_MPR0 + q]);
     }
     const uint64_t b = __ballot(cand);
+    mine |= cand ? 1u << r : 0u;
     env_cand[r / 4] |= ((b >> (grp * 16)) & 0xFFFFull) << (16 * (r % 4));
-    wave_cand[r / 4] |= ((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFull) << (16 * (r % 4));
   }
-  int ns = 0;
+  // the wave's candidate list: env e's at [pre_e, pre_e + c_e)
+  const int cnt = __popcll(env_cand[0]) + __popcll(env_cand[1]);
+  const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
+  const int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
+  const int pre1 = c0, pre2 = c0 + c1, pre3 = c0 + c1 + c2;
+  int total = pre3 + c3;
 #ifdef SO100_EXPERIMENT_MPR_BROAD_ONLY
-  wave_cand[0] = wave_cand[1] = 0;   // timing experiment only: broadphase without the narrowphase
+  total = 0;   // timing experiment only: broadphase without the narrowphase
 #endif
+  if (total == 0) return 0;
+  uint8_t* list = reinterpret_cast<uint8_t*>(&shm[0].con[0]);
+  const int pre_own = grp == 0 ? 0 : grp == 1 ? pre1 : grp == 2 ? pre2 : pre3;
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-   while (wave_cand[h]) {
-    const int q = 64 * h + __builtin_ctzll(wave_cand[h]);
-    wave_cand[h] &= wave_cand[h] - 1ull;
-    if ((env_cand[h] >> (q - 64 * h)) & 1ull) {
-      const int p = SO100_PAIR_MPR0 + q, k = -1 - m->pair_g2[p];
+  for (int r = 0; r < kRounds; r++) {
+    if ((mine >> r) & 1u) {
+      const int q = lane + kLanes * r;     // rank = candidates of this env below pair q
+      const uint64_t below0 = q >= 64 ? env_cand[0] : (env_cand[0] & ((1ull << q) - 1ull));
+      const uint64_t below1 = q >= 64 ? (env_cand[1] & ((1ull << (q - 64)) - 1ull)) : 0ull;
+      list[pre_own + __popcll(below0) + __popcll(below1)] = (uint8_t)q;
+    }
+  }
+  __syncthreads();
+  int f0 = 0, f1 = 0, f2 = 0, f3 = 0;           // staged contacts per env (wave-uniform)
+  const int rounds = (total + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  auto env_of = [&](int item) { return item >= pre3 ? 3 : item >= pre2 ? 2 : item >= pre1 ? 1 : 0; };
+  for (int rd = 0; rd < rounds; rd++) {
+    const int item = kEnvsPerBlock * rd + grp;
+    const bool act = item < total;
+    const int ie = env_of(item);
+    float depth = 0.f, dir[3] = {0.f, 0.f, 0.f}, pos[3] = {0.f, 0.f, 0.f};
+    bool hit = false;
+    int p = SO100_PAIR_MPR0;
+    if (act) {
+      p = SO100_PAIR_MPR0 + list[item];
       MprObj o;
-      mpr_obj_setup(m, sh, p, o);
-      float depth, dir[3], pos[3];
-      if (mpr_penetration(m, o, depth, dir, pos, lane)) {
-        if (ns < kMaxCon && lane == 0) {
-          float RH[9], pH[3], wn[3], wp[3];
-          hull_frame(m, sh, m->hull_body[k], RH, pH);
-          mulmv3(wn, RH, dir);
-          mulmv3(wp, RH, pos);
-          MprStage& st = sh.mpr[ns];
-          st.pos[0] = wp[0] + pH[0]; st.pos[1] = wp[1] + pH[1];
-          st.pos[2] = wp[2] + pH[2]; st.pos[3] = -depth;
-          st.nrm[0] = wn[0]; st.nrm[1] = wn[1]; st.nrm[2] = wn[2];
-          st.nrm[3] = __int_as_float(p);
-        }
-        ns++;
+      mpr_obj_setup(m, shm[ie], p, o);
+      hit = mpr_penetration(m, o, depth, dir, pos, lane);
+    }
+    // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
+    const uint64_t hb = __ballot(hit);
+    int slot = ie == 0 ? f0 : ie == 1 ? f1 : ie == 2 ? f2 : f3;
+#pragma unroll
+    for (int g = 0; g < kEnvsPerBlock; g++) {
+      const int it = kEnvsPerBlock * rd + g;
+      const bool h = it < total && ((hb >> (16 * g)) & 1ull);
+      if (g < grp && h && env_of(it) == ie) slot++;
+    }
+    if (hit && lane == 0 && slot < kMaxCon) {
+      const int k = -1 - m->pair_g2[p];
+      float RH[9], pH[3], wn[3], wp[3];
+      hull_frame(m, shm[ie], m->hull_body[k], RH, pH);
+      mulmv3(wn, RH, dir);
+      mulmv3(wp, RH, pos);
+      MprStage& st = shm[ie].mpr[slot];
+      st.pos[0] = wp[0] + pH[0]; st.pos[1] = wp[1] + pH[1];
+      st.pos[2] = wp[2] + pH[2]; st.pos[3] = -depth;
+      st.nrm[0] = wn[0]; st.nrm[1] = wn[1]; st.nrm[2] = wn[2];
+      st.nrm[3] = __int_as_float(p);
+    }
+#pragma unroll
+    for (int g = 0; g < kEnvsPerBlock; g++) {
+      const int it = kEnvsPerBlock * rd + g;
+      if (it < total && ((hb >> (16 * g)) & 1ull)) {
+        const int e = env_of(it);
+        f0 += e == 0; f1 += e == 1; f2 += e == 2; f3 += e == 3;
       }
     }
-   }
   }
+  const int ns = grp == 0 ? f0 : grp == 1 ? f1 : grp == 2 ? f2 : f3;
   return ns < kMaxCon ? ns : kMaxCon;
 }
 
@@ -1877,7 +1922,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
     SSTAMP(6);
-    const int nmpr = mpr_contacts(m, sh, lane, grp, valid);
+    const int nmpr = mpr_contacts(m, &sh - grp, lane, grp, valid);
     SSTAMP(7);
     PairContacts pc;
     pc.n = 0;
@@ -2008,6 +2053,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       if constexpr (kFused) {
         // the J rows of contacts kJReg.. go to the contact-geometry area of LDS, dead from here to the next
         // substep's collision (ConArea is exactly kJLds x 12 float4)
+        static_assert(kJLds * SO100_NV * sizeof(float4) <= sizeof(ConArea), "the LDS J rows fit the contact area");
         float4* jx = reinterpret_cast<float4*>(&sh.con[0]);
         if (kJReg < ncon_max) {
           __syncthreads();
@@ -2443,9 +2489,10 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
 // functions on the same values.
 __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kernel(const DevModel* __restrict__ model,
-                                                                                  StageArgs args) {
+                                                                                  StageArgs kargs) {
   // the model as a noalias kernel argument: no store of the step can clobber it, so its uniform loads stay
   // scalar (s_load) after the substeps' global stores (through args.m they became vector loads)
+  StageArgs args = kargs;
   args.m = model;
 #ifdef SO100_TIMELINE
   // diagnostic build: wave start / end (s_memrealtime) and shader cycles in assembly / Newton / epilogue
@@ -2471,8 +2518,7 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
   const int env0 = group * kEnvsPerBlock + grp0;
   const int e0 = env0 < args.n ? env0 : 0;
   {
-  const int grp = grp0, lane = lane0, env = env0, e = e0;
-  const bool valid = env < args.n;
+  const int grp = grp0, lane = lane0, e = e0;
   EnvShared& sh = shm[grp];
   float qpos_r, qvel_r, warm_r, mscale, fscale, sigma;
   int elapsed0;
@@ -2520,8 +2566,16 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
     TL_MARK(1);
   }
   TL_MARK(-1);
-  euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
-  final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+  {
+    // fresh ids again: the epilogue's store addresses must not be the prologue's load addresses (CSE would
+    // hold those across the substep loop)
+    int lane = lane0, grp = grp0, env = env0, e = e0;
+    asm volatile("" : "+v"(lane), "+v"(grp), "+v"(env), "+v"(e));
+    const bool valid = env < args.n;
+    EnvShared& sh = shm[grp];
+    euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
+    final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+  }
   TL_MARK(2);
   if (args.w.gcost && tid == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
 #ifdef SO100_TIMELINE

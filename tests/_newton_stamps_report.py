@@ -13,11 +13,13 @@ g = torch.Generator(device="cuda").manual_seed(0)
 for i in range(60):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
 acc, it = np.zeros(8), 0.0
+rows = []
 for i in range(3):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
     d = env.debug.cpu().numpy()
     acc += d[::4, 88:96].mean(0)
+    rows.append(d[::4, 88:96])
     it += d[:, 1].mean()
 acc /= 3
 names = ["load record", "warmstart choice", "rows + gradient", "Hessian", "Cholesky + solves", "line search",
@@ -25,3 +27,8 @@ names = ["load record", "warmstart choice", "rows + gradient", "Hessian", "Chole
 print(f"Newton steps per substep (env mean) {it / 3:.2f}")
 for k, v in zip(names, acc):
     print(f"{k:26s} {v / 1e3:8.1f} Kcyc  {100 * v / acc.sum():5.1f}%")
+R = np.concatenate(rows)
+top = R[np.argsort(R.sum(1))[-max(1, len(R) // 100):]].mean(0)
+print("slowest 1% of waves:")
+for k, v in zip(names, top):
+    print(f"{k:26s} {v / 1e3:8.1f} Kcyc  {100 * v / top.sum():5.1f}%")

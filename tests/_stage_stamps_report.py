@@ -13,12 +13,19 @@ g = torch.Generator(device="cuda").manual_seed(0)
 for i in range(60):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
 acc = np.zeros(8)
+rows = []
 for i in range(3):
     env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
     acc += env.debug.cpu().numpy()[::4, 88:96].mean(0)
+    rows.append(env.debug.cpu().numpy()[::4, 88:96])
 acc /= 3
 names = ["Euler", "S1-S2 FK + dynamics", "S3c box-box + compaction", "S6a J + reductions", "S6b per-contact setup",
          "S7 + record", "S3a hulls vs table", "S3b box-hull MPR"]
 for k, v in zip(names, acc):
     print(f"{k:24s} {v / 1e3:8.1f} Kcyc  {100 * v / acc.sum():5.1f}%")
+R = np.concatenate(rows)
+top = R[np.argsort(R.sum(1))[-max(1, len(R) // 100):]].mean(0)
+print("slowest 1% of waves:")
+for k, v in zip(names, top):
+    print(f"{k:26s} {v / 1e3:8.1f} Kcyc  {100 * v / top.sum():5.1f}%")
