@@ -1886,7 +1886,7 @@ DEV void set_controls(const StageArgs& args, EnvShared& sh, int lane, int e, flo
 // previous substep's Euler): kinematics, CRBA/RNE, actuation, collision, the frictionloss / limit /
 // contact rows.  Newton: the rows go to nr (kFused: kept in registers for newton_solve; split: stored to the
 // HBM record); PGS: the solver record of so100_pgs_kernel.
-template <int kSolver, bool kFused>
+template <int kSolver, bool kFused, bool kDebug = true>
 DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int env, int e, bool valid, float qpos_r,
                   float qvel_r, float warm_r, float mscale, float fscale, int sub, NewtonRows& nr) {
   const DevModel* __restrict__ m = args.m;
@@ -2101,12 +2101,12 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         }
         SSTAMP(5);
 #ifdef SO100_STAGE_STAMPS
-        if (B.debug && sub == m->nsubstep - 1 && lane == 0) {
+        if (kDebug && B.debug && sub == m->nsubstep - 1 && lane == 0) {
 #pragma unroll
           for (int k = 0; k < 8; k++) B.debug[(size_t)env * SO100_DBG_STRIDE + 88 + k] = (float)sst_acc_[k];
         }
 #endif
-        if (B.debug && sub == m->nsubstep - 1) {
+        if (kDebug && B.debug && sub == m->nsubstep - 1) {
           float* dbg = B.debug + (size_t)env * SO100_DBG_STRIDE;
           if (lane < kMaxCon) {
             dbg[16 + lane] = lane < ncon ? sh.con_dist[lane] : 0.f;
@@ -2487,7 +2487,9 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 // and the epilogue, with the state in registers throughout.  The split path's 21 launches end every
 // substep at the slowest wave of the chip; here a wave only waits for itself.
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
-// functions on the same values.
+// functions on the same values.  kDebug: the instantiation that also fills the debug buffer (launched when
+// the caller passes one); the other has no debug code, which costs registers in the substep loop.
+template <bool kDebug>
 __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kernel(const DevModel* __restrict__ model,
                                                                                   StageArgs kargs) {
   // the model as a noalias kernel argument: no store of the step can clobber it, so its uniform loads stay
@@ -2503,7 +2505,7 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
     __builtin_amdgcn_sched_barrier(0);                                                           \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();                                            \
     __builtin_amdgcn_sched_barrier(0);                                                           \
-    if ((slot) >= 0) tl_acc[(slot)] += t_ - tl_prev;                                             \
+    if ((slot) >= 0) tl_acc[(slot) < 0 ? 0 : (slot)] += t_ - tl_prev;                            \
     tl_prev = t_;                                                                                \
   } while (0)
 #else
@@ -2551,11 +2553,11 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
     }
 #endif
     NewtonRows nr;
-    assemble<SO100_SOLVER_NEWTON, true>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale, fscale,
-                                        sub, nr);
+    assemble<SO100_SOLVER_NEWTON, true, kDebug>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale,
+                                                fscale, sub, nr);
     TL_MARK(0);
     NewtonDiag diag;
-    const bool dbg = args.b.debug && sub == nsub - 1;
+    const bool dbg = kDebug && args.b.debug && sub == nsub - 1;
     const float qacc = newton_solve(sa.m, nr, lane, valid, dbg, diag);
     if (dbg) {
       int row = env;
@@ -2579,9 +2581,9 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
   TL_MARK(2);
   if (args.w.gcost && tid == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
 #ifdef SO100_TIMELINE
-  if (args.b.debug && valid && lane == 0) {
+  if (args.b.debug && env0 < args.n && lane0 == 0) {
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-    float* dbg = args.b.debug + (size_t)env * SO100_DBG_STRIDE;
+    float* dbg = args.b.debug + (size_t)env0 * SO100_DBG_STRIDE;
     dbg[88] = __uint_as_float((uint32_t)tl_t0); dbg[89] = __uint_as_float((uint32_t)(tl_t0 >> 32));
     dbg[90] = __uint_as_float((uint32_t)t1); dbg[91] = __uint_as_float((uint32_t)(t1 >> 32));
     dbg[92] = (float)tl_acc[0];
@@ -2755,7 +2757,8 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, W
     } else {
       a.w.order = nullptr;
     }
-    hipLaunchKernelGGL(so100_fused_kernel, grid, dim3(kThreads), 0, s, m, a);
+    if (b.debug) hipLaunchKernelGGL(so100_fused_kernel<true>, grid, dim3(kThreads), 0, s, m, a);
+    else hipLaunchKernelGGL(so100_fused_kernel<false>, grid, dim3(kThreads), 0, s, m, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[k++], s);

@@ -386,7 +386,7 @@ class SO100VecEnv:
     def fused(self):
         """True when a step is one fused kernel launch (Newton solver); False: the split stage/solver
         launches (always for PGS).  Set True / False to force a mode, None for auto (the default: fused up
-        to SO100_FUSED_MAX envs, by default any count; include/so100.h so100_set_step_mode)."""
+        to 49,152 envs per GPU, SO100_FUSED_MAX overrides; include/so100.h so100_set_step_mode)."""
         return bool(self.lib.so100_step_mode(self._handle))
 
     @fused.setter

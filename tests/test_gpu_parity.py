@@ -312,12 +312,15 @@ def test_fused_step_matches_split(variant, task, dr):
 
 
 def test_step_mode_switch():
-    """PGS always runs split; auto mode (the default) runs fused; the mode can be switched between steps
-    (Newton), and the contact counter reads the record of the mode that ran."""
+    """PGS always runs split; auto mode (the default) runs fused up to 49,152 envs; the mode can be switched
+    between steps (Newton), and the contact counter reads the record of the mode that ran."""
     from gym_so100 import SO100VecEnv
     big = SO100VecEnv(32768, device="cuda:0")
     assert big.fused and big.chunk_info() == (1, 32768)
     big.fused = False
+    assert not big.fused and big.chunk_info()[0] == 4
+    big.close()
+    big = SO100VecEnv(65536, device="cuda:0")
     assert not big.fused and big.chunk_info()[0] == 4
     big.close()
     pgs = SO100VecEnv(8, device="cuda:0", solver="pgs")
