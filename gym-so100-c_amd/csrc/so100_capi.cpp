@@ -296,7 +296,7 @@ int build_device_model(const so100_model* s, DevModel* d) {
       s->hull_start[SO100_HULL_BASE] + s->hull_count[SO100_HULL_BASE] > SO100_HULL_NVERT)
     return fail("model: Base hull vertex range out of bounds");
   if (s->body_parent[1] != 0) return fail("model: the Base must hang off the world");
-  for (int p = SO100_PAIR_BASE0; p < SO100_PAIR_PAD0; p++) {
+  for (int p = SO100_PAIR_BASE0; p < SO100_PAIR_PADLINK0; p++) {
     const int g1 = s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
     if (p == SO100_PAIR_BASE0) {
       if (g1 != SO100_CUBE_GEOM || k2 != SO100_HULL_BASE) return fail("model: pair 98 must be (cube, Base hull)");
@@ -313,6 +313,17 @@ int build_device_model(const so100_model* s, DevModel* d) {
     if (s->pair_body1[p] != s->hull_body[k1] || s->pair_body2[p] != s->hull_body[k2] || k1 == k2)
       return fail("model: self pair bodies");
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: self pairs must have condim 3 or 4");
+    if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
+  }
+  // (finger pad, link hull) pairs through MPR: a pad box on a jaw against the Base or a link hull on bodies
+  // 2..5 (the MPR kernel takes the pad's pose from its jaw's frame)
+  for (int p = SO100_PAIR_PADLINK0; p < SO100_PAIR_PAD0; p++) {
+    const int g1 = s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
+    if (g1 < 1 || g1 > SO100_NPAD || (s->geom_body[g1] != 6 && s->geom_body[g1] != 7))
+      return fail("model: pad-link pair p must have a finger pad as geom1");
+    if (k2 < 0 || k2 >= SO100_NHULL_ALL || s->hull_body[k2] > 5) return fail("model: pad-link pair p must have a link hull as geom2");
+    if (s->pair_body1[p] != s->geom_body[g1] || s->pair_body2[p] != s->hull_body[k2]) return fail("model: pad-link pair bodies");
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: pad-link pairs must have condim 3 or 4");
     if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
   }
   // pad pairs: (finger pad i, table) at SO100_PAIR_PAD0 + i, (pad i, bin box j) at SO100_PAIR_PADBIN0 + 5 i + j

@@ -1251,7 +1251,7 @@ DEV void hull_frame(const DevModel* __restrict__ m, const EnvShared& sh, int b, 
   }
 }
 
-// Convex pair p (23..106): obj1 = box geom (cube, bin box) or hull k1 (self-collision, the Base), obj2 = hull k, both
+// Convex pair p (23..142): obj1 = box geom (cube, bin box, finger pad) or hull k1 (self-collision, the Base), obj2 = hull k, both
 // in hull k's body frame H.  Oracle collision().
 DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int p, MprObj& o) {
   const int g = m->pair_g1[p], k = -1 - m->pair_g2[p];
@@ -1263,11 +1263,13 @@ DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int 
     for (int t = 0; t < 3; t++) pb[t] = sh.cube_pos[t];
 #pragma unroll
     for (int t = 0; t < 9; t++) Rb[t] = sh.cube_mat[t];
-  } else if (g >= 0) {
+  } else if (g >= 0 && m->geom_body[g] == 0) {       // a bin box (static)
 #pragma unroll
     for (int t = 0; t < 3; t++) pb[t] = m->geom_pos[g][t];
 #pragma unroll
     for (int t = 0; t < 9; t++) Rb[t] = m->geom_mat[g][t];
+  } else if (g >= 0) {                               // a finger pad on a jaw (pad / link-hull pairs)
+    geom_pose(m, sh, g, pb, Rb);
   } else {
     hull_frame(m, sh, m->hull_body[-1 - g], Rb, pb);
   }
@@ -1318,9 +1320,13 @@ DEV bool mpr_sphere(const DevModel* __restrict__ m, const EnvShared& sh, int p) 
 #pragma unroll
     for (int t = 0; t < 3; t++) c1[t] = sh.cube_pos[t];
     r1 = m->geom_rbound[g];
-  } else if (g >= 0) {
+  } else if (g >= 0 && m->geom_body[g] == 0) {       // a bin box
 #pragma unroll
     for (int t = 0; t < 3; t++) c1[t] = m->geom_pos[g][t];
+    r1 = m->geom_rbound[g];
+  } else if (g >= 0) {                               // a finger pad on a jaw
+    float Rp[9];
+    geom_pose(m, sh, g, c1, Rp);
     r1 = m->geom_rbound[g];
   } else {
     const int k1 = -1 - g;
@@ -1373,9 +1379,10 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
   return true;
 }
 
-// The MPR pairs 23..106 of one substep ((cube | bin box, hull), hull-hull self-collision, the Base hull),
+// The MPR pairs 23..142 of one substep ((cube | bin box, hull), hull-hull self-collision, the Base hull, the
+// finger pads vs the arm's link hulls),
 // contacts staged in sh.mpr in pair order.
-//  * broadphase, lane-parallel: lane l of the env's row tests pairs 23 + l + 16 r (r < 6);
+//  * broadphase, lane-parallel: lane l of the env's row tests pairs 23 + l + 16 r (r < 8);
 //  * narrowphase, shared across the wave: the 4 envs' candidates form one list (env by env, pairs ascending,
 //    in the LDS contact area of env 0, dead until the compaction); each round the 4 rows take the next 4
 //    items, whichever env they belong to, and run MPR on that env's frames.  A wave whose envs hold c_e
@@ -1387,12 +1394,12 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
 #ifdef SO100_EXPERIMENT_NO_MPR
   return 0;   // timing experiment only: box-hull contacts off
 #endif
-#ifdef SO100_NO_BASE
-  constexpr int kConvex = SO100_NPAIR_CONVEX - SO100_NPAIR_BASE;   // A/B diagnostic builds only
+#ifdef SO100_NO_PADLINK
+  constexpr int kConvex = SO100_NPAIR_CONVEX - SO100_NPAIR_PADLINK;   // A/B diagnostic builds only
 #else
   constexpr int kConvex = SO100_NPAIR_CONVEX;
 #endif
-  constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 6
+  constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 8
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
   static_assert(kEnvsPerBlock * kConvex <= (int)sizeof(shm[0].con), "the candidate list fits the contact area");
   const EnvShared& sh = shm[grp];

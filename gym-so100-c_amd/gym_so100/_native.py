@@ -44,7 +44,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 8          # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 9          # include/so100.h SO100_ABI_VERSION
 
 
 def load():

@@ -22,10 +22,12 @@ PAIR_SELF0 = PAIR_MPR0 + (1 + NBINBOX) * NHULL  # 77: hull-hull self-collision p
 NHULL_ALL, HULL_BASE = NHULL + 1, NHULL          # hull arrays hold the static Base's hull at index 9
 NPAIR_SELF = 21
 PAIR_BASE0 = PAIR_SELF0 + NPAIR_SELF             # 98: (cube, Base hull), 99..106 (Base hull, hull k = 1..8)
-PAIR_PAD0 = PAIR_BASE0 + 9                       # 107: (pad i, table) pairs 107..114
-PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 115: (pad i, bin box j) at 115 + 5 i + j, box-box
+PAIR_PADLINK0 = PAIR_BASE0 + 9                   # 107: (pad, link hull) pairs 107..142 through MPR
+NPAIR_PADLINK = 36
+PAIR_PAD0 = PAIR_PADLINK0 + NPAIR_PADLINK        # 143: (pad i, table) pairs 143..150
+PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 151: (pad i, bin box j) at 151 + 5 i + j, box-box
 NPAIR_PAD = 8 * (1 + NBINBOX)                    # 48
-NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 155
+NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 191
 NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
 MAXCON, CONDIM, NOBS = 16, 4, 15
 NEFC_MAX = NV + NHINGE + MAXCON * CONDIM

@@ -441,19 +441,32 @@ def compile_model():
         pairs.append(dict(g1=-1 - 9, g2=-1 - k, body1=bid["Base"], body2=h["body"], name1=hulls[9]["name"],
                           name2=h["name"], hull=k, hull1=9, **mixed(hulls[9], h)))
     assert len(pairs) == 107
-    # Pairs 107..114: the 8 finger pads against the table; 115..154: against the 5 bin boxes (115 + 5 i + j).
+    # Pairs 107..142: the finger pads (boxes on the jaws) against the arm's own link hulls, through MPR:
+    # the Base (hull 9), Rotation_Pitch, Upper_Arm, Lower_Arm (hulls 0..2) and Wrist_Pitch_Roll (hull 3),
+    # less the fixed-jaw pads vs Wrist_Pitch_Roll (their parent body: MuJoCo's parent filter).  geom1 = the
+    # pad (box < mesh), normal from the pad to the hull.
+    pads = [f"{side}_jaw_pad_{i}" for side in ("fixed", "moving") for i in range(1, 5)]
+    for n1 in pads:
+        g1 = geoms[gid[n1]]
+        for k in (9, 0, 1, 2, 3):
+            h = hulls[k]
+            if parent[g1["body"]] == h["body"]:
+                continue
+            pairs.append(dict(g1=gid[n1], g2=-1 - k, body1=g1["body"], body2=h["body"], name1=n1,
+                              name2=h["name"], hull=k, **mixed(g1, h)))
+    assert len(pairs) == 143
+    # Pairs 143..150: the 8 finger pads against the table; 151..190: against the 5 bin boxes (151 + 5 i + j).
     # geom1 = the pad: the table is a mesh (box < mesh) and the bin boxes come after the arm in the model
     # (so100_transfer_cube.xml includes the arm before the bin), so the normal points from the pad to the
     # table / bin box.  Pad-table contacts follow the hull-table rule (one per pair); pad-bin pairs are
     # box-box like the cube's.
-    pads = [f"{side}_jaw_pad_{i}" for side in ("fixed", "moving") for i in range(1, 5)]
     pad_pairs = ([(n1, "table") for n1 in pads]
                  + [(n1, n2) for n1 in pads for n2 in ("bin_wall", "bin_wall2", "bin_wall3", "bin_wall4", "bin_floor")])
     for n1, n2 in pad_pairs:
         g1, g2 = geoms[gid[n1]], geoms[gid[n2]]
         pairs.append(dict(g1=gid[n1], g2=gid[n2], body1=g1["body"], body2=g2["body"], name1=n1, name2=n2,
                           **mixed(g1, g2)))
-    assert len(pairs) == 155
+    assert len(pairs) == 191
 
     # ---- EE / mocap variant (so100_transfer_cube_ee.xml: the same scene with trs_so_arm100/so_arm100_ee.xml,
     # whose only differences are the mocap body at :155 and the weld equality at :171-173) ----

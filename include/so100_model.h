@@ -42,13 +42,16 @@
 #define SO100_NPAIR_SELF 21                                 /* hulls on non-adjacent arm links */
 #define SO100_PAIR_BASE0 (SO100_PAIR_SELF0 + SO100_NPAIR_SELF)  /* 98: (cube, Base hull), then (Base hull, hull k) */
 #define SO100_NPAIR_BASE 9                                  /* 99..106: hull k = 1..8 (Rotation_Pitch excluded) */
-#define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF + SO100_NPAIR_BASE)  /* 84 pairs through MPR */
-#define SO100_PAIR_PAD0 (SO100_PAIR_BASE0 + SO100_NPAIR_BASE)  /* 107: first (pad, table | bin box) pair */
+#define SO100_PAIR_PADLINK0 (SO100_PAIR_BASE0 + SO100_NPAIR_BASE)  /* 107: first (pad, link hull) pair */
+#define SO100_NPAIR_PADLINK 36                              /* 107..142: pads vs Base, Rotation_Pitch, Upper_Arm,
+                                                               Lower_Arm, Wrist_Pitch_Roll (not the fixed pads' parent) */
+#define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF + SO100_NPAIR_BASE + SO100_NPAIR_PADLINK)  /* 120 through MPR */
+#define SO100_PAIR_PAD0 (SO100_PAIR_PADLINK0 + SO100_NPAIR_PADLINK)  /* 143: first (pad, table | bin box) pair */
 #define SO100_NPAD 8                                        /* finger pads: geoms 1..8 */
-#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 115: (pad i, bin box j) at 115 + 5 i + j */
+#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 151: (pad i, bin box j) at 151 + 5 i + j */
 #define SO100_NPAIR_PADBIN (SO100_NPAD * SO100_NBINBOX)     /* 40, box-box */
-#define SO100_NPAIR_PAD (SO100_NPAD + SO100_NPAIR_PADBIN)   /* 48: 107..114 (pad i, table), then pad-bin */
-#define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 155 */
+#define SO100_NPAIR_PAD (SO100_NPAD + SO100_NPAIR_PADBIN)   /* 48: 143..150 (pad i, table), then pad-bin */
+#define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 191: every pair MuJoCo's filters leave */
 #define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_CUBE_BODY 8

@@ -983,8 +983,9 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = best - top;
     add_contact(d, &con, p);
   }
-  /* pairs 23..97 through the MPR convex collider, in H = the body frame of hull k (geom2):
-   *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links */
+  /* pairs 23..142 through the MPR convex collider, in H = the body frame of hull k (geom2):
+   *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links;
+   *   98..106 the static Base hull (the cube, then link hulls 1..8); 107..142 (finger pad, link hull k) */
   for (int p = SO100_PAIR_MPR0; p < SO100_PAIR_PAD0; p++) {
     const int k = -1 - m->pair_geom2[p], g = m->pair_geom1[p], b = m->hull_body[k];
     const real* RH = d->xmat[b];
@@ -1031,7 +1032,7 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = -depth;
     add_contact(d, &con, p);
   }
-  /* pairs 98..145: the finger pads vs the table (98..105), then vs the bin boxes (box-box) */
+  /* pairs 143..190: the finger pads vs the table (143..150), then vs the bin boxes (box-box) */
   for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_PADBIN0; p++) pad_table(m, d, p);
   for (int p = SO100_PAIR_PADBIN0; p < SO100_NPAIR; p++) collide_box_pair(m, d, p);
 }

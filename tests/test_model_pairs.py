@@ -1,6 +1,6 @@
-"""The model's contact-pair table (gym_so100/assets/so100_model.json, 155 pairs) against MuJoCo's collision
-filters applied to the reference MJCF: every pair in the table is one MuJoCo would hand
-to a narrowphase, and of MuJoCo's pairs only the 36 finger-pad/link-hull pairs are missing.  Filters restated from MuJoCo 3.3.3's broadphase (mj_collision /
+"""The model's contact-pair table (gym_so100/assets/so100_model.json, 191 pairs) against MuJoCo's collision
+filters applied to the reference MJCF: the table is exactly the pair set MuJoCo would hand
+to a narrowphase, no pair more, none missing.  Filters restated from MuJoCo 3.3.3's broadphase (mj_collision /
 filter): contype/conaffinity compatibility, same weld body (which includes static-static), the
 parent-child filter (skipped for world-welded bodies), and the model's <exclude> (so_arm100.xml:165-167).
 Reads the reference MJCF, so it runs only where /root/reference exists (this container)."""
@@ -49,13 +49,11 @@ def test_pair_table_is_mujocos_filtered_pair_set():
             want.add(frozenset((n1, n2)))
     model = json.load(open(os.path.join(ROOT, "gym-so100-c_amd", "gym_so100", "assets", "so100_model.json")))
     have = {frozenset((p["name1"], p["name2"])) for p in model["pairs"]}
-    assert len(have) == len(model["pairs"]) == 155
+    assert len(have) == len(model["pairs"]) == 191
     assert not have - want, sorted(map(sorted, have - want))     # no pair MuJoCo would filter out
-    # the one documented gap (DESIGN.md §4 deviation 1): the finger pads against the arm's own link
-    # hulls — 4 links for the fixed-jaw pads (Wrist_Pitch_Roll is their parent), 5 for the moving-jaw
-    # pads; the pads sit inside the jaw hulls, whose pairs with those links are collided
-    links = {"Base", "Rotation_Pitch", "Upper_Arm", "Lower_Arm", "Wrist_Pitch_Roll"}
-    gap = {frozenset((f"{side}_jaw_pad_{i}", h)) for side in ("fixed", "moving") for i in range(1, 5)
-           for h in links if not (side == "fixed" and h == "Wrist_Pitch_Roll")}
-    assert want - have == gap, sorted(map(sorted, (want - have) ^ gap))
-    assert len(gap) == 36
+    assert not want - have, sorted(map(sorted, want - have))     # none missing: round 2 added the 36
+    # finger-pad / link-hull pairs (4 links for the fixed-jaw pads, Wrist_Pitch_Roll being their parent, 5
+    # for the moving-jaw pads)
+    pads = [p for p in model["pairs"] if p["name1"].endswith(("_pad_1", "_pad_2", "_pad_3", "_pad_4"))
+            and p["g2"] < 0]
+    assert len(pads) == 36

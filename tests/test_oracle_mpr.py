@@ -276,7 +276,7 @@ def test_base_contacts_are_real_overlaps(model, oracle64):
     depth; arm poses whose link hulls the LP proves disjoint from the Base get no such contact.  The
     Base/Rotation_Pitch exclude (so_arm100.xml:165-167) leaves hull 0 out."""
     from scipy.optimize import linprog
-    from gym_so100.model import PAIR_BASE0, PAIR_PAD0, HULL_BASE
+    from gym_so100.model import PAIR_BASE0, PAIR_PADLINK0 as PAIR_PAD0, HULL_BASE   # the Base pairs end here
     rng = np.random.default_rng(21)
     lo = np.array([r[0] for r in model.jnt_range]); hi = np.array([r[1] for r in model.jnt_range])
     assert model.hull_body[HULL_BASE] == 1
@@ -333,3 +333,57 @@ def test_base_contacts_are_real_overlaps(model, oracle64):
         assert bool(cons) == (t > 0), (t, len(cons))
         hit += bool(cons)
     assert hit >= 5
+
+
+def test_pad_link_contacts_are_real_overlaps(model, oracle64):
+    """The finger pads against the arm's own link hulls (pairs 107..142, round 2: the last 36 of the 191
+    pairs MuJoCo's filters leave): every MPR contact is between a pad box and a link hull that an LP shows
+    to intersect, overlapping along the normal (pad -> hull) by at least the reported depth; pads an LP
+    proves to overlap a link by more than the tolerance always get their contact.  Random arm poses fold the
+    jaws onto the links."""
+    from scipy.optimize import linprog
+    from gym_so100.model import PAIR_PADLINK0, PAIR_PAD0
+    rng = np.random.default_rng(33)
+    lo = np.array([r[0] for r in model.jnt_range]); hi = np.array([r[1] for r in model.jnt_range])
+    assert PAIR_PAD0 - PAIR_PADLINK0 == 36
+
+    def world(d, k):
+        b = model.hull_body[k]
+        R, p = np.array(d.xmat[b][:]).reshape(3, 3), np.array(d.xpos[b][:])
+        return _hull(model, k) @ R.T + p
+
+    def depth_lp(V1, V2):
+        H1, H2 = ConvexHull(V1).equations, ConvexHull(V2).equations
+        A = np.vstack([H1[:, :3], H2[:, :3]])
+        b = -np.concatenate([H1[:, 3], H2[:, 3]])
+        res = linprog(c=[0, 0, 0, -1], A_ub=np.hstack([A, np.ones((len(A), 1))]), b_ub=b,
+                      bounds=[(None, None)] * 3 + [(None, 1.0)], method="highs")
+        return -res.fun
+    checked = overlaps = 0
+    for _ in range(600):
+        d = _state(oracle64, model, rng.uniform(lo, hi), (0.4, 0.95, 0.6, 1, 0, 0, 0))
+        if d.ncon_dropped:
+            continue
+        got = {d.con[i].pair: d.con[i] for i in range(d.ncon) if PAIR_PADLINK0 <= d.con[i].pair < PAIR_PAD0}
+        for p in range(PAIR_PADLINK0, PAIR_PAD0):
+            g, k = model.pair_geom1[p], -1 - model.pair_geom2[p]
+            R = np.array(d.geom_xmat[g][:]).reshape(3, 3)
+            pad = _box_corners(np.array(d.geom_xpos[g][:]), R, np.array(model.geom_size[g][:]))
+            link = world(d, k)
+            lc = link.mean(0)
+            if p not in got and (np.linalg.norm(pad.mean(0) - lc) > np.linalg.norm(pad - pad.mean(0), axis=1).max()
+                                 + np.linalg.norm(link - lc, axis=1).max()):
+                continue                           # bounding spheres apart: no overlap to miss
+            t = depth_lp(pad, link)
+            if p in got:
+                c = got[p]
+                assert t > -1e-9, (p, t)
+                n = np.array(c.frame[:3])
+                assert (pad @ n).max() - (link @ n).min() >= -c.dist - 1e-9
+                checked += 1
+            elif t > 1e-6:
+                overlaps += 1                      # an overlap without its contact: must not happen
+        if checked >= 30:
+            break
+    assert overlaps == 0
+    assert checked >= 15, checked
