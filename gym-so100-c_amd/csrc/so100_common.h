@@ -44,6 +44,27 @@ DEV float rowsum16(float v) {
   v += dpp<0x140>(v);  // row_mirror
   return v;
 }
+template <int CTRL>
+DEV int dppi(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true); }
+// one butterfly step of arg_best16: keep the better (score, index) of this lane and its DPP partner, the
+// lower index among equal scores; the point (x, y, z) follows its score
+template <int CTRL, bool kMin>
+DEV void arg_best_step(float& s, int& i, float& x, float& y, float& z) {
+  const float os = dpp<CTRL>(s), ox = dpp<CTRL>(x), oy = dpp<CTRL>(y), oz = dpp<CTRL>(z);
+  const int oi = dppi<CTRL>(i);
+  const bool t = (kMin ? os < s : os > s) || (os == s && oi < i);
+  s = t ? os : s; i = t ? oi : i; x = t ? ox : x; y = t ? oy : y; z = t ? oz : z;
+}
+// the best (max, or min with kMin) score of the 16 lanes of this DPP row, first index among ties, with its
+// point, in every lane of the row (the selection is commutative, so all lanes agree bitwise).  The whole
+// row must be active.
+template <bool kMin>
+DEV void arg_best16(float& s, int& i, float& x, float& y, float& z) {
+  arg_best_step<0xB1, kMin>(s, i, x, y, z);    // quad_perm [1,0,3,2]
+  arg_best_step<0x4E, kMin>(s, i, x, y, z);    // quad_perm [2,3,0,1]
+  arg_best_step<0x141, kMin>(s, i, x, y, z);   // row_half_mirror
+  arg_best_step<0x140, kMin>(s, i, x, y, z);   // row_mirror
+}
 // ------------------------------------------------------------------ row broadcast (DPP row_newbcast, gfx90a+)
 template <int L>
 DEV float bcast_row_c(float v) { return dpp<0x150 + L>(v); }

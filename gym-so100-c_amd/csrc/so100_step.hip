@@ -939,12 +939,7 @@ DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lan
         if (in && wz < bz) { bz = wz; bx = wx; by = wy; bi = i; }
       }
     }
-#pragma unroll
-    for (int off = 1; off < kLanes; off <<= 1) {
-      const float oz = __shfl_xor(bz, off, kLanes), ox = __shfl_xor(bx, off, kLanes), oy = __shfl_xor(by, off, kLanes);
-      const int oi = __shfl_xor(bi, off, kLanes);
-      if (oz < bz || (oz == bz && oi < bi)) { bz = oz; bx = ox; by = oy; bi = oi; }
-    }
+    arg_best16<true>(bz, bi, bx, by, bz);   // the score is the point's z (passed as both)
     if (lane == k) {
       found = mine && bi != 0x7fffffff && (bz - top < m->pair_margin[SO100_NPAIR_BOX + k]);
       hx = bx; hy = by; hz = bz;
@@ -1019,13 +1014,7 @@ DEV float3 hull_support(const DevModel* __restrict__ m, int s0, int cnt, float n
       bx = t ? vb[u].x : bx; by = t ? vb[u].y : by; bz = t ? vb[u].z : bz;
     }
   }
-#pragma unroll
-  for (int off = 1; off < kLanes; off <<= 1) {
-    const float os = __shfl_xor(best, off, kLanes), ox = __shfl_xor(bx, off, kLanes);
-    const float oy = __shfl_xor(by, off, kLanes), oz = __shfl_xor(bz, off, kLanes);
-    const int oi = __shfl_xor(bi, off, kLanes);
-    if (os > best || (os == best && oi < bi)) { best = os; bi = oi; bx = ox; by = oy; bz = oz; }
-  }
+  arg_best16<false>(best, bi, bx, by, bz);
   return make_float3(bx, by, bz);
 }
 
@@ -2486,6 +2475,9 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 #ifndef SO100_LAUNDER_IDS
 #define SO100_LAUNDER_IDS 1
 #endif
+#ifndef SO100_PRIO
+#define SO100_PRIO 1
+#endif
 #ifndef SO100_FUSED_WAVES
 #define SO100_FUSED_WAVES 3
 #endif
@@ -2524,6 +2516,14 @@ __global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kerne
   const int grp0 = tid >> 4;
   const int lane0 = tid & 15;
   const int group = args.w.order ? args.w.order[blockIdx.x] : (int)blockIdx.x;   // heavy-first (so100_order_kernel)
+#if SO100_PRIO
+  if (args.w.order) {   // the heavier half of the waves, by launch rank, issue first on their SIMD
+    const unsigned rank = blockIdx.x, ng = gridDim.x;
+    if (rank < ng / 8) __builtin_amdgcn_s_setprio(3);
+    else if (rank < ng / 4) __builtin_amdgcn_s_setprio(2);
+    else if (rank < ng / 2) __builtin_amdgcn_s_setprio(1);
+  }
+#endif
   const int env0 = group * kEnvsPerBlock + grp0;
   const int e0 = env0 < args.n ? env0 : 0;
   {
@@ -2716,7 +2716,11 @@ hipError_t launch_newton(const DevModel* m, const Workspace& w, float* qacc_out,
 // in descending order of their previous step's cost: a counting sort on a 12-bit float key (exponent + 4
 // mantissa bits, 6 % buckets), one workgroup.  The order changes the schedule, never a result.
 constexpr int kOrderBuckets = 4096;
+#if SO100_PRIO
+constexpr int kOrderMinGroups = 256;           // the order also sets the waves' issue priority
+#else
 constexpr int kOrderMinGroups = 3072;          // up to the resident capacity (12 waves x 256 CUs) all start at once
+#endif
 __global__ void __launch_bounds__(1024) so100_order_kernel(const uint32_t* __restrict__ gcost, int ng,
                                                            int* __restrict__ order) {
   __shared__ int hist[kOrderBuckets];
