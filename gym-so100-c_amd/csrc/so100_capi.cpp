@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 #include "so100.h"
@@ -87,6 +89,7 @@ struct so100_env {
   hipStream_t cap_s = nullptr;
   std::vector<StepGraph> graphs;
   uint64_t graph_clock = 0;
+  float4* d_cand = nullptr;     // the hulls' support-cell candidates (DevModel::hull_cand)
 };
 
 // An instantiated step graph can still be running when it is evicted: wait for its last replay first.
@@ -517,6 +520,95 @@ extern "C" {
 int so100_abi_version(void) { return SO100_ABI_VERSION; }
 const char* so100_last_error(void) { return g_err.c_str(); }
 
+// ---- support-direction cells of the hulls (so100_hull_cells, include/so100.h).  For each cube-map cell
+// (face f: axis f / 2, sign f % 2; cell (cu, cv) of u = n_a / |n_axis|, v = n_b / |n_axis|, a < b the other
+// axes) the candidates are the vertices not beaten over the whole cell by one vertex of a sample support set
+// S by >= kCellMargin: (v_j - v_i) . d is affine in (u, v), so its minimum over the (widened) cell is at a
+// corner.  A vertex that is the support for some direction of the cell, or within kCellMargin of it, is never
+// left out, so fp32 scans of the list and of the hull agree (the fp32 winner is within rounding, << the
+// margin, of the exact maximum).  Deterministic: a function of the model only.
+static constexpr double kCellWiden = 1e-3, kCellMargin = 1e-6;
+static void hull_cells_build(const so100_model* s, std::vector<uint32_t>& cells, std::vector<float>& cand) {
+  constexpr int G = SO100_HULL_CELLG;
+  cells.assign((size_t)SO100_NHULL_ALL * SO100_HULL_NCELL, 0u);
+  cand.clear();
+  std::vector<double> V, P;
+  std::vector<int> S;
+  for (int k = 0; k < SO100_NHULL_ALL; k++) {
+    const int n = s->hull_count[k], s0 = s->hull_start[k];
+    V.resize(3 * (size_t)n);
+    for (int i = 0; i < n; i++)
+      for (int t = 0; t < 3; t++) V[3 * i + t] = (double)(float)s->hull_vert[s0 + i][t];   // the device's values
+    P.resize(4 * (size_t)n);
+    for (int f = 0; f < 6; f++) {
+      const int ax = f / 2, a = ax == 0 ? 1 : 0, b = ax == 2 ? 1 : 2;
+      const double sg = (f & 1) ? -1.0 : 1.0;
+      for (int cu = 0; cu < G; cu++)
+        for (int cv = 0; cv < G; cv++) {
+          const double u0 = -1.0 + 2.0 * cu / G - kCellWiden, u1 = -1.0 + 2.0 * (cu + 1) / G + kCellWiden;
+          const double v0 = -1.0 + 2.0 * cv / G - kCellWiden, v1 = -1.0 + 2.0 * (cv + 1) / G + kCellWiden;
+          auto score = [&](int i, double u, double v) { return sg * V[3 * i + ax] + u * V[3 * i + a] + v * V[3 * i + b]; };
+          // sample supports (first maximal vertex) on a 7 x 7 grid of the widened cell
+          S.clear();
+          for (int su = 0; su < 7; su++)
+            for (int sv = 0; sv < 7; sv++) {
+              const double u = u0 + (u1 - u0) * su / 6.0, v = v0 + (v1 - v0) * sv / 6.0;
+              int bi = 0;
+              double bs = score(0, u, v);
+              for (int i = 1; i < n; i++) {
+                const double sc = score(i, u, v);
+                if (sc > bs) { bs = sc; bi = i; }
+              }
+              if (std::find(S.begin(), S.end(), bi) == S.end()) S.push_back(bi);
+            }
+          const double cu4[4] = {u0, u0, u1, u1}, cv4[4] = {v0, v1, v0, v1};
+          for (int i = 0; i < n; i++)
+            for (int c = 0; c < 4; c++) P[4 * i + c] = score(i, cu4[c], cv4[c]);
+          const size_t start = cand.size() / 4;
+          int cnt = 0;
+          for (int i = 0; i < n; i++) {
+            bool beaten = false;
+            for (int j : S) {
+              if (j == i) continue;
+              double mn = P[4 * j] - P[4 * i];
+              for (int c = 1; c < 4; c++) mn = std::min(mn, P[4 * j + c] - P[4 * i + c]);
+              if (mn >= kCellMargin) { beaten = true; break; }
+            }
+            if (beaten) continue;
+            float w;
+            std::memcpy(&w, &i, sizeof(w));
+            cand.insert(cand.end(), {(float)V[3 * i], (float)V[3 * i + 1], (float)V[3 * i + 2], w});
+            cnt++;
+          }
+          uint32_t& e = cells[(size_t)k * SO100_HULL_NCELL + (size_t)(f * G + cu) * G + cv];
+          if (cnt > 255 || start > 0xFFFFFFu) {
+            cand.resize(start * 4);          // too many for the 8-bit count: the kernel scans the whole hull
+            e = 0u;
+          } else {
+            e = (uint32_t)start << 8 | (uint32_t)cnt;
+          }
+        }
+    }
+  }
+}
+
+int so100_hull_cells(const so100_model* model, uint32_t* cells, float* cand, int cap) {
+  if (!model) return fail("so100_hull_cells: model is NULL");
+  for (int k = 0; k < SO100_NHULL_ALL; k++)
+    if (model->hull_start[k] < 0 || model->hull_count[k] < 1 || model->hull_start[k] + model->hull_count[k] > SO100_HULL_NVERT)
+      return fail("so100_hull_cells: hull vertex range");
+  std::vector<uint32_t> c;
+  std::vector<float> v;
+  hull_cells_build(model, c, v);
+  const int nc = (int)(v.size() / 4);
+  if (cells) std::memcpy(cells, c.data(), c.size() * sizeof(uint32_t));
+  if (cand) {
+    if (cap < nc) return fail("so100_hull_cells: cap too small");
+    std::memcpy(cand, v.data(), v.size() * sizeof(float));
+  }
+  return nc;
+}
+
 int so100_struct_sizes(int* model_bytes, int* buffers_bytes) {
   if (model_bytes) *model_bytes = (int)sizeof(so100_model);
   if (buffers_bytes) *buffers_bytes = (int)sizeof(so100_buffers);
@@ -533,12 +625,23 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   DevModel h;
   if (build_device_model(model, &h) != 0) return nullptr;
   DeviceGuard g(device);
+  // the hulls' support cells: the table in the model, the candidates in their own buffer
+  std::vector<uint32_t> hc;
+  std::vector<float> hv;
+  hull_cells_build(model, hc, hv);
+  std::memcpy(h.hull_cells, hc.data(), sizeof(h.hull_cells));
+  float4* dcand = nullptr;
+  e = hipMalloc(&dcand, std::max<size_t>(hv.size(), 4) * sizeof(float));
+  if (e == hipSuccess && !hv.empty()) e = hipMemcpy(dcand, hv.data(), hv.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { if (dcand) (void)hipFree(dcand); fail_hip("so100_create: hull cells", e); return nullptr; }
+  h.hull_cand = reinterpret_cast<const so100::float4_t*>(dcand);
   DevModel* dm = nullptr;
   e = hipMalloc(&dm, sizeof(DevModel));
-  if (e != hipSuccess) { fail_hip("so100_create: hipMalloc", e); return nullptr; }
+  if (e != hipSuccess) { (void)hipFree(dcand); fail_hip("so100_create: hipMalloc", e); return nullptr; }
   e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { (void)hipFree(dm); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
+  if (e != hipSuccess) { (void)hipFree(dm); (void)hipFree(dcand); fail_hip("so100_create: hipMemcpy", e); return nullptr; }
   so100_env* env = new so100_env{device, n_envs, dm, h.nsubstep, h.solver, -1, kFusedAutoMax, {}, false, {}, nullptr, SO100_TASK_CUBE_TO_BIN, 700, 0, 0, {}, 0, 0};
+  env->d_cand = dcand;
   if (const char* v = getenv("SO100_GRAPH")) env->use_graph = atoi(v) != 0;
   if (const char* v = getenv("SO100_FUSED")) env->fused = atoi(v) < 0 ? -1 : atoi(v) != 0;   // A/B: 0 split, 1 fused
   if (const char* v = getenv("SO100_FUSED_MAX")) env->fused_max = atoi(v);
@@ -550,6 +653,7 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (e != hipSuccess) {
     (void)free_chunks(env);
     (void)hipFree(dm);
+    (void)hipFree(dcand);
     delete env;
     fail_hip("so100_create: workspace", e);
     return nullptr;
@@ -567,6 +671,7 @@ int so100_destroy(so100_env* env) {
   if (env->r_body) (void)hipFree(env->r_body);
   if (env->r_rgb) (void)hipFree(env->r_rgb);
   hipError_t e = hipFree(env->d_model);
+  if (env->d_cand) (void)hipFree(env->d_cand);
   hipError_t e2 = free_chunks(env);
   if (e == hipSuccess) e = e2;
   if (e == hipSuccess) e = so100::free_workspace(&env->fws);

@@ -82,6 +82,10 @@ struct DevModel {
   float4_t hull_center[SO100_NHULL_ALL], hull_half[SO100_NHULL_ALL];   // hull_half.w = |half extents|
   float4_t hull_centroid[SO100_NHULL_ALL];   // MPR portal centre (mesh volume centroid), body frame
   float4_t hull_vert[SO100_HULL_NVERT];
+  // MPR support lookup (so100_hull_cells): hull k's cube-map cells at k * SO100_HULL_NCELL, start << 8 | count
+  // into hull_cand (x, y, z, vertex index bits; count 0: scan the hull)
+  uint32_t hull_cells[SO100_NHULL_ALL * SO100_HULL_NCELL];
+  const float4_t* hull_cand;
   float table_top, table_lo[2], table_hi[2];
 
   // sites

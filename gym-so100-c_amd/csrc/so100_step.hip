@@ -966,7 +966,8 @@ struct MprObj {
   float hc[3];                      // obj2 (hull) centroid in H
   int hull1;                        // obj1: -1 a box, else a hull (self-collision); uniform over the wave
   int s1, n1;                       // obj1 hull vertex range
-  int s0, n;                        // obj2 hull vertex range
+  int k, s0, n;                     // obj2: hull index, vertex range
+  bool cells;                       // hull supports through the direction cells (fused kernel) or full scans
 };
 constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
 constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
@@ -995,12 +996,49 @@ DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
   }
 }
 
-// first vertex of hull range [s0, s0 + n) maximising (n0, n1, n2) . v: lanes split the vertices, then a
-// 16-lane (score, index) max keeps the oracle's first maximal vertex; every lane of the row gets it
-DEV float3 hull_support(const DevModel* __restrict__ m, int s0, int cnt, float n0, float n1, float n2, int lane) {
-  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + s0;
+// first vertex of hull k (vertex range [s0, s0 + n)) maximising (n0, n1, n2) . v: lanes split the
+// candidates, then a 16-lane (score, index) max keeps the oracle's first maximal vertex; every lane of the
+// row gets it.  The candidates are those of the direction's cube-map cell (so100_hull_cells: a superset of
+// the cell's possible supports, in vertex order, so the same vertex as a scan of the whole hull, which
+// remains for a cell whose list did not fit and for a zero or non-finite direction).  The direction is
+// uniform over the row, so is the path.
+DEV float3 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s0, int cnt, float n0, float n1, float n2,
+                        int lane) {
   float best = -__builtin_inff(), bx = 0.f, by = 0.f, bz = 0.f;
   int bi = 0x7fffffff;
+  {
+    const float a0 = fabsf(n0), a1 = fabsf(n1), a2 = fabsf(n2);
+    const bool fx = a0 >= a1 && a0 >= a2, fy = !fx && a1 >= a2;
+    const float am = fx ? a0 : fy ? a1 : a2;
+    uint32_t e = 0u;
+#ifdef SO100_NO_HULL_CELLS
+    if (false) {                             // A/B diagnostic builds only: the whole-hull scan
+#else
+    if (cells && am > 1e-30f && am < __builtin_inff()) {
+#endif
+      const float na = fx ? n0 : fy ? n1 : n2, nu = fx ? n1 : n0, nv = (fx || fy) ? n2 : n1;
+      const float g = 0.5f * (float)SO100_HULL_CELLG / am;
+      const int cu = min(max((int)((nu + am) * g), 0), SO100_HULL_CELLG - 1);
+      const int cv = min(max((int)((nv + am) * g), 0), SO100_HULL_CELLG - 1);
+      const int face = 2 * (fx ? 0 : fy ? 1 : 2) + (na >= 0.f ? 0 : 1);
+      e = m->hull_cells[k * SO100_HULL_NCELL + (face * SO100_HULL_CELLG + cu) * SO100_HULL_CELLG + cv];
+    }
+    const int cc = (int)(e & 255u);
+    if (cc > 0) {
+      const float4* __restrict__ cand = reinterpret_cast<const float4*>(m->hull_cand) + (e >> 8);
+      for (int base = lane; base < cc; base += 2 * kLanes) {
+        const float4 c0 = cand[base];
+        const float4 c1 = cand[min(base + kLanes, cc - 1)];
+        const float s0c = n0 * c0.x + n1 * c0.y + n2 * c0.z;
+        if (s0c > best) { best = s0c; bi = __float_as_int(c0.w); bx = c0.x; by = c0.y; bz = c0.z; }
+        const float s1c = n0 * c1.x + n1 * c1.y + n2 * c1.z;
+        if (base + kLanes < cc && s1c > best) { best = s1c; bi = __float_as_int(c1.w); bx = c1.x; by = c1.y; bz = c1.z; }
+      }
+      arg_best16<false>(best, bi, bx, by, bz);
+      return make_float3(bx, by, bz);
+    }
+  }
+  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + s0;
   for (int base = lane; base < cnt; base += 8 * kLanes) {
     float4 vb[8];
 #pragma unroll
@@ -1033,13 +1071,13 @@ DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const floa
     // obj1 hull: the direction into its body frame, its support back into H
     float dl[3], w[3];
     mulmtv3(dl, o.ax, d);
-    const float3 v = hull_support(m, o.s1, o.n1, dl[0], dl[1], dl[2], lane);
+    const float3 v = hull_support(m, o.cells, o.hull1, o.s1, o.n1, dl[0], dl[1], dl[2], lane);
     const float vv[3] = {v.x, v.y, v.z};
     mulmv3(w, o.ax, vv);
 #pragma unroll
     for (int t = 0; t < 3; t++) s.v1[t] += w[t];
   }
-  const float3 v = hull_support(m, o.s0, o.n, -d[0], -d[1], -d[2], lane);
+  const float3 v = hull_support(m, o.cells, o.k, o.s0, o.n, -d[0], -d[1], -d[2], lane);
   s.v2[0] = v.x; s.v2[1] = v.y; s.v2[2] = v.z;
   sub3(s.v, s.v1, s.v2);
 }
@@ -1291,6 +1329,8 @@ DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int 
   }
   const float4 hc = reinterpret_cast<const float4*>(m->hull_centroid)[k];
   o.hc[0] = hc.x; o.hc[1] = hc.y; o.hc[2] = hc.z;
+  o.k = k;
+  o.cells = false;
   o.s0 = m->hull_start[k];
   o.n = m->hull_count[k];
 }
@@ -1379,6 +1419,7 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
 //    pair of the wave's union per round, on the rows holding it: 60 % of the slowest waves' assembly);
 //  * each round's hits go to their env's staging slots in list order, so each env keeps its pair order.
 // Returns the env's number of staged contacts (uniform across its row, capped at kMaxCon).
+template <bool kCells>
 DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, int grp, bool valid) {
 #ifdef SO100_EXPERIMENT_NO_MPR
   return 0;   // timing experiment only: box-hull contacts off
@@ -1443,6 +1484,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
       p = SO100_PAIR_MPR0 + list[item];
       MprObj o;
       mpr_obj_setup(m, shm[ie], p, o);
+      o.cells = kCells;
       hit = mpr_penetration(m, o, depth, dir, pos, lane);
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
@@ -1918,7 +1960,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
     SSTAMP(6);
-    const int nmpr = mpr_contacts(m, &sh - grp, lane, grp, valid);
+    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, lane, grp, valid);
     SSTAMP(7);
     PairContacts pc;
     pc.n = 0;

@@ -44,7 +44,9 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 9          # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 10         # include/so100.h SO100_ABI_VERSION
+HULL_CELLG = 8           # SO100_HULL_CELLG
+HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 
 
 def load():
@@ -78,10 +80,11 @@ def load():
     lib.so100_step_mode.argtypes = [_P]
     lib.so100_render_mesh.argtypes = [_P, _P, _P, _P, ctypes.c_int]
     lib.so100_render.argtypes = [_P, _P, _P, ctypes.POINTER(SO100Camera), ctypes.c_int, ctypes.c_int, _P, _P]
+    lib.so100_hull_cells.argtypes = [_P, _P, _P, ctypes.c_int]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
                "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info",
-               "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode"):
+               "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
     lib.so100_struct_sizes.restype = ctypes.c_int
@@ -101,7 +104,7 @@ EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
                     "so100_contact_count", "so100_chunk_info", "so100_render_mesh", "so100_render",
-                    "so100_set_step_mode", "so100_step_mode")
+                    "so100_set_step_mode", "so100_step_mode", "so100_hull_cells")
 
 
 def check(rc, what):

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 9   /* 9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 10  /* 10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -122,6 +122,19 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
  * (stage: 0) and so100_chunk_info reports 1 chunk of N envs. */
 int so100_set_step_mode(so100_env* env, int fused);
 int so100_step_mode(const so100_env* env);
+
+/* Support-direction cells of the convex hulls (host only; no device needed).  The MPR collider's hull
+ * support (the first vertex maximising n . v, MuJoCo's mesh support by exhaustive scan) reads a candidate
+ * list instead of the whole hull: the direction's cube-map face (largest |n_k|) and its G x G cell on that
+ * face select the vertices that can be the support for some direction of the cell (a vertex beaten by one
+ * other vertex by >= 1e-6 over the whole cell, its bounds widened by 1e-3, is left out), so the scan of the
+ * list returns the same vertex as the scan of the hull.
+ *   cells[SO100_NHULL_ALL * SO100_HULL_NCELL]: hull k, face f (2 axis + (n_axis < 0)), cell (cu, cv) at
+ *     k * NCELL + (f * G + cu) * G + cv: start << 8 | count (count 0: scan the whole hull);
+ *   cand[cap][4]: x, y, z (the hull vertex as float) and the vertex index within the hull (as float bits).
+ * Returns the number of candidates (cand may be NULL to query it), -1 on error. */
+/* (SO100_HULL_CELLG, SO100_HULL_NCELL: so100_model.h) */
+int so100_hull_cells(const so100_model* model, uint32_t* cells, float* cand, int cap);
 
 /* Number of env chunks and the env count of chunk 0 (the launches so100_profile_read times). */
 int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs);

@@ -54,6 +54,8 @@
 #define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 191: every pair MuJoCo's filters leave */
 #define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
+#define SO100_HULL_CELLG 8          /* support-direction cells per cube-map face edge (so100_hull_cells) */
+#define SO100_HULL_NCELL (6 * SO100_HULL_CELLG * SO100_HULL_CELLG)   /* cells per hull */
 #define SO100_CUBE_BODY 8
 #define SO100_CUBE_GEOM 9
 #define SO100_PAIR_TABLE 8          /* ("red_box", "table") — single_arm.py:354 touch_table */
