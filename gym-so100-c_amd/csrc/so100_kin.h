@@ -199,4 +199,92 @@ DEV void fk_stage(const DevModel* __restrict__ m, EnvShared& sh) {
   }
 }
 
+// Forward kinematics with the 16 lanes of the env's row (lane a < 6: body a of the chain; lane 6: the cube):
+// the same frames as fk_stage from the staged qpos (a barrier must separate the qpos stores), without its
+// serial chain on one lane.  fk_stage's per-body product q_a = normalize(q_{a-1} (x) qb_a (x) qj_a) becomes
+// a prefix product over the lanes of c_a = qb_a (x) qj_a (3 DPP steps), normalised once per body; the
+// positions pos_a = pos_{a-1} + R_{a-1} body_pos[a] a prefix sum (3 DPP steps); the joint axis R_a
+// jnt_axis[a] (the joint rotation leaves its axis fixed: fk_stage's pre-rotation frame gives the same axis).
+// Equal to fk_stage up to fp32 rounding (association), which the parity tests' tolerances cover.
+// row_shr:D with a fill: lane l of the row gets v of lane l - D, lanes l < D get `old` (no select, so the
+// compiler cannot put the DPP under an exec mask that disables its source lanes, which then read 0)
+template <int D>
+DEV float fk_shr(float old, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                0x110 + D, 0xF, 0xF, false));
+}
+DEV void fk_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, bool act = true) {
+  const bool arm = lane < 6;
+  const int a = arm ? lane : 5;
+  float c[4];
+  {
+    float sn, cs;
+    sincosf(0.5f * sh.qpos[a], &sn, &cs);
+    const float qj[4] = {cs, m->jnt_axis[a][0] * sn, m->jnt_axis[a][1] * sn, m->jnt_axis[a][2] * sn};
+    float t[4], u[4];
+    quat_mul(t, m->body_quat[a], qj);
+    quat_mul(u, m->base_quat, t);                 // lane 0 starts from the Base's frame
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = lane == 0 ? u[k] : (arm ? t[k] : (k == 0 ? 1.f : 0.f));
+  }
+  // inclusive prefix product over lanes 0..5 (left factor: the earlier lanes)
+#define FK_SCAN_Q(D)                                                                             \
+  {                                                                                              \
+    float p[4];                                                                                  \
+    for (int k = 0; k < 4; k++) p[k] = fk_shr<D>(k == 0 ? 1.f : 0.f, c[k]);   /* identity fill */  \
+    quat_mul(c, p, c);                                                                           \
+  }
+  FK_SCAN_Q(1) FK_SCAN_Q(2) FK_SCAN_Q(4)
+#undef FK_SCAN_Q
+  quat_normalize(c);
+  float R[9], Rp[9], Rb[9];
+  quat2mat(R, c);
+  quat2mat(Rb, m->base_quat);
+#pragma unroll
+  for (int k = 0; k < 9; k++) Rp[k] = fk_shr<1>(Rb[k], R[k]);   // the parent's frame (lane 0: the Base's)
+  float t[3];
+  mulmv3(t, Rp, m->body_pos[a]);
+#define FK_SCAN_P(D)                                                                             \
+  {                                                                                              \
+    for (int k = 0; k < 3; k++) t[k] += fk_shr<D>(0.f, t[k]);                                    \
+  }
+  FK_SCAN_P(1) FK_SCAN_P(2) FK_SCAN_P(4)
+#undef FK_SCAN_P
+  const float pos[3] = {m->base_pos[0] + t[0], m->base_pos[1] + t[1], m->base_pos[2] + t[2]};
+  float ax[3];
+  mulmv3(ax, R, m->jnt_axis[a]);
+  if (act && arm) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) { sh.anchor[a][k] = pos[k]; sh.axis[a][k] = ax[k]; sh.ser.xp[a][k] = pos[k]; }
+#pragma unroll
+    for (int k = 0; k < 9; k++) sh.ser.xm[a][k] = R[k];
+    if (a >= 4) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) sh.jaw_pos[a - 4][k] = pos[k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) sh.jaw_mat[a - 4][k] = R[k];
+    }
+    if (a == 4) {
+      float w[3];
+      mulmv3(w, R, m->site_ee);
+#pragma unroll
+      for (int k = 0; k < 3; k++) sh.site_ee[k] = pos[k] + w[k];
+    }
+  }
+  if (act && lane == 6) {
+    float qp[7], cpos[3], cmat[9];
+#pragma unroll
+    for (int k = 0; k < 7; k++) qp[k] = sh.qpos[6 + k];
+    cube_frame(qp, cpos, cmat);
+#pragma unroll
+    for (int k = 0; k < 3; k++) sh.cube_pos[k] = cpos[k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) sh.cube_mat[k] = cmat[k];
+    float w[3];
+    mulmv3(w, cmat, m->site_cube);
+#pragma unroll
+    for (int k = 0; k < 3; k++) sh.site_cube[k] = cpos[k] + w[k];
+  }
+}
+
 }  // namespace so100

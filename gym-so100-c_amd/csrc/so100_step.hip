@@ -175,6 +175,30 @@ DEV float hash_normal(uint64_t key) {
   return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
 }
 
+// Diagnostic builds only: SSTAMP_RAW accumulates the shader cycles since the last stamp into slot (-1: none).
+// With -DSO100_DYN_STAMPS the stage stamps cover the position / dynamics stage's phases instead (DSTAMP,
+// slots 0..7: sincos, FK, comPos, CRBA, Cholesky, M^-1 + RNE velocities, RNE forces, bias + qacc_smooth).
+#ifdef SO100_STAGE_STAMPS
+#define SSTAMP_RAW(slot)                                                                         \
+  do {                                                                                           \
+    unsigned long long t_;                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if ((slot) >= 0) sst_acc_[(slot) & 7] += t_ - sst_prev_;                                     \
+    sst_prev_ = t_;                                                                              \
+  } while (0)
+#endif
+#if defined(SO100_STAGE_STAMPS) && defined(SO100_DYN_STAMPS)
+#define DSTAMP_PARAMS , unsigned long long &sst_prev_, unsigned long long *sst_acc_
+#define DSTAMP_ARGS , sst_prev_, sst_acc_
+#define DSTAMP(slot) SSTAMP_RAW(slot)
+#else
+#define DSTAMP_PARAMS
+#define DSTAMP_ARGS
+#define DSTAMP(slot) do {} while (0)
+#endif
+
 // Lane-parallel dynamics stage (all 16 lanes of the env's row; lanes 0..5 = bodies/dofs of the arm):
 // comPos, CRBA, Cholesky (lane 0) + M^-1 columns, RNE and actuation, with every sum in the serial
 // order of the lane-0 version (prefix sums of cvel/cacc, suffix sums of crb/bias) so results are the
@@ -296,7 +320,7 @@ DEV void weld_fold(const DevModel* __restrict__ m, EnvShared& sh, int lane) {
   __syncthreads();
 }
 
-DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale) {
+DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale DSTAMP_PARAMS) {
   SerialScratch& S = sh.ser;
   // ---- comPos (body a = lane): cinert about the tree reference point r = Base xpos; cdof
   if (lane < 6) {
@@ -334,6 +358,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     for (int k = 0; k < 3; k++) { S.cdof[a][k] = ax[k]; S.cdof[a][3 + k] = lin[k]; }
   }
   __syncthreads();
+  DSTAMP(2);
   // ---- CRBA: composite inertia crb_i = cin_5 + ... + cin_i (that order), F_i = crb_i cdof_i
   if (lane < 6) {
     const int i = lane;
@@ -367,6 +392,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     }
   }
   __syncthreads();
+  DSTAMP(3);
   if (m->ee) weld_fold(m, sh, lane);
   // ---- Cholesky of the 6x6 (lane 0), diagonal reciprocals stored for the column solves
   if (lane == 0) {
@@ -394,6 +420,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     }
   }
   __syncthreads();
+  DSTAMP(4);
   // ---- M^-1 columns: lane c solves M x = e_c
   if (lane < 6) {
     const int c = lane;
@@ -441,6 +468,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     for (int k = 0; k < 6; k++) S.cdd[a][k] = cdd[k];
   }
   __syncthreads();
+  DSTAMP(5);
   // symmetrised M^-1 -> LDS (minv), RNE part 2: cacc_a = -g + sum_{k<=a} cdd_k qd_k, body forces
   if (lane < 6) {
     const int a = lane;
@@ -469,6 +497,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     for (int k = 0; k < 6; k++) S.cfrc[a][k] = f1[k] + f2[k];
   }
   __syncthreads();
+  DSTAMP(6);
   // ---- bias_a = cdof_a . sum_{k>=a} cfrc_k (suffix, from body 5 down); actuation
   if (lane < 6) {
     const int a = lane;
@@ -1684,18 +1713,14 @@ DEV void write_obs(const DevModel* __restrict__ m, const EnvShared& sh, int lane
 }
 
 // Diagnostic build only (-DSO100_STAGE_STAMPS): per-phase cycle attribution of the stage kernel
-// (substep nsubstep-1, mode 1), written to debug[88..93].
+// (substep nsubstep-1, mode 1), written to debug[88..93] (SSTAMP_RAW, DSTAMP: top of this file).
 #ifdef SO100_STAGE_STAMPS
 #define SSTAMP_DECL unsigned long long sst_prev_ = 0, sst_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define SSTAMP(slot)                                                                             \
-  do {                                                                                           \
-    unsigned long long t_;                                                                       \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    if ((slot) >= 0) sst_acc_[(slot) & 7] += t_ - sst_prev_;                                     \
-    sst_prev_ = t_;                                                                              \
-  } while (0)
+#ifdef SO100_DYN_STAMPS
+#define SSTAMP(slot) SSTAMP_RAW(-1)
+#else
+#define SSTAMP(slot) SSTAMP_RAW(slot)
+#endif
 #else
 #define SSTAMP_DECL
 #define SSTAMP(slot) do {} while (0)
@@ -1936,12 +1961,12 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
     __syncthreads();
     // ---------------- S2: serial kinematics / dynamics (lane 0 of each group)
-    joint_sincos(sh, lane);
+    fk_par(m, sh, lane);
     __syncthreads();
-    if (lane == 0) fk_stage(m, sh);
+    DSTAMP(1);
+    dynamics_par(m, sh, lane, mscale DSTAMP_ARGS);
     __syncthreads();
-    dynamics_par(m, sh, lane, mscale);
-    __syncthreads();
+    DSTAMP(7);
     if constexpr (kSolver == SO100_SOLVER_NEWTON) {
       // the Newton solver works with M itself: arm rows from the CRBA scratch (which collision reuses),
       // the cube's diagonal masses
@@ -2359,9 +2384,7 @@ DEV void final_stage(const StageArgs& args, EnvShared& sh, int lane, int grp, in
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   if (lane < SO100_NV) sh.qvel[lane] = qvel_r;
   __syncthreads();
-  joint_sincos(sh, lane);
-  __syncthreads();
-  if (lane == 0) fk_stage(m, sh);
+  fk_par(m, sh, lane);
   __syncthreads();
   float hx, hy, hz;
   const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
@@ -2435,9 +2458,7 @@ DEV void final_stage(const StageArgs& args, EnvShared& sh, int lane, int grp, in
     __syncthreads();
     if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
     __syncthreads();
-    joint_sincos(sh, lane, do_reset && valid);
-    __syncthreads();
-    if (lane == 0 && do_reset && valid) fk_stage(m, sh);
+    fk_par(m, sh, lane, do_reset && valid);
     __syncthreads();
     const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
     if (do_reset && valid) {
@@ -2673,9 +2694,7 @@ __global__ void __launch_bounds__(kThreads) so100_reset_kernel(ResetArgs args) {
   }
   if (lane < SO100_NQ) sh.qpos[lane] = qpos_r;
   __syncthreads();
-  joint_sincos(sh, lane, act);
-  __syncthreads();
-  if (lane == 0 && act) fk_stage(m, sh);
+  fk_par(m, sh, lane, act);
   __syncthreads();
   const float qv_r = bcast16(qpos_r, lane >= 9 ? lane - 9 : 0);
   if (act) {

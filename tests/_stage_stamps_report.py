@@ -1,5 +1,5 @@
 """Diagnostic: per-phase cycles of the stage kernel (mode 1, last substep); stage-stamps build via SO100_LIB.
-usage: SO100_LIB=<stamps build> python tests/_stage_stamps_report.py [solver] [n]"""
+usage: SO100_LIB=<stamps build> python tests/_stage_stamps_report.py [solver] [n] [dyn]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,6 +22,9 @@ for i in range(3):
 acc /= 3
 names = ["Euler", "S1-S2 FK + dynamics", "S3c box-box + compaction", "S6a J + reductions", "S6b per-contact setup",
          "S7 + record", "S3a hulls vs table", "S3b box-hull MPR"]
+if len(sys.argv) > 3 and sys.argv[3] == "dyn":     # -DSO100_DYN_STAMPS build: the S1-S2 phases
+    names = ["sincos", "FK chain (lane 0)", "comPos", "CRBA", "Cholesky (lane 0)", "M^-1 + RNE velocities",
+             "RNE forces", "bias + qacc_smooth"]
 for k, v in zip(names, acc):
     print(f"{k:24s} {v / 1e3:8.1f} Kcyc  {100 * v / acc.sum():5.1f}%")
 R = np.concatenate(rows)
