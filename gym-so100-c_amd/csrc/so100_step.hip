@@ -394,9 +394,12 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
   __syncthreads();
   DSTAMP(3);
   if (m->ee) weld_fold(m, sh, lane);
-  // ---- Cholesky of the 6x6 (lane 0), diagonal reciprocals stored for the column solves
-  if (lane == 0) {
-    float L[6][6], Linv[6];
+  // ---- Cholesky of the 6x6 on each of lanes 0..5 (the same instructions on the same values: no serial lane,
+  // no barrier, no LDS round trip), then lane c solves M x = e_c for the M^-1 column c
+  DSTAMP(4);
+  if (lane < 6) {
+    const int c = lane;
+    float L[6][6], Linv[6], z[6], x[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) {
       float sdiag = S.M[j][j];
@@ -411,25 +414,6 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
         for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
         L[i][j] = t * Linv[j];
       }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-#pragma unroll
-      for (int k = 0; k <= i; k++) S.L[i][k] = L[i][k];
-      S.L[i][6] = Linv[i];
-    }
-  }
-  __syncthreads();
-  DSTAMP(4);
-  // ---- M^-1 columns: lane c solves M x = e_c
-  if (lane < 6) {
-    const int c = lane;
-    float L[6][6], Linv[6], z[6], x[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-#pragma unroll
-      for (int k = 0; k <= i; k++) L[i][k] = S.L[i][k];
-      Linv[i] = S.L[i][6];
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) {
@@ -499,6 +483,7 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
   __syncthreads();
   DSTAMP(6);
   // ---- bias_a = cdof_a . sum_{k>=a} cfrc_k (suffix, from body 5 down); actuation
+  float tau = 0.f;
   if (lane < 6) {
     const int a = lane;
     float acc[6] = {0, 0, 0, 0, 0, 0};
@@ -515,14 +500,18 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
     const float c = fminf(fmaxf(sh.ctrl[a], m->act_clo[a]), m->act_chi[a]);
     float f = m->act_kp[a] * c - m->act_kp[a] * sh.qpos[a] - m->act_kv[a] * sh.qvel[a];
     f = fminf(fmaxf(f, m->act_flo[a]), m->act_fhi[a]);
-    S.tau[a] = f - bias + (m->ee ? sh.qacc_smooth[a] : 0.f);   // + J'D aref of the weld (weld_fold)
+    tau = f - bias + (m->ee ? sh.qacc_smooth[a] : 0.f);   // + J'D aref of the weld (weld_fold)
   }
-  __syncthreads();
+  // tau_j to every lane by DPP broadcasts, taken by the whole row before any lane branches (no barrier and
+  // no LDS round trip; minv was written before the last barrier)
+  float tj[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) tj[j] = bcast_row(tau, j);
   if (lane < 6) {
     const int i = lane;
     float sacc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 6; j++) sacc += sh.minv[i][j] * S.tau[j];
+    for (int j = 0; j < 6; j++) sacc += sh.minv[i][j] * tj[j];
     sh.qacc_smooth[i] = sacc;
   } else if (lane < 9) {
     // cube (free body): -bias / m = g, gyroscopic term on the rotational dofs
