@@ -363,8 +363,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 #pragma unroll
         for (int k = 0; k < SO100_NV; k++) {
           const float dkk = bcast_row(H[k], k);
-          const float Lkk = sqrtf(fmaxf(dkk, kMinVal));
-          const float inv = 1.f / Lkk;
+          const float inv = __builtin_amdgcn_rsqf(fmaxf(dkk, kMinVal));   // 1 / L_kk: one v_rsq (1 ulp)
           const float lik = H[k] * inv;
           if (lane >= k) H[k] = lik;
           if (lane == k) dinv = inv;
