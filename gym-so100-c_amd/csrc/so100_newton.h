@@ -139,6 +139,27 @@ DEV float4 contact_rows(const NewtonRows& rw, float x, int lane, int ncon_max) {
   }
   return r;
 }
+// contact_rows of two vectors in one pass: 8 independent row sums per contact instead of two chains of
+// 4 behind their own uniform branches (the same sums in the same order: bitwise contact_rows twice)
+DEV void contact_rows2(const NewtonRows& rw, float x, float y, int lane, int ncon_max, float4& rx, float4& ry) {
+  rx = make_float4(0.f, 0.f, 0.f, 0.f);
+  ry = rx;
+#pragma unroll
+  for (int c = 0; c < kJReg; c++) {
+    if (c < ncon_max) {
+      const float4 j = rw.J[c];
+      const float a0 = rowsum16(j.x * x), a1 = rowsum16(j.y * x), a2 = rowsum16(j.z * x), a3 = rowsum16(j.w * x);
+      const float b0 = rowsum16(j.x * y), b1 = rowsum16(j.y * y), b2 = rowsum16(j.z * y), b3 = rowsum16(j.w * y);
+      if (lane == c) { rx = make_float4(a0, a1, a2, a3); ry = make_float4(b0, b1, b2, b3); }
+    }
+  }
+  for (int c = kJReg; c < ncon_max; c++) {
+    const float4 j = jx_own(rw, c, lane);
+    const float a0 = rowsum16(j.x * x), a1 = rowsum16(j.y * x), a2 = rowsum16(j.z * x), a3 = rowsum16(j.w * x);
+    const float b0 = rowsum16(j.x * y), b1 = rowsum16(j.y * y), b2 = rowsum16(j.z * y), b3 = rowsum16(j.w * y);
+    if (lane == c) { rx = make_float4(a0, a1, a2, a3); ry = make_float4(b0, b1, b2, b3); }
+  }
+}
 
 // The split path's HBM record (so100_device.h NewtonHdr): the stage kernel stores a lane's rows, the
 // Newton kernel loads them back.  J is stored by the stage as it is computed (so100_step.hip).
@@ -275,25 +296,29 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 
   STAMP(0);
   // ---------------- start: the warmstart if its cost is below qacc_smooth's (mj_fwdConstraint)
-  float qacc, jc[4];
+  // The start's a - a_smooth, M(a - a_smooth), Gauss term and cost are the chosen candidate's, already
+  // evaluated for the choice (at qacc_smooth: exactly 0, 0, 0 and its row cost), not evaluated again.
+  float qacc, jc[4], ev, Me, gauss, cost;
   {
-    const float4 jw = contact_rows(r, warm, lane, ncon_max), js = contact_rows(r, qs, lane, ncon_max);
+    float4 jw, js;
+    contact_rows2(r, warm, qs, lane, ncon_max, jw, js);
     const float xw[4] = {jw.x - c_aref[0], jw.y - c_aref[1], jw.z - c_aref[2], jw.w - c_aref[3]};
     const float xs[4] = {js.x - c_aref[0], js.y - c_aref[1], js.z - c_aref[2], js.w - c_aref[3]};
     const float ew = warm - qs;
-    const float gw = 0.5f * rowsum16(dof ? ew * mul_m(mrow, mcd, ew) : 0.f);
+    const float mew = mul_m(mrow, mcd, ew);
+    const float gw = 0.5f * rowsum16(dof ? ew * mew : 0.f);
     const float cw = gw + rowsum16(rows_cost(warm - fr_aref, lim_s * warm - lim_aref, xw));
     const float cs = rowsum16(rows_cost(qs - fr_aref, lim_s * qs - lim_aref, xs));
     const bool use_w = cw < cs;
     qacc = use_w ? warm : qs;
 #pragma unroll
     for (int k = 0; k < 4; k++) jc[k] = use_w ? xw[k] : xs[k];
+    ev = use_w ? ew : 0.f;                                // a - a_smooth
+    Me = use_w ? mew : 0.f;
+    gauss = use_w ? gw : 0.f;
+    cost = use_w ? cw : cs;
   }
-  float ev = qacc - qs;                                   // a - a_smooth
-  float Me = mul_m(mrow, mcd, ev);
   float jfr = qacc - fr_aref, jlim = lim_s * qacc - lim_aref;
-  float gauss = 0.5f * rowsum16(dof ? ev * Me : 0.f);
-  float cost = gauss + rowsum16(rows_cost(jfr, jlim, jc));
   const float scale = m->pgs_scale, tolerance = m->tolerance;
   STAMP(1);
 
