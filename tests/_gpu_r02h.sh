@@ -1,6 +1,6 @@
 # GPU parity suite + bench line + fused/split per shard size on the current build (gpurun_out/r02h/*)
 export TMPDIR=/tmp
-O=gpurun_out/r02h
+O=gpurun_out/${TAG:-r02h}
 rm -rf $O; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
