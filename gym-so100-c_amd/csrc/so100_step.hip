@@ -2540,9 +2540,13 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
 // functions on the same values.  kDebug: the instantiation that also fills the debug buffer (launched when
 // the caller passes one); the other has no debug code, which costs registers in the substep loop.
-template <bool kDebug>
-__global__ void __launch_bounds__(kThreads, SO100_FUSED_WAVES) so100_fused_kernel(const DevModel* __restrict__ model,
-                                                                                  StageArgs kargs) {
+// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, 32 B/lane of spills) when
+// the grid exceeds 2 waves per SIMD; a grid of at most 2 waves per SIMD (8,192 envs on 256 CUs: all waves
+// resident at once) takes the 2-wave build (186 VGPRs, no scratch; +0.8 % there, -7 % at 16,384 envs).
+// Register allocation only: both give the same results bit for bit.
+template <bool kDebug, int kWaves = SO100_FUSED_WAVES>
+__global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const DevModel* __restrict__ model,
+                                                                       StageArgs kargs) {
   // the model as a noalias kernel argument: no store of the step can clobber it, so its uniform loads stay
   // scalar (s_load) after the substeps' global stores (through args.m they became vector loads)
   StageArgs args = kargs;
@@ -2799,6 +2803,19 @@ __global__ void __launch_bounds__(1024) so100_order_kernel(const uint32_t* __res
   for (int g = t; g < ng; g += 1024) order[atomicAdd(&hist[key(gcost[g])], 1)] = g;
 }
 
+// compute units of the current device (cached per device; 0 if the query fails: the 3-wave build then)
+static int device_cus() {
+  static int cus[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 0;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
+
 // fused (Newton only): the whole env step as one so100_fused_kernel launch; ev then takes 2 events.
 hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, Workspace& w, const so100_buffers& b,
                        int n, int task, int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s,
@@ -2819,6 +2836,7 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, W
       a.w.order = nullptr;
     }
     if (b.debug) hipLaunchKernelGGL(so100_fused_kernel<true>, grid, dim3(kThreads), 0, s, m, a);
+    else if (ng <= 2 * 4 * device_cus()) hipLaunchKernelGGL((so100_fused_kernel<false, 2>), grid, dim3(kThreads), 0, s, m, a);
     else hipLaunchKernelGGL(so100_fused_kernel<false>, grid, dim3(kThreads), 0, s, m, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
