@@ -2530,6 +2530,9 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 #ifndef SO100_PRIO
 #define SO100_PRIO 1
 #endif
+#ifndef SO100_W2_NOLAUNDER
+#define SO100_W2_NOLAUNDER 0
+#endif
 #ifndef SO100_FUSED_WAVES
 #define SO100_FUSED_WAVES 3
 #endif
@@ -2593,14 +2596,13 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
   const int nsub = args.m->nsubstep;
   const float h = args.m->timestep;
   for (int sub = 0; sub < nsub; sub++) {
-#if SO100_LAUNDER_IDS
     // the lane / env ids laundered per substep too: what derives from them (masks, addresses, per-lane
     // model values) is recomputed in each substep instead of hoisted and held live across the loop
     int lane = lane0, grp = grp0, env = env0, e = e0;
-    asm volatile("" : "+v"(lane), "+v"(grp), "+v"(env), "+v"(e));
+    if constexpr (SO100_LAUNDER_IDS && !(kWaves == 2 && SO100_W2_NOLAUNDER))
+      asm volatile("" : "+v"(lane), "+v"(grp), "+v"(env), "+v"(e));
     const bool valid = env < args.n;
     EnvShared& sh = shm[grp];
-#endif
     TL_MARK(-1);
     if (sub > 0) euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
     // the model pointer laundered per substep: the model loads (uniform, ~1 KB) must not be hoisted out of
