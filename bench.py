@@ -27,21 +27,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 
 METRIC = "env steps/sec (whole node), 65k parallel bin-a-cube envs at 1/2/4/8 MI355X"
-# algorithmic HBM bytes per env step at the boundary: reads action 24 + qpos 52 + qvel 48
-# + warmstart 48 + elapsed 4 + episode 4 = 180; writes qpos 52 + qvel 48 + warmstart 48 + obs 60 + reward 4
-# + terminated/truncated/success/diverged 4 + contact_bits 4 + elapsed 4 + episode 4 = 228.
-BYTES_PER_ENV_STEP = 408
-# dominant kernel = the solver (so100_newton.hip / so100_pgs.hip).  PGS algorithmic bytes per launch: per env the solver
-# record header (4 lanes x 40 floats = 640 B) read + qacc (48 B) written; per contact the solver block
-# (160 B) + J rows (192 B) read once.
-SOLVER_BYTES_PER_ENV = 640 + 48
-SOLVER_BYTES_PER_CONTACT = 160 + 192
-# Newton record (so100_device.h NewtonHdr): header 100 floats read + qacc write; per contact 12 floats of
-# block + 48 of J read
-NEWTON_BYTES_PER_ENV = 4 * 100 + 48
-NEWTON_BYTES_PER_CONTACT = 4 * (12 + 48)
-# fused kernel: the boundary bytes of the env step (state/action in, state/outputs out) + the contact count
-FUSED_BYTES_PER_ENV = BYTES_PER_ENV_STEP + 4
+# algorithmic HBM bytes per env step at the boundary.  Reads action 24 + qpos 52 + qvel 48
+# + warmstart 48 + step counter 4 = 176; writes qpos 52 + qvel 48 + warmstart 48 + obs 60 + reward 4
+# + terminated 1 + truncated 1 + step counter 4 = 218.  GoalEnv +24 (desired goal read, achieved goal
+# written), domain randomisation +32 (params read, RNG state).  roofline.achieved = env steps/s per GPU x
+# these bytes (never padded with intermediate traffic; the kernels' own record and PMC bytes are reported
+# beside it as separate fields).
+BYTES_PER_ENV_STEP = {"base": 394, "goal": 418, "dr": 426}
+# the split path's stage -> solver HBM record (not algorithmic: an intermediate of the split launches),
+# per Newton launch: per env the NewtonHdr (100 floats) read + qacc written, per contact 12 + 48 floats read
+NEWTON_RECORD_BYTES_PER_ENV = 4 * 100 + 48
+NEWTON_RECORD_BYTES_PER_CONTACT = 4 * (12 + 48)
+PGS_RECORD_BYTES_PER_ENV = 640 + 48
+PGS_RECORD_BYTES_PER_CONTACT = 160 + 192
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 CLOCK_HZ = 2.4e9             # MI355X peak engine clock (valu_busy uses it: a lower real clock only raises the share)
 SIMDS = 1024                 # 256 CUs x 4 SIMDs
@@ -74,17 +72,30 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds, solver="newton"):
-    """Time the oracle (fp64 C restatement, OpenMP over envs) on this host's cores — a reported,
-    non-target baseline (the reference's MuJoCo is not installed here)."""
-    import ctypes
+    """Time the oracle (the fp64 clarity-first C restatement: dense 12x12 matrices, OpenMP over envs, one
+    env per thread) on this host's cores: a reported, non-target baseline.  The reference's MuJoCo is not
+    installed here, so it cannot be timed.  Threads: every CPU in this process's affinity set, capped by
+    OMP_NUM_THREADS where the pool sets it (the GPU box's CPU share: 16 of its CPUs per GPU)."""
     import numpy as np
     sys.path.insert(0, ROOT)
     from oracle.oracle import Oracle
     from gym_so100.model import build_model
     o = Oracle(64)
     m = build_model(solver=solver)
-    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    allowed = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS") or allowed)
+    cores = max(1, min(allowed, cap))
     nenv = 4 * cores
     datas = (o.Data * nenv)()
     for i in range(nenv):
@@ -98,26 +109,24 @@ def cpu_baseline(seconds, solver="newton"):
         done += o.batch_run(m, datas, nenv, steps_per_call, 0, acts, nthreads=cores)
         t_used += time.perf_counter() - t0
     return {"value": done / t_used, "unit": "env_steps/s", "cores": cores, "kind": "port",
-            "sample": f"{nenv} CubeToBin envs x {done // nenv} steps (fp64 oracle, {solver} solver, OpenMP "
-                      f"{cores} threads, {t_used:.1f}s)"}
+            "cpus_allowed": allowed, "cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+            "sample": f"{nenv} CubeToBin envs x {done // nenv} steps ({solver} solver, OpenMP {cores} threads, "
+                      f"{t_used:.1f}s)",
+            "note": "the repo's fp64 oracle (oracle/so100_oracle.c: a clarity-first restatement with dense 12x12 "
+                    "matrices), not MuJoCo; a non-target baseline"}
 
 
-def load_traffic(n_envs, solver="pgs", fused=False):
-    """(HBM bytes per solver launch of n_envs envs, VALU wave-instructions per env step) from the
-    committed rocprofv3 PMC passes (profiles/pmc_traffic[_newton].json, tests/_pmc_traffic.py), or
-    (None, None)."""
-    name = "pmc_traffic_fused.json" if fused else ("pmc_traffic.json" if solver == "pgs" else f"pmc_traffic_{solver}.json")
-    path = os.path.join(ROOT, "profiles", name)
+def load_step_traffic(n_envs, mode, solver):
+    """The committed rocprofv3 PMC measurement of one env step's HBM traffic at this size and step mode
+    (profiles/r03_pmc_step_*.json, tools/gpurun/pmc_step_traffic.py: FETCH_SIZE and WRITE_SIZE passes, summed
+    over every kernel of a step), or None."""
+    path = os.path.join(ROOT, "profiles", f"r03_pmc_step_{mode}_{solver}_{n_envs}.json")
     if not os.path.exists(path):
-        return None, None
+        return None
     try:
-        d = json.load(open(path))
-        if int(d.get("n_envs", -1)) != n_envs:
-            return None, None
-        v = d.get("valu_insts_per_step")
-        return float(d["hbm_bytes_per_launch"]), (float(v) if v else None)
-    except Exception:
-        return None, None
+        return json.load(open(path))
+    except ValueError:
+        return None
 
 
 def main(argv=None):
@@ -132,7 +141,9 @@ def main(argv=None):
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        # host-side barrier and MAX over ranks only: the env shards exchange nothing, so RCCL is never
+        # initialised (north_star: no RCCL on the data path)
+        dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -180,16 +191,20 @@ def main(argv=None):
         s_ms, s_n, t_ms, t_n = env.profile_read()
         env.profile_enable(0)
         solver_ms, stage_ms = s_ms / max(s_n, 1), t_ms / max(t_n, 1)
-    # untimed: contacts per env per solver launch (for the solver's algorithmic bytes)
+    # untimed: contacts per env per solver launch (the split record bytes) and contacts the 16-per-env cap
+    # dropped (MuJoCo has no cap)
     accum = torch.zeros(1, dtype=torch.int64, device=dev)
+    dropped = torch.zeros(1, dtype=torch.int64, device=dev)
     for i in range(args.contact_steps):
         env.set_action_buffer(pool[i % len(pool)])
         env.step_async_raw()
         env.contact_count(accum)
+        dropped += env.ncon_dropped.sum()
     torch.cuda.synchronize(dev)
     contacts_per_env = float(accum.item()) / max(1, args.contact_steps * count)
+    dropped_per_env_step = float(dropped.item()) / max(1, args.contact_steps * count)
     if world > 1:
-        t = torch.tensor([elapsed, step_ms, solver_ms, stage_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, step_ms, solver_ms, stage_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_ms, solver_ms, stage_ms = (float(x) for x in t)
 
@@ -199,19 +214,25 @@ def main(argv=None):
     if rank == 0:
         env_steps = total * args.steps
         value = env_steps / elapsed
-        # the timed launches are chunk 0's (n0 envs), concurrent with the other chunks' (so100_chunk_info);
-        # fused: the one launch over all envs
         fused = env.fused
         nchunks, n0 = env.chunk_info()
+        mode = "fused" if fused else "split"
+        kind = "goal" if args.task == "so100_goal" else "base"
+        bpe = BYTES_PER_ENV_STEP[kind]
+        # achieved = env steps/s per GPU x algorithmic bytes per env step.  Per GPU from this
+        # rank's device time per step (HIP events on the launch stream around the timed steps: the fused
+        # launch, or a split step's 21 launches per chunk with the chunks joined back to this stream)
+        per_gpu_rate = count / (step_ms * 1e-3)
+        achieved = per_gpu_rate * bpe
+        pmc = load_step_traffic(count, mode, args.solver)
+        traffic = pmc["hbm_bytes_per_step"] / count if pmc else None      # per env step, like achieved
         if fused:
-            solver_bytes = n0 * FUSED_BYTES_PER_ENV
+            rec_per_launch = None
         else:
-            per_env, per_con = ((SOLVER_BYTES_PER_ENV, SOLVER_BYTES_PER_CONTACT) if args.solver == "pgs" else
-                                (NEWTON_BYTES_PER_ENV, NEWTON_BYTES_PER_CONTACT))
-            solver_bytes = n0 * (per_env + per_con * contacts_per_env)
-        achieved = solver_bytes / (solver_ms * 1e-3)
-        traffic, valu_insts = load_traffic(n0, args.solver, fused)
-        # VALU issue share of the timed run: insts x 2 cyc (wave64 on SIMD-32) / (step x 2.4 GHz x 1024 SIMDs)
+            per_env, per_con = ((PGS_RECORD_BYTES_PER_ENV, PGS_RECORD_BYTES_PER_CONTACT) if args.solver == "pgs" else
+                                (NEWTON_RECORD_BYTES_PER_ENV, NEWTON_RECORD_BYTES_PER_CONTACT))
+            rec_per_launch = n0 * (per_env + per_con * contacts_per_env)
+        valu_insts = pmc.get("valu_insts_per_step") if pmc else None
         valu_busy = valu_insts * 2.0 / (step_ms * 1e-3 * CLOCK_HZ * SIMDS) if valu_insts else None
         line = {
             "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
@@ -222,28 +243,32 @@ def main(argv=None):
                                     "auto-reset"),
                        "envs_total": total, "envs_per_gpu": count, "task": args.task, "substeps": 10,
                        "solver": args.solver, "solver_iterations": env.model.iterations,
-                       "step_mode": "fused" if fused else "split",
-                       "parallelism": f"env-sharded x{world}, no collectives",
+                       "step_mode": mode, "fused_build": env.fused_build if fused else None,
+                       "parallelism": f"env-sharded x{world}, no collectives (gloo barrier + MAX for timing)",
                        "actions": "U[-1,1]^6 pool resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": traffic, "valu_busy": valu_busy,
-                         "kernel": "so100_fused_kernel" if fused else f"so100_{args.solver}_kernel", "kernel_ms": solver_ms,
-                         "bytes_per_launch": solver_bytes, "envs_per_launch": n0, "concurrent_chunks": nchunks,
+                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "bytes_per_env_step": bpe, "env_steps_per_s_per_gpu": per_gpu_rate,
+                         "step_device_ms": step_ms,
+                         "kernel": "so100_fused_kernel (one launch per env step)" if fused else
+                                   f"split step: stage + so100_{args.solver}_kernel x 10 + final stage, {nchunks} chunks",
+                         "traffic_over_algorithmic": (traffic / bpe) if traffic else None,
+                         "pmc_source": pmc.get("file") if pmc else None,
+                         "valu_busy": valu_busy,
+                         "solver_kernel_ms": None if fused else solver_ms,
+                         "stage_kernel_ms": None if fused else stage_ms,
+                         "fused_kernel_ms": solver_ms if fused else None,
+                         "split_record_bytes_per_solver_launch": rec_per_launch, "envs_per_launch": n0,
                          "contacts_per_env": contacts_per_env,
-                         "stage_kernel_ms": stage_ms, "step_device_ms": step_ms,
-                         "boundary_bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "note": (("fused step kernel: the whole env step per wave (10 x (kinematics, CRBA/RNE, "
-                                   "collision, constraint rows, primal Newton) + epilogue), state in registers, the "
-                                   "Newton rows handed over in registers, so its algorithmic HBM bytes are the "
-                                   "boundary's 412 B per env step; "
-                                   if fused else
-                                   f"solver = primal Newton ({args.solver}): per env a 12x12 Hessian, its Cholesky "
-                                   "factor and an exact line search on 16 lanes, 2-3 Newton steps per substep; "
-                                   if args.solver == "newton" else
-                                   "solver = serial Gauss-Seidel chains per env, 100 sweeps; ") +
-                                  "issue/latency-bound, not HBM-bound (DESIGN.md §3.5); traffic = measured PMC bytes per "
-                                  "launch of that kernel; valu_busy = PMC SQ_INSTS_VALU per step x 2 cyc / (step time x 2.4 GHz x "
-                                  "1024 SIMDs): VALU issue share beside the HBM share (SURVEY §8d)")},
+                         "contacts_dropped_per_env_step": dropped_per_env_step,
+                         "note": ("achieved = env steps/s per GPU x SURVEY §8(d)'s algorithmic bytes per env step "
+                                  "(state/action in, state/outputs out; GoalEnv 418, DR 426): nothing else is "
+                                  "algorithmic. traffic = measured HBM bytes per env step from rocprofv3 "
+                                  "FETCH_SIZE + WRITE_SIZE over every kernel of a step (raw counters, the 16-B/lane x2 "
+                                  "correction not applied), so traffic_over_algorithmic shows re-read and spill "
+                                  "waste. The path is per-env dependent arithmetic (issue/latency-bound, DESIGN.md "
+                                  "§3.5); valu_busy = PMC SQ_INSTS_VALU per step x 2 cyc / (step time x 2.4 GHz x "
+                                  "1024 SIMDs)")},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

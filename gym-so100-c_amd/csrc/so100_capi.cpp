@@ -18,8 +18,9 @@
 #include "so100_device.h"
 
 namespace so100 {
-hipError_t launch_step(const DevModel*, int, int, int, Workspace&, const so100_buffers&, int, int, int, int, uint64_t,
-                       int, hipStream_t, hipEvent_t*);
+hipError_t launch_step(const DevModel*, int, int, int, int, Workspace&, const so100_buffers&, int, int, int, int,
+                       uint64_t, int, hipStream_t, hipEvent_t*);
+int fused_build(int n, int waves, bool debug);
 hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
 hipError_t launch_render(const DevModel*, const float4*, const int*, const uint32_t*, int, const float*,
                          const uint8_t*, const so100_camera&, int, int, int, uint8_t*, hipStream_t);
@@ -90,6 +91,7 @@ struct so100_env {
   std::vector<StepGraph> graphs;
   uint64_t graph_clock = 0;
   float4* d_cand = nullptr;     // the hulls' support-cell candidates (DevModel::hull_cand)
+  int fused_waves = 0;          // the fused product build: 2 | 3 waves per SIMD, 0 auto (so100_set_fused_build)
 };
 
 // An instantiated step graph can still be running when it is evicted: wait for its last replay first.
@@ -196,6 +198,7 @@ static so100_buffers offset_buffers(const so100_buffers& b, int s) {
   o.debug = off(b.debug, SO100_DBG_STRIDE);
   o.mocap = off(b.mocap, 7);
   o.reward64 = off(b.reward64, 1);
+  o.ncon_dropped = off(b.ncon_dropped, 1);
   return o;
 }
 
@@ -645,6 +648,10 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   if (const char* v = getenv("SO100_GRAPH")) env->use_graph = atoi(v) != 0;
   if (const char* v = getenv("SO100_FUSED")) env->fused = atoi(v) < 0 ? -1 : atoi(v) != 0;   // A/B: 0 split, 1 fused
   if (const char* v = getenv("SO100_FUSED_MAX")) env->fused_max = atoi(v);
+  if (const char* v = getenv("SO100_FUSED_WAVES")) {
+    const int w = atoi(v);
+    env->fused_waves = (w == 2 || w == 3) ? w : 0;
+  }
   e = make_chunks(env, default_chunks(n_envs));
   if (e == hipSuccess && env->solver == SO100_SOLVER_NEWTON) {
     // the fused launches: the record header (only its contact counts are written) and the wave order
@@ -716,12 +723,12 @@ static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags
   env->last_fused = step_is_fused(env);
   if (env->last_fused) {
     // one launch over all n envs (every wave runs its whole env step: no chunks needed to fill the gaps)
-    return so100::launch_step(env->d_model, env->nsubstep, env->solver, 1, env->fws, *b, env->n, env->task, flags,
+    return so100::launch_step(env->d_model, env->nsubstep, env->solver, 1, env->fused_waves, env->fws, *b, env->n, env->task, flags,
                               env->max_steps, env->base_seed, env->env_offset, s, ev);
   }
   if (env->chunks.size() == 1) {
     Chunk& c = env->chunks[0];
-    return so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, c.ws, *b, c.count, env->task, flags, env->max_steps,
+    return so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, 0, c.ws, *b, c.count, env->task, flags, env->max_steps,
                               env->base_seed, env->env_offset, s, ev);
   }
   hipError_t e = hipEventRecord(env->fork, s);
@@ -729,13 +736,13 @@ static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags
     Chunk& c = env->chunks[k];
     e = hipStreamWaitEvent(c.s, env->fork, 0);
     if (e == hipSuccess)
-      e = so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
+      e = so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, 0, c.ws, offset_buffers(*b, c.start), c.count, env->task, flags,
                              env->max_steps, env->base_seed, env->env_offset + c.start, c.s, nullptr);
     if (e == hipSuccess) e = hipEventRecord(c.done, c.s);
   }
   Chunk& c0 = env->chunks[0];
   if (e == hipSuccess)
-    e = so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
+    e = so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, 0, c0.ws, *b, c0.count, env->task, flags, env->max_steps,
                            env->base_seed, env->env_offset, s, ev);
   for (size_t k = 1; k < env->chunks.size() && e == hipSuccess; k++) e = hipStreamWaitEvent(s, env->chunks[k].done, 0);
   return e;
@@ -873,6 +880,22 @@ int so100_set_step_mode(so100_env* env, int fused) {
 int so100_step_mode(const so100_env* env) {
   if (!env) return fail("so100_step_mode: env is NULL");
   return step_is_fused(env) ? 1 : 0;
+}
+
+int so100_set_fused_build(so100_env* env, int waves) {
+  if (!env) return fail("so100_set_fused_build: env is NULL");
+  if (waves != 0 && waves != 2 && waves != 3) return fail("so100_set_fused_build: waves must be 0 (auto), 2 or 3");
+  if (env->prof_cap > 0) return fail("so100_set_fused_build: disable profiling first");
+  DeviceGuard g(env->device);
+  graph_free(env);                     // captured graphs hold the other build's launch
+  env->fused_waves = waves;
+  return 0;
+}
+
+int so100_fused_build(const so100_env* env, int debug) {
+  if (!env) return fail("so100_fused_build: env is NULL");
+  DeviceGuard g(env->device);
+  return so100::fused_build(env->n, env->fused_waves, debug != 0);
 }
 
 int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs) {

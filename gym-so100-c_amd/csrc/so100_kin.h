@@ -56,6 +56,7 @@ struct __attribute__((aligned(16))) EnvShared {
   float site_cube[4];
   float site_ee[4];
   int ncon;
+  int ndrop;                     // contacts the kMaxCon cap left out, summed over the fused step's substeps
   int con_pair[kMaxCon];
   float con_dist[kMaxCon];
   float mocap[7];                // EE variant: mocap pose (pos, quat wxyz)
@@ -67,10 +68,11 @@ struct __attribute__((aligned(16))) EnvShared {
     SerialScratch ser;           // dynamics scratch (dead before collision) + link frames (live through it)
   };
 };
-// 3,168 B per env: 4 envs = 12,672 B per wave, under the 12,800 B that lets 12 workgroups share a CU's LDS
+// 3,184 B per env: 4 envs = 12,736 B per wave, under the 12,800 B that lets 12 workgroups share a CU's LDS
 // (allocated in 1,280-B steps: 12,928 B held the stage and fused kernels to 11 waves per CU, measured), and
-// a stride of 12.375 x 256 B, so the 4 envs of a wave hit different LDS bank windows for the same field.
-static_assert(sizeof(EnvShared) == 3168, "EnvShared: 4 per workgroup must stay within 12,800 B");
+// a stride of 796 dwords (28 banks mod 64), so the 4 envs of a wave hit different LDS bank windows for the
+// same field.
+static_assert(sizeof(EnvShared) == 3184, "EnvShared: 4 per workgroup must stay within 12,800 B");
 
 // ------------------------------------------------------------------ small math (same formulas as oracle)
 DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }

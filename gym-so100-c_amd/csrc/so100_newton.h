@@ -232,9 +232,10 @@ DEV void newton_rows_load(const Workspace& w, int e, int lane, bool valid, float
 }
 
 // Diagnostics of a solve (debug buffer rows): the final frictionloss force of the lane's dof, contact
-// `lane`'s normal force, the iteration count, the last cost improvement, and the phase stamps.
+// `lane`'s force (normal, then its friction rows), the iteration count, the last cost improvement, and the
+// phase stamps.
 struct NewtonDiag {
-  float f_fr, f_n, impr;
+  float f_fr, f_n, f_t[3], impr;
   int iters;
 #ifdef SO100_STAMPS
   unsigned long long st[8];
@@ -249,7 +250,11 @@ DEV void newton_diag_write(float* dbg, int lane, bool valid, float qacc, const N
   }
 #endif
   if (lane < SO100_NV) { dbg[4 + lane] = qacc; dbg[76 + lane] = d.f_fr; }
-  if (lane < kMaxCon) dbg[32 + lane] = d.f_n;
+  if (lane < kMaxCon) {
+    dbg[32 + lane] = d.f_n;
+#pragma unroll
+    for (int k = 0; k < 3; k++) dbg[96 + 3 * lane + k] = d.f_t[k];
+  }
   if (lane == 0) { dbg[1] = (float)d.iters; dbg[2] = d.impr; }
 }
 
@@ -504,6 +509,8 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     cone_eval(jc, c_D, c_mu, c_fr0, c_fr1, cc, fc, hc);
     diag.f_fr = f_fr;
     diag.f_n = own ? fc[0] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) diag.f_t[k] = own ? fc[1 + k] : 0.f;
     diag.iters = iters;
     diag.impr = last_impr;
   }

@@ -332,9 +332,12 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
         dbg[1] = (float)iters;
         dbg[2] = last_impr;
         for (int c = 0; c < kMaxCon; c++) {
-          float f0 = 0.f;
-          if (c < ncon) f0 = c < kResident ? blk[c][ew][kBlkF].x : crec[c * kConRec + 4 * kBlkF];
-          dbg[32 + c] = f0;
+          float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (c < ncon) f = c < kResident ? blk[c][ew][kBlkF] : reinterpret_cast<const float4*>(crec + c * kConRec)[kBlkF];
+          dbg[32 + c] = f.x;
+          dbg[96 + 3 * c] = f.y;
+          dbg[97 + 3 * c] = f.z;
+          dbg[98 + 3 * c] = f.w;
         }
       }
     }

@@ -1436,7 +1436,8 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
 //    candidates runs ceil(sum c_e / 4) rounds: the envs' own rows share a heavy env's pairs (this was one
 //    pair of the wave's union per round, on the rows holding it: 60 % of the slowest waves' assembly);
 //  * each round's hits go to their env's staging slots in list order, so each env keeps its pair order.
-// Returns the env's number of staged contacts (uniform across its row, capped at kMaxCon).
+// Returns the env's number of MPR contacts (uniform across its row; those beyond kMaxCon are not staged and
+// count as dropped).
 template <bool kCells>
 DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, int grp, bool valid) {
 #ifdef SO100_EXPERIMENT_NO_MPR
@@ -1535,8 +1536,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
       }
     }
   }
-  const int ns = grp == 0 ? f0 : grp == 1 ? f1 : grp == 2 ? f2 : f3;
-  return ns < kMaxCon ? ns : kMaxCon;
+  return grp == 0 ? f0 : grp == 1 ? f1 : grp == 2 ? f2 : f3;
 }
 
 DEV void make_frame(float* f) {
@@ -2015,7 +2015,15 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       tot += nmpr;
       __syncthreads();
       tot = pad_contacts(m, sh, lane, grp, valid, tot);
-      if (lane == 0) sh.ncon = tot < kMaxCon ? tot : kMaxCon;
+      const int drop = tot > kMaxCon ? tot - kMaxCon : 0;   // the oracle's ncon_dropped
+      if (lane == 0) {
+        sh.ncon = tot < kMaxCon ? tot : kMaxCon;
+        if constexpr (kFused) sh.ndrop = (sub == 0 ? 0 : sh.ndrop) + drop;   // stored by the fused epilogue
+      }
+      if constexpr (!kFused) {
+        if (valid && lane == 0 && B.ncon_dropped)
+          B.ncon_dropped[env] = (sub == 0 ? 0u : B.ncon_dropped[env]) + (uint32_t)drop;
+      }
     }
     __syncthreads();
     const int ncon = valid ? sh.ncon : 0;
@@ -2642,6 +2650,7 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     EnvShared& sh = shm[grp];
     euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
     final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+    if (valid && lane == 0 && args.b.ncon_dropped) args.b.ncon_dropped[env] = (uint32_t)sh.ndrop;
   }
   TL_MARK(2);
   if (args.w.gcost && tid == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
@@ -2818,10 +2827,21 @@ static int device_cus() {
   return cus[dev];
 }
 
+// The fused kernel build a launch of n envs takes: 1 = the debug build (a debug buffer is passed), else the
+// product build for `waves` waves per SIMD (2 | 3; 0 = auto: 2 when the grid fits the chip at 2 waves per
+// SIMD, i.e. at most 8 workgroups per CU, else 3).
+int fused_build(int n, int waves, bool debug) {
+  if (debug) return 1;
+  if (waves == 2 || waves == 3) return waves;
+  const int ng = (n + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  return ng <= 2 * 4 * device_cus() ? 2 : 3;
+}
+
 // fused (Newton only): the whole env step as one so100_fused_kernel launch; ev then takes 2 events.
-hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, Workspace& w, const so100_buffers& b,
-                       int n, int task, int flags, int max_steps, uint64_t base_seed, int env_offset, hipStream_t s,
-                       hipEvent_t* ev) {
+// waves: the fused product build (fused_build).
+hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, int waves, Workspace& w,
+                       const so100_buffers& b, int n, int task, int flags, int max_steps, uint64_t base_seed,
+                       int env_offset, hipStream_t s, hipEvent_t* ev) {
   StageArgs a{m, b, w, n, task, flags, max_steps, base_seed, env_offset, 0, 0};
   const dim3 grid((n + kEnvsPerBlock - 1) / kEnvsPerBlock);
   int k = 0;
@@ -2837,9 +2857,10 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, W
     } else {
       a.w.order = nullptr;
     }
-    if (b.debug) hipLaunchKernelGGL(so100_fused_kernel<true>, grid, dim3(kThreads), 0, s, m, a);
-    else if (ng <= 2 * 4 * device_cus()) hipLaunchKernelGGL((so100_fused_kernel<false, 2>), grid, dim3(kThreads), 0, s, m, a);
-    else hipLaunchKernelGGL(so100_fused_kernel<false>, grid, dim3(kThreads), 0, s, m, a);
+    const int build = fused_build(n, waves, b.debug != nullptr);
+    if (build == 1) hipLaunchKernelGGL(so100_fused_kernel<true>, grid, dim3(kThreads), 0, s, m, a);
+    else if (build == 2) hipLaunchKernelGGL((so100_fused_kernel<false, 2>), grid, dim3(kThreads), 0, s, m, a);
+    else hipLaunchKernelGGL((so100_fused_kernel<false, 3>), grid, dim3(kThreads), 0, s, m, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[k++], s);

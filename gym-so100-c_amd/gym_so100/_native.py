@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("SO100_LIB") or os.path.join(HERE, "_lib", "libso100_h
 
 SO100_FLAG_AUTORESET = 1
 SO100_FLAG_DR = 2
-SO100_DBG_STRIDE = 96
+SO100_DBG_STRIDE = 160
 TASKS = {"so100_cube_to_bin": 0, "so100_touch_cube": 1, "so100_touch_cube_sparse": 2, "so100_goal": 3}
 
 _P = ctypes.c_void_p
@@ -22,7 +22,7 @@ class SO100Buffers(ctypes.Structure):
     _fields_ = [(n, _P) for n in (
         "qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "action",
         "obs", "reward", "terminated", "truncated", "success", "final_obs", "diverged", "contact_bits",
-        "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64")]
+        "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64", "ncon_dropped")]
 
 
 SO100_MAX_LIGHTS = 4
@@ -44,7 +44,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 10         # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 11         # include/so100.h SO100_ABI_VERSION
 HULL_CELLG = 8           # SO100_HULL_CELLG
 HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 
@@ -81,10 +81,13 @@ def load():
     lib.so100_render_mesh.argtypes = [_P, _P, _P, _P, ctypes.c_int]
     lib.so100_render.argtypes = [_P, _P, _P, ctypes.POINTER(SO100Camera), ctypes.c_int, ctypes.c_int, _P, _P]
     lib.so100_hull_cells.argtypes = [_P, _P, _P, ctypes.c_int]
+    lib.so100_set_fused_build.argtypes = [_P, ctypes.c_int]
+    lib.so100_fused_build.argtypes = [_P, ctypes.c_int]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
                "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info",
-               "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells"):
+               "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells",
+               "so100_set_fused_build", "so100_fused_build"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
     lib.so100_struct_sizes.restype = ctypes.c_int
@@ -104,7 +107,8 @@ EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
                     "so100_contact_count", "so100_chunk_info", "so100_render_mesh", "so100_render",
-                    "so100_set_step_mode", "so100_step_mode", "so100_hull_cells")
+                    "so100_set_step_mode", "so100_step_mode", "so100_hull_cells", "so100_set_fused_build",
+                    "so100_fused_build")
 
 
 def check(rc, what):

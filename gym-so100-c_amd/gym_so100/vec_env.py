@@ -83,15 +83,19 @@ class SO100VecEnv:
             MuJoCo's default).
         solver: "newton" (default: MuJoCo's default solver, which the reference's model runs; the
             unique minimiser of the constraint problem) or "pgs" (north_star's projected Gauss-Seidel).
-        debug: allocate the [N, 96] diagnostics buffer (contacts, forces, solver iterations).
+        debug: allocate the [N, 160] diagnostics buffer (contacts, forces, solver iterations; layout:
+            include/so100.h SO100_DBG_STRIDE).  While it is passed (``debug_enabled``, default True) the
+            fused step launches its debug build; set ``debug_enabled = False`` to run the product build.
         reward64: also keep the reward in float64 (``self.reward64``), as the reference returns it; the
             float32 ``reward`` rounds the dense TouchCube shaping (the other ladders are exact in float32).
+        nsubstep: physics substeps per env step (default: the reference's 10, control_timestep / timestep);
+            1 makes an env step one mj_step + the final mj_step1 (the parity tests' per-substep checks).
     """
 
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
                  iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480,
-                 variant="joint", reward64=False):
+                 variant="joint", reward64=False, nsubstep=None):
         torch = _torch()
         if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
             raise NotImplementedError(f"obs_type={obs_type!r}: 'so100_state' or 'so100_pixels_agent_pos'")
@@ -110,7 +114,7 @@ class SO100VecEnv:
         self.env_offset = int(env_offset)
         self.solver = solver
         self.variant = variant
-        self.model = build_model(iterations=iterations, solver=solver, variant=variant)
+        self.model = build_model(iterations=iterations, solver=solver, variant=variant, nsubstep=nsubstep)
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._handle = self.lib.so100_create(ctypes.byref(self.model), self.num_envs, dev_index)
         if not self._handle:
@@ -133,6 +137,8 @@ class SO100VecEnv:
         self.diverged = torch.zeros(n, dtype=torch.bool, device=d)
         self.final_obs = torch.zeros(n, NOBS, dtype=f32, device=d)
         self.contact_bits = torch.zeros(n, dtype=i32, device=d)
+        # contacts the 16-per-env cap left out in the last step (MuJoCo has no cap: 0 is the bar)
+        self.ncon_dropped = torch.zeros(n, dtype=i32, device=d)
         self.is_goal = task == "so100_goal"
         self.achieved_goal = torch.zeros(n, 3, dtype=f32, device=d) if self.is_goal else None
         self.desired_goal = torch.zeros(n, 3, dtype=f32, device=d) if self.is_goal else None
@@ -164,9 +170,11 @@ class SO100VecEnv:
         b = self._buf
         for name in ("qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "obs", "reward", "terminated",
                      "truncated", "success", "final_obs", "diverged", "contact_bits", "achieved_goal",
-                     "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64"):
+                     "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64", "ncon_dropped"):
             setattr(b, name, P(getattr(self, name)))
-        b.action = P(self.actions)
+        if not getattr(self, "_debug_enabled", True):
+            b.debug = None
+        b.action = P(self.actions) if getattr(self, "_action_ref", None) is None else P(self._action_ref)
 
     def set_mocap(self, pos, quat=None, mask=None):
         """EE variant: the mocap target pose of every env (pos [N,3], quat [N,4] wxyz; the data.mocap_pos /
@@ -262,7 +270,8 @@ class SO100VecEnv:
             done = self.terminated | self.truncated
         else:
             done = self._step_pixels()
-        info = {"is_success": self.success, "diverged": self.diverged, "contact_bits": self.contact_bits}
+        info = {"is_success": self.success, "diverged": self.diverged, "contact_bits": self.contact_bits,
+                "ncon_dropped": self.ncon_dropped}
         if self.autoreset:
             info["final_observation"] = self.final_obs if self.renderer is None else \
                 {"pixels": self.final_pixels, "agent_pos": self.final_obs[:, 9:15]}
@@ -393,6 +402,27 @@ class SO100VecEnv:
     def fused(self, on):
         mode = -1 if on is None else (1 if on else 0)
         _native.check(self.lib.so100_set_step_mode(self._handle, mode), "so100_set_step_mode")
+
+    @property
+    def debug_enabled(self):
+        """Whether steps write the debug buffer (and so launch the fused kernel's debug build)."""
+        return self.debug is not None and getattr(self, "_debug_enabled", True)
+
+    @debug_enabled.setter
+    def debug_enabled(self, on):
+        self._debug_enabled = bool(on)
+        self._fill_buffers()
+
+    @property
+    def fused_build(self):
+        """The fused kernel build the next fused step launches: 1 = debug build, 2 / 3 = the product build for
+        2 / 3 waves per SIMD.  Set 2, 3 or 0 (auto, the default) to choose the product build
+        (include/so100.h so100_set_fused_build); every build gives the same results bit for bit."""
+        return int(self.lib.so100_fused_build(self._handle, 1 if self.debug_enabled else 0))
+
+    @fused_build.setter
+    def fused_build(self, waves):
+        _native.check(self.lib.so100_set_fused_build(self._handle, int(waves or 0)), "so100_set_fused_build")
 
     def chunk_info(self):
         """(chunks, envs of chunk 0): the env split of a step; profile_read times chunk 0's launches."""

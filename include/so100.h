@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 10  /* 10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 11  /* 11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -71,9 +71,19 @@ typedef struct so100_buffers {
    * holds its float32 rounding, exact for the CubeToBin / sparse / GoalEnv ladders, rounded for the dense
    * TouchCube shaping); NULL = not written */
   double*   reward64;
+  /* [N] contacts the 16-per-env cap (SO100_MAXCON) left out, summed over the step's substeps: the counterpart
+   * of the oracle's ncon_dropped (MuJoCo has no such cap; 0 is the bar).  NULL = not written */
+  uint32_t* ncon_dropped;
 } so100_buffers;
 
-#define SO100_DBG_STRIDE 96  /* ncon, solver_iter, improvement, nefc, qacc[12], contact(dist,fn)[16], ... */
+/* Debug record per env (floats), written by the last substep of a step when `debug` is not NULL:
+ *   [0] ncon  [1] solver iterations  [2] last improvement  [3] nefc  [4..15] qacc (the last solve)
+ *   [16..31] contact dist  [32..47] contact normal force (efc_force row 0 of contact c)
+ *   [48..63] contact pair id (-1 unused)  [64..75] qacc_smooth  [76..87] dof frictionloss forces
+ *   [88..95] profiling stamps (diagnostic builds)
+ *   [96..143] contact c's friction forces (efc_force rows 1..3 of contact c) at 96 + 3 c
+ *   [144..159] reserved */
+#define SO100_DBG_STRIDE 160
 
 typedef struct so100_env so100_env;   /* opaque: device model copy + launch config */
 
@@ -122,6 +132,15 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
  * (stage: 0) and so100_chunk_info reports 1 chunk of N envs. */
 int so100_set_step_mode(so100_env* env, int fused);
 int so100_step_mode(const so100_env* env);
+
+/* Register budget of the fused kernel's product build (the build launched when `debug` is NULL): 2 = 2 waves
+ * per SIMD (186 VGPRs, no scratch), 3 = 3 waves per SIMD (168 VGPRs), 0 = auto (default: the 2-wave build
+ * when the grid fits the chip at 2 waves per SIMD, <= 8 x CUs workgroups; the 3-wave build above).  The
+ * SO100_FUSED_WAVES environment variable sets the initial value.  Register allocation only: every build
+ * gives the same results bit for bit (tests/test_gpu_parity.py test_product_builds_bitwise).
+ * so100_fused_build returns the build the next fused step of the env launches (1 = the debug build). */
+int so100_set_fused_build(so100_env* env, int waves);
+int so100_fused_build(const so100_env* env, int debug);
 
 /* Support-direction cells of the convex hulls (host only; no device needed).  The MPR collider's hull
  * support (the first vertex maximising n . v, MuJoCo's mesh support by exhaustive scan) reads a candidate

@@ -53,6 +53,8 @@ def _make_types(real):
             ("mocap_pos", _arr(real, 3)), ("mocap_quat", _arr(real, 4)),
             ("weld_pos", _arr(real, 6)), ("weld_J", _arr(real, 6, NV)), ("weld_D", _arr(real, 6)),
             ("weld_aref", _arr(real, 6)), ("weld_f", _arr(real, NV)),
+            ("snap_ncon", i), ("snap_ndrop", i), ("snap_pair", _arr(i, MAXCON)),
+            ("snap_force", _arr(real, MAXCON, 4)), ("snap_frf", _arr(real, NV)), ("snap_qacc", _arr(real, NV)),
         ]
     return Contact, Data
 
@@ -149,6 +151,13 @@ class Oracle:
         assert a.shape == (steps, nenv, 6)
         return self.lib.so100o_batch_run(self._p(model), ctypes.c_void_p(ctypes.addressof(datas)), nenv, steps,
                                          int(task), self._p(a), int(nthreads))
+
+    def last_solve(self, d):
+        """so100o_env_step's record of its last substep's solve: (pairs [ncon], forces [ncon, 4] (normal,
+        friction rows), dof frictionloss forces [12], qacc [12], contacts dropped over the step)."""
+        n = d.snap_ncon
+        return (np.array(d.snap_pair[:n], np.int64), np.array([d.snap_force[c][:] for c in range(n)], np.float64).reshape(n, 4),
+                np.array(d.snap_frf[:], np.float64), np.array(d.snap_qacc[:], np.float64), int(d.snap_ndrop))
 
     # state <-> numpy
     def get_state(self, d):

@@ -1852,7 +1852,24 @@ double so100o_env_step(const so100_model* m, so100o_data* d, int task, const flo
   float ctrl[6];
   so100o_unnormalize(m, action, ctrl);
   for (int k = 0; k < 6; k++) d->ctrl[k] = (real)ctrl[k];
-  for (int s = 0; s < m->nsubstep; s++) so100o_substep(m, d);
+  int ndrop = 0;
+  for (int s = 0; s < m->nsubstep; s++) {
+    so100o_substep(m, d);
+    ndrop += d->ncon_dropped;
+  }
+  /* the last substep's solve, for the force parity tests (the final position stage replaces the contacts) */
+  d->snap_ncon = d->ncon;
+  d->snap_ndrop = ndrop;
+  memset(d->snap_force, 0, sizeof(d->snap_force));
+  memset(d->snap_frf, 0, sizeof(d->snap_frf));
+  for (int c = 0; c < d->ncon; c++) d->snap_pair[c] = d->con[c].pair;
+  for (int c = d->ncon; c < SO100_MAXCON; c++) d->snap_pair[c] = -1;
+  for (int i = 0; i < d->nefc; i++) {
+    if (d->efc_type[i] == SO100O_EFC_FRICTION) d->snap_frf[d->efc_id[i]] = d->efc_force[i];
+    if (d->efc_type[i] != SO100O_EFC_CONTACT || d->efc_dim[i] == 0) continue;
+    for (int k = 0; k < d->efc_dim[i] && k < 4; k++) d->snap_force[d->efc_id[i]][k] = d->efc_force[i + k];
+  }
+  memcpy(d->snap_qacc, d->qacc, sizeof(d->qacc));
   so100o_fwd_position(m, d);                         /* dm_control legacy step ends with mj_step1 */
   so100o_fwd_velocity(m, d);
   float cube_f[3] = {(float)d->site_cube[0], (float)d->site_cube[1], (float)d->site_cube[2]};

@@ -1,6 +1,6 @@
 """Diagnostic: GPU vs oracle contact sets on random folded-arm states (the self-collision parity states).
 Counts, per pair category, contacts present in one and not the other, and the distance differences of the
-shared ones.  usage: python tests/dev/contact_set_diff.py [n_states]"""
+shared ones.  usage: python tools/dev/contact_set_diff.py [n_states]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

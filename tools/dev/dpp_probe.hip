@@ -1,4 +1,4 @@
-// probe: what lane i reads with DPP row_shr:1 / row_shr:2 (diagnostic, tests/dev)
+// probe: what lane i reads with DPP row_shr:1 / row_shr:2 (diagnostic, tools/dev)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 __global__ void k(float* o) {

@@ -1,4 +1,4 @@
-// probe: fk_par (lane-parallel) against fk_stage (lane 0) on the start pose, one env row (tests/dev)
+// probe: fk_par (lane-parallel) against fk_stage (lane 0) on the start pose, one env row (tools/dev)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>

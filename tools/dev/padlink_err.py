@@ -1,5 +1,5 @@
 """Diagnostic: qvel error (GPU vs fp64 oracle, and the fp32 oracle's own) on folded-arm states, grouped by
-whether the env has pad/link-hull contacts.  usage: python tests/dev/padlink_err.py [n] [solver]"""
+whether the env has pad/link-hull contacts.  usage: python tools/dev/padlink_err.py [n] [solver]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

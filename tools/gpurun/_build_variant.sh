@@ -1,6 +1,6 @@
 #!/bin/bash
 # build a diagnostic/experimental variant of libso100_hip.so into gym_so100/_lib_var/<name>.so
-# usage: tests/_build_variant.sh <name> "<extra hipcc flags>"
+# usage: tools/gpurun/_build_variant.sh <name> "<extra hipcc flags>"
 set -e
 NAME=$1; EXTRA=$2
 W=/tmp/variant_$NAME

@@ -1,6 +1,6 @@
-"""Copy the round-2 measurement set (tests/_gpu_round2.sh -> gpurun_out/r02) into profiles/r02_*."""
+"""Copy the round-2 measurement set (tools/gpurun/_gpu_round2.sh -> gpurun_out/r02) into profiles/r02_*."""
 import json, os, shutil, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 S, P = os.path.join(ROOT, "gpurun_out", "r02"), os.path.join(ROOT, "profiles")
 cp = {"bench.json": "r02_bench.json", "bench_pgs.json": "r02_bench_pgs.json", "smoke.log": "r02_smoke.log",
       "pytest_gpu.log": "r02_pytest_gpu.log", "lscpu.txt": "r02_gpu_host_lscpu.txt",
@@ -12,7 +12,7 @@ cp = {"bench.json": "r02_bench.json", "bench_pgs.json": "r02_bench_pgs.json", "s
 for a, b in cp.items():
     shutil.copy(os.path.join(S, a), os.path.join(P, b))
 lines = ["# round 2: env steps/s per GPU at the per-GPU shard sizes of the 1/2/4/8-GPU strong-scaling runs (65,536 envs total),",
-         "# 1 MI355X, bench.py --total-envs N --steps 200 --warmup 20, both step modes on the same box (tests/_gpu_round2.sh).",
+         "# 1 MI355X, bench.py --total-envs N --steps 200 --warmup 20, both step modes on the same box (tools/gpurun/_gpu_round2.sh).",
          "# auto mode (the default) takes the fused step up to 49,152 envs per GPU.",
          "# envs  fused_env_steps/s  fused_ms/step  split_env_steps/s  split_ms/step  auto"]
 per = {}

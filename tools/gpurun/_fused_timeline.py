@@ -1,13 +1,13 @@
 """Fused-kernel wave timeline (diagnostic; needs the -DSO100_TIMELINE library variant via SO100_LIB).
 
-usage: SO100_LIB=.../libso100_hip_timeline.so python tests/_fused_timeline.py N [out.npz]
+usage: SO100_LIB=.../libso100_hip_timeline.so python tools/gpurun/_fused_timeline.py N [out.npz]
 (out.npz: wave durations and start times of 4 consecutive steps)
 Each wave's lane-0 env records s_memrealtime (100 MHz) at kernel entry and exit plus HW_ID / XCC_ID in the
 debug row (slots 88..93).  Prints the launch span, wave durations, and how many waves were resident at once.
 """
 import os, sys
 import numpy as np
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-so100-c_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv
 

@@ -1,6 +1,6 @@
 # A/B of library variants (gym_so100/_lib_var/libso100_hip_<name>.so) against the in-tree build on ONE box:
 # bench (default steps) twice each, then a kernel trace of each in the bench's steady state.
-# usage: bash tests/_gpu_ab.sh name1 name2 ...   (writes gpurun_out/ab/*)
+# usage: bash tools/gpurun/_gpu_ab.sh name1 name2 ...   (writes gpurun_out/ab/*)
 export TMPDIR=/tmp
 O=gpurun_out/ab
 rm -rf $O; mkdir -p $O

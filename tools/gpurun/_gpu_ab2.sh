@@ -1,5 +1,5 @@
 # A/B on one box (gpurun_out/ab2/*): in-tree build vs library variants, bench at 65,536 and 8,192 envs,
-# twice each, alternating.  usage: bash tests/_gpu_ab2.sh variant1 [variant2 ...]
+# twice each, alternating.  usage: bash tools/gpurun/_gpu_ab2.sh variant1 [variant2 ...]
 export TMPDIR=/tmp
 O=gpurun_out/ab2
 rm -rf $O; mkdir -p $O

@@ -9,5 +9,5 @@ for n in 65536 8192; do
 done
 B="python bench.py --steps 4 --warmup 30 --no-cpu-baseline --no-kernel-timing --contact-steps 1"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc -o write --output-format csv -- $B > $O/pmc_write.log 2>&1 || exit $?
-python tests/_pmc_report.py $O/pmc | grep -A2 write
+python tools/gpurun/_pmc_report.py $O/pmc | grep -A2 write
 for f in $O/*.json; do echo $f $(grep -o '"value": [0-9.]*' $f); done

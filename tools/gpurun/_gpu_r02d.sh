@@ -12,6 +12,6 @@ for mode in 1 0; do
   SO100_FUSED=$mode timeout -k 10 -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_ICACHE_REQ -d $O/pmc$mode -o sqc --output-format csv -- $B > $O/sqc$mode.log 2>&1 || exit $?
   SO100_FUSED=$mode timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM -d $O/pmc$mode -o sq --output-format csv -- $B > $O/sq$mode.log 2>&1 || exit $?
 done
-python tests/_pmc_sum.py $O/pmc1 $O/pmc0 > $O/pmc_sum.txt 2>&1
+python tools/gpurun/_pmc_sum.py $O/pmc1 $O/pmc0 > $O/pmc_sum.txt 2>&1
 for f in $O/*.json; do echo $f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"kernel_ms": [0-9.]*' $f); done
 echo R02DDONE

@@ -18,12 +18,12 @@ for cfg in "split 65536 16384 4 newton" "fused 8192 8192 1 fused"; do
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $P -o write --output-format csv -- $B > $P.write.log 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $P -o sq --output-format csv -- $B > $P.sq.log 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $P -o misc --output-format csv -- $B > $P.misc.log 2>&1 || exit $?
-  python tests/_pmc_traffic.py $P $3 $O/pmc_traffic_$5.json $4 $5 > $P.traffic.log 2>&1 || exit $?
-  python tests/_pmc_report.py $P > $O/pmc_report_$1.txt 2>&1 || exit $?
+  python tools/gpurun/_pmc_traffic.py $P $3 $O/pmc_traffic_$5.json $4 $5 > $P.traffic.log 2>&1 || exit $?
+  python tools/gpurun/_pmc_report.py $P > $O/pmc_report_$1.txt 2>&1 || exit $?
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_fused -o fused8192 --output-format csv -- python bench.py --total-envs 8192 --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace_fused.log 2>&1 || exit $?
-python tests/_trace_report.py $O/trace > $O/trace_report.txt 2>&1 || exit $?
-python tests/_trace_report.py $O/trace_fused >> $O/trace_report.txt 2>&1 || exit $?
+python tools/gpurun/_trace_report.py $O/trace > $O/trace_report.txt 2>&1 || exit $?
+python tools/gpurun/_trace_report.py $O/trace_fused >> $O/trace_report.txt 2>&1 || exit $?
 lscpu > $O/lscpu.txt 2>&1; nproc > $O/nproc.txt; echo "OMP_NUM_THREADS=$OMP_NUM_THREADS" >> $O/nproc.txt
 for n in 65536 32768 16384 8192; do
   for f in 1 0; do

@@ -1,8 +1,8 @@
 """Diagnostic: per-phase cycles of the Newton solver kernel (last substep of a step); SO100_STAMPS build via
-SO100_LIB.  usage: SO100_LIB=<stamps build> python tests/_newton_stamps_report.py [n]"""
+SO100_LIB.  usage: SO100_LIB=<stamps build> python tools/gpurun/_newton_stamps_report.py [n]"""
 import os, sys
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv

@@ -1,5 +1,5 @@
 """Sum rocprofv3 --pmc counters over the so100 dispatches of a pass directory, per kernel and total
-(diagnostics: tests/_gpu_icache.sh).  usage: python tests/_pmc_sum.py <dir> [<dir> ...]"""
+(diagnostics: tools/gpurun/_gpu_icache.sh).  usage: python tools/gpurun/_pmc_sum.py <dir> [<dir> ...]"""
 import collections, csv, glob, sys
 
 for d in sys.argv[1:]:

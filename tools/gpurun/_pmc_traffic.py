@@ -1,6 +1,6 @@
 """Solver-kernel HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes -> JSON.
 
-usage: python tests/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json>
+usage: python tools/gpurun/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json>
 FETCH_SIZE/WRITE_SIZE are in KB (MI355X_MICROARCH.md, HBM/rocprofv3): memory-side L2->fabric bytes, one
 counter per pass.  The last 20 solver dispatches of each pass are averaged.  gfx950 reports half the
 bytes of 16-B/lane streaming reads in FETCH_SIZE; the solver's reads are 16-B/lane dwordx4, so the
@@ -14,7 +14,7 @@ MI355X_MICROARCH.md) / (step time x 2.4 GHz x 1024 SIMDs).  Counter passes seria
 per-dispatch busy figure from GRBM_GUI_ACTIVE would miss the chunks' overlap; it is recorded as
 valu_issue_frac_serialised for reference only.
 
-usage: python tests/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json> [chunks] [solver]
+usage: python tools/gpurun/_pmc_traffic.py <pmc dir> <envs per solver launch> <out.json> [chunks] [solver]
 solver: newton (so100_newton_kernel), pgs (so100_pgs_kernel; default for old profiles) or fused
 (so100_fused_kernel: one launch per step, chunks = 1).  The Newton
 kernel's reads mix 16-B J rows with 4-B header loads; the same x2 correction is applied (the J rows

@@ -1,8 +1,8 @@
 """Diagnostic: per-phase cycles of the stage kernel (mode 1, last substep); stage-stamps build via SO100_LIB.
-usage: SO100_LIB=<stamps build> python tests/_stage_stamps_report.py [solver] [n] [dyn]"""
+usage: SO100_LIB=<stamps build> python tools/gpurun/_stage_stamps_report.py [solver] [n] [dyn]"""
 import os, sys
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv

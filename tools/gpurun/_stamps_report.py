@@ -2,7 +2,7 @@
 contact count, and QCQP Newton steps per env (stamps build via SO100_LIB)."""
 import os, sys
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv

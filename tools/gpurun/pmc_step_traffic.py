@@ -1,0 +1,64 @@
+"""HBM traffic and VALU work of ONE env step (every kernel of the step) from rocprofv3 --pmc passes -> JSON.
+
+usage: python tools/gpurun/pmc_step_traffic.py <pmc dir> <n_envs> <mode> <solver> <warmup> <steps> <out.json>
+
+The passes profile `bench.py --total-envs n --warmup W --steps S --contact-steps 0 --no-kernel-timing
+--no-cpu-baseline` (fetch*: FETCH_SIZE, write*: WRITE_SIZE, sq*: SQ_INSTS_VALU; one counter block per pass,
+MI355X_MICROARCH.md).  The step's kernels (stage / solver / fused / order) dispatch P times per step; the last
+S x P dispatches (the timed steps) are summed and divided by S.  FETCH_SIZE and WRITE_SIZE are in KB
+(memory-side L2 -> fabric requests).  gfx950 tallies a 16-B/lane streaming read at half its bytes in
+FETCH_SIZE; the step's loads are mostly 4-B/lane and scalar, so hbm_bytes_per_step uses the raw count and
+hbm_bytes_per_step_fetch_x2 is the upper bound with every read doubled.  bench.py reads the JSON
+(profiles/r03_pmc_step_<mode>_<solver>_<n>.json) for roofline.traffic.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+STEP_KERNELS = ("so100_stage_kernel", "so100_newton_kernel", "so100_pgs_kernel", "so100_fused_kernel",
+                "so100_order_kernel")
+
+
+def step_rows(pattern, counter):
+    rows = []
+    for f in glob.glob(pattern):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and any(k in r["Kernel_Name"] for k in STEP_KERNELS):
+                rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"]), r["Kernel_Name"]))
+    rows.sort()
+    return rows
+
+
+def per_step(rows, warmup, steps):
+    total = warmup + steps
+    if not rows or len(rows) % total:
+        raise SystemExit(f"{len(rows)} step-kernel dispatches are not a multiple of {total} steps")
+    p = len(rows) // total
+    last = rows[-steps * p:]
+    return sum(v for _, v, _ in last) / steps, p
+
+
+def main():
+    d, n, mode, solver, warmup, steps, out = sys.argv[1:8]
+    n, warmup, steps = int(n), int(warmup), int(steps)
+    fetch, p = per_step(step_rows(d + "/fetch*counter_collection.csv", "FETCH_SIZE"), warmup, steps)
+    write, _ = per_step(step_rows(d + "/write*counter_collection.csv", "WRITE_SIZE"), warmup, steps)
+    valu = None
+    if glob.glob(d + "/sq*counter_collection.csv"):
+        valu, _ = per_step(step_rows(d + "/sq*counter_collection.csv", "SQ_INSTS_VALU"), warmup, steps)
+    res = {"n_envs": n, "mode": mode, "solver": solver, "dispatches_per_step": p,
+           "fetch_kb_per_step": fetch, "write_kb_per_step": write,
+           "hbm_bytes_per_step": (fetch + write) * 1024, "hbm_bytes_per_step_fetch_x2": (2 * fetch + write) * 1024,
+           "hbm_bytes_per_env_step": (fetch + write) * 1024 / n, "valu_insts_per_step": valu,
+           "file": os.path.basename(out),
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU (separate passes) over bench.py "
+                     f"--total-envs {n} --warmup {warmup} --steps {steps}: the last {steps} steps' {p} step-kernel "
+                     f"dispatches each, summed per step"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
