@@ -361,6 +361,8 @@ int build_device_model(const so100_model* s, DevModel* d) {
   d->iterations = s->iterations;
   if (s->solver != SO100_SOLVER_PGS && s->solver != SO100_SOLVER_NEWTON) return fail("model: unknown solver");
   d->solver = s->solver;
+  if (s->convex != SO100_CONVEX_MPR && s->convex != SO100_CONVEX_EPA) return fail("model: unknown convex collider");
+  d->convex = s->convex;
   d->tolerance = (float)s->tolerance;
   d->impratio = (float)s->impratio;
   for (int k = 0; k < 3; k++) d->gravity[k] = (float)s->gravity[k];

@@ -19,6 +19,7 @@ struct DevModel {
   int nsubstep;
   int iterations;
   int solver;                       // SO100_SOLVER_PGS | SO100_SOLVER_NEWTON
+  int convex;                       // SO100_CONVEX_EPA | SO100_CONVEX_MPR (the mesh pairs' collider)
   float tolerance;
   float impratio;
   float gravity[3];

@@ -575,66 +575,6 @@ DEV void clip_stage(const Poly8& q, Poly8& r, int dir, float sign, float h) {
   }
 }
 
-// deepest point first, then the points closest in angle to the spread targets (ODE cullPoints order)
-DEV void cull_points8(const Poly8& p, int mm, int i0, int* iret) {
-  const int n = p.n;
-  float cx, cy;
-  if (n == 1) { cx = p.x[0]; cy = p.y[0]; }
-  else if (n == 2) { cx = 0.5f * (p.x[0] + p.x[1]); cy = 0.5f * (p.y[0] + p.y[1]); }
-  else {
-    float a = 0.f;
-    cx = 0.f; cy = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if (i < n) {
-        const bool last = (i + 1 >= n);
-        const float xj = last ? p.x[0] : p.x[(i + 1) & 7], yj = last ? p.y[0] : p.y[(i + 1) & 7];
-        const float qq = p.x[i] * yj - xj * p.y[i];
-        a += qq;
-        cx += qq * (p.x[i] + xj);
-        cy += qq * (p.y[i] + yj);
-      }
-    }
-    if (fabsf(a) > 1e-12f) { a = 1.0f / (3.0f * a); cx *= a; cy *= a; }
-    else {
-      cx = 0.f; cy = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; i++) if (i < n) { cx += p.x[i]; cy += p.y[i]; }
-      cx /= (float)n; cy /= (float)n;
-    }
-  }
-  float A[8];
-  uint32_t avail = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    A[i] = (i < n) ? atan2f(p.y[i] - cy, p.x[i] - cx) : 0.f;
-    if (i < n) avail |= 1u << i;
-  }
-  avail &= ~(1u << i0);
-  iret[0] = i0;
-  float Ai0 = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; i++) Ai0 = (i == i0) ? A[i] : Ai0;
-  const float PI = 3.14159265358979323846f;
-#pragma unroll
-  for (int j = 1; j < SO100_MAXCONPAIR; j++) {
-    float a = (float)j * (2.f * PI / (float)mm) + Ai0;
-    if (a > PI) a -= 2.f * PI;
-    float best = 1e9f;
-    int pick = i0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if ((avail >> i) & 1u) {
-        float df = fabsf(A[i] - a);
-        if (df > PI) df = 2.f * PI - df;
-        if (df < best) { best = df; pick = i; }
-      }
-    }
-    iret[j] = pick;
-    avail &= ~(1u << pick);
-  }
-}
-
 // Runtime-indexed reads of small register arrays as masked blends a0 w0 + a1 w1 + a2 w2 (one weight 1,
 // exact for finite values).  A pointer, a dynamic index, or a select chain (which the compiler folds back
 // into an index) would force the array into scratch memory.
@@ -837,26 +777,13 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   }
   const int cnum = K.n;
   if (cnum < 1) return;
-  int idx[SO100_MAXCONPAIR] = {0, 1, 2, 3};
-  int nout = cnum;
-  if (cnum > SO100_MAXCONPAIR) {
-    int i0 = 0;
-    float dmax = D[0];
-#pragma unroll
-    for (int k = 1; k < 8; k++) if (k < cnum && D[k] > dmax) { dmax = D[k]; i0 = k; }
-    cull_points8(K, SO100_MAXCONPAIR, i0, idx);
-    nout = SO100_MAXCONPAIR;
-  }
-  // every slot written unconditionally (slots >= nout are never read): stores under `c < nout` were merged
-  // by the compiler into one store with a run-time slot index, which put `out` in scratch memory
+  // every clipped point within the margin, in clip order (up to 8: mjc_BoxBox keeps them all).  Every slot is
+  // written unconditionally (slots >= cnum are never read): stores under `c < cnum` were merged by the compiler
+  // into one store with a run-time slot index, which put `out` in scratch memory
+  static_assert(SO100_MAXCONPAIR == 8, "the clip polygon holds 8 points");
 #pragma unroll
   for (int c = 0; c < SO100_MAXCONPAIR; c++) {
-    float x = 0.f, y = 0.f, dp = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const bool w = (k == idx[c]);
-      x = w ? K.x[k] : x; y = w ? K.y[k] : y; dp = w ? D[k] : dp;
-    }
+    const float x = K.x[c], y = K.y[c], dp = D[c];
     const float xr = x - cc1, yr = y - cc2;
     const float s1 = i11 * xr + i12 * yr, s2 = i21 * xr + i22 * yr;
 #pragma unroll
@@ -866,7 +793,7 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
     }
     out.dist[c] = -dp;
   }
-  out.n = nout;
+  out.n = cnum;
 }
 
 // geom world pose from the staged body frames
@@ -902,6 +829,24 @@ DEV void collide_pair(const DevModel* __restrict__ m, const EnvShared& sh, int p
   const float margin = m->pair_margin[p];
   if (sqrtf(dot3(d, d)) > sqrtf(dot3(A, A)) + sqrtf(dot3(B, B)) + margin) return;
   box_box(p1, R1, A, p2, R2, B, margin, pc);
+  // the cube against the table's mesh (geom2 = geom 0): MuJoCo's convex collider, one contact per pair (the
+  // oracle's collide_box_pair): the SAT normal, the deepest distance, the mean of the clipped positions
+  if (g2 == 0 && pc.n > 1) {
+    float sp[3] = {0.f, 0.f, 0.f}, dmin = pc.dist[0];
+#pragma unroll
+    for (int c = 0; c < SO100_MAXCONPAIR; c++) {
+      if (c < pc.n) {
+#pragma unroll
+        for (int t = 0; t < 3; t++) sp[t] += pc.pos[c][t];
+        dmin = pc.dist[c] < dmin ? pc.dist[c] : dmin;
+      }
+    }
+    const float nf = (float)pc.n;
+#pragma unroll
+    for (int t = 0; t < 3; t++) pc.pos[0][t] = sp[t] / nf;
+    pc.dist[0] = dmin;
+    pc.n = 1;
+  }
 }
 
 // Arm/jaw hulls vs the table top (pairs SO100_NPAIR_BOX + k; oracle collision()): hull k's lowest
@@ -975,6 +920,8 @@ DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lan
 // constant indices (no scratch).
 struct MprSup {
   float v[3], v1[3], v2[3];
+  uint32_t id;                      // the supports: obj1 box corner signs (bits 0..2) or hull vertex (0..9), obj2 hull
+                                    // vertex << 10 (EPA rebuilds a vertex from it: sup_from_id)
 };
 struct MprObj {
   float c[3], ax[9], h[3];          // obj1 frame in H: origin (box centre / hull body origin), axes
@@ -1012,6 +959,7 @@ DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
     d.v1[t] = w ? s.v1[t] : d.v1[t];
     d.v2[t] = w ? s.v2[t] : d.v2[t];
   }
+  d.id = w ? s.id : d.id;
 }
 
 // first vertex of hull k (vertex range [s0, s0 + n)) maximising (n0, n1, n2) . v: lanes split the
@@ -1020,8 +968,8 @@ DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
 // the cell's possible supports, in vertex order, so the same vertex as a scan of the whole hull, which
 // remains for a cell whose list did not fit and for a zero or non-finite direction).  The direction is
 // uniform over the row, so is the path.
-DEV float3 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s0, int cnt, float n0, float n1, float n2,
-                        int lane) {
+DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s0, int cnt, float n0, float n1, float n2,
+                        int lane) {   // (x, y, z, vertex index within the hull as int bits)
   float best = -__builtin_inff(), bx = 0.f, by = 0.f, bz = 0.f;
   int bi = 0x7fffffff;
   {
@@ -1053,7 +1001,7 @@ DEV float3 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
         if (base + kLanes < cc && s1c > best) { best = s1c; bi = __float_as_int(c1.w); bx = c1.x; by = c1.y; bz = c1.z; }
       }
       arg_best16<false>(best, bi, bx, by, bz);
-      return make_float3(bx, by, bz);
+      return make_float4(bx, by, bz, __int_as_float(bi));
     }
   }
   const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert) + s0;
@@ -1071,10 +1019,11 @@ DEV float3 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
     }
   }
   arg_best16<false>(best, bi, bx, by, bz);
-  return make_float3(bx, by, bz);
+  return make_float4(bx, by, bz, __int_as_float(bi));
 }
 
 DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const float* d, MprSup& s, int lane) {
+  uint32_t id = 0u;
 #pragma unroll
   for (int t = 0; t < 3; t++) s.v1[t] = o.c[t];
   if (o.hull1 < 0) {
@@ -1082,6 +1031,7 @@ DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const floa
     for (int i = 0; i < 3; i++) {
       const float l = o.ax[i] * d[0] + o.ax[3 + i] * d[1] + o.ax[6 + i] * d[2];
       const float sz = l >= 0.f ? o.h[i] : -o.h[i];
+      id |= l >= 0.f ? 1u << i : 0u;
 #pragma unroll
       for (int t = 0; t < 3; t++) s.v1[t] += sz * o.ax[3 * t + i];
     }
@@ -1089,14 +1039,40 @@ DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const floa
     // obj1 hull: the direction into its body frame, its support back into H
     float dl[3], w[3];
     mulmtv3(dl, o.ax, d);
-    const float3 v = hull_support(m, o.cells, o.hull1, o.s1, o.n1, dl[0], dl[1], dl[2], lane);
+    const float4 v = hull_support(m, o.cells, o.hull1, o.s1, o.n1, dl[0], dl[1], dl[2], lane);
     const float vv[3] = {v.x, v.y, v.z};
+    id = (uint32_t)__float_as_int(v.w);
     mulmv3(w, o.ax, vv);
 #pragma unroll
     for (int t = 0; t < 3; t++) s.v1[t] += w[t];
   }
-  const float3 v = hull_support(m, o.cells, o.k, o.s0, o.n, -d[0], -d[1], -d[2], lane);
+  const float4 v = hull_support(m, o.cells, o.k, o.s0, o.n, -d[0], -d[1], -d[2], lane);
   s.v2[0] = v.x; s.v2[1] = v.y; s.v2[2] = v.z;
+  s.id = id | (uint32_t)__float_as_int(v.w) << 10;
+  sub3(s.v, s.v1, s.v2);
+}
+// the support point of mpr_support with these ids, rebuilt by the same arithmetic (bitwise the same point)
+DEV void sup_from_id(const DevModel* __restrict__ m, const MprObj& o, uint32_t id, MprSup& s) {
+#pragma unroll
+  for (int t = 0; t < 3; t++) s.v1[t] = o.c[t];
+  if (o.hull1 < 0) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const float sz = (id >> i) & 1u ? o.h[i] : -o.h[i];
+#pragma unroll
+      for (int t = 0; t < 3; t++) s.v1[t] += sz * o.ax[3 * t + i];
+    }
+  } else {
+    const float4 hv = reinterpret_cast<const float4*>(m->hull_vert)[o.s1 + (int)(id & 1023u)];
+    const float vv[3] = {hv.x, hv.y, hv.z};
+    float w[3];
+    mulmv3(w, o.ax, vv);
+#pragma unroll
+    for (int t = 0; t < 3; t++) s.v1[t] += w[t];
+  }
+  const float4 v2 = reinterpret_cast<const float4*>(m->hull_vert)[o.s0 + (int)((id >> 10) & 1023u)];
+  s.v2[0] = v2.x; s.v2[1] = v2.y; s.v2[2] = v2.z;
+  s.id = id;
   sub3(s.v, s.v1, s.v2);
 }
 DEV void portal_dir(const MprSup* P, float* dir) {
@@ -1237,9 +1213,11 @@ DEV bool mpr_penetration(const DevModel* __restrict__ m, const MprObj& o, float&
                          int lane) {
   MprSup P[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < 4; i++) {
 #pragma unroll
     for (int t = 0; t < 3; t++) { P[i].v[t] = 0.f; P[i].v1[t] = 0.f; P[i].v2[t] = 0.f; }
+    P[i].id = 0u;
+  }
   const int res = mpr_discover(m, o, P, lane);
   if (res < 0 || res == 1) return false;
   if (res == 2) {
@@ -1277,6 +1255,314 @@ DEV bool mpr_penetration(const DevModel* __restrict__ m, const MprObj& o, float&
   normalize3(dir);
   mpr_find_pos(P, pos);
   return true;
+}
+
+// ------------------------------------------------------------------ mesh pairs: GJK + EPA (oracle epa_penetration)
+// MuJoCo 3.3.3's default convex collider (native mjc_ccd): GJK decides the overlap and leaves a tetrahedron of
+// Minkowski-difference support points around the origin; EPA grows it to the facet of A - B nearest the origin:
+// the minimum penetration (depth, normal geom1 -> geom2), witness points from the origin's projection on that
+// facet, one contact at their midpoint.  Row-redundant like MPR: every lane of the row runs the same scalar
+// path on bitwise-identical values, the hull supports and the facet scans are lane-parallel.  The simplex
+// lives in registers (constant slot indices, selects); the polytope in LDS, in the row's env's contact area
+// (ConSlot con[kMaxCon], dead while the narrowphase runs): kEpaMaxF facet planes + vertex triples and
+// kEpaMaxV vertex support ids, the horizon's edge list in registers across the row (3 per lane).
+constexpr int kEpaMaxV = 24, kEpaMaxF = 44, kEpaMaxE = 48;   // oracle EPA_MAXV / EPA_MAXF / EPA_MAXE
+struct EpaPoly {
+  float4 plane[kEpaMaxF];           // outward normal, distance from the origin
+  uint32_t fv[kEpaMaxF];            // vertex indices v0 | v1 << 5 | v2 << 10
+  uint32_t vid[kEpaMaxV];           // the vertices' support ids (sup_from_id)
+};
+static_assert(sizeof(EpaPoly) <= sizeof(ConSlot) * kMaxCon, "an EPA polytope fits an env's contact area");
+
+// the simplex part nearest the origin and the next search direction (oracle gjk_simplex); true when the
+// tetrahedron S[0..3] encloses the origin.  S[n - 1] is the newest point.
+DEV bool gjk_simplex(MprSup* S, int& n, float* d) {
+  if (n == 4) {                                   // A = S[3], B = S[2], C = S[1], D = S[0]
+    float ao[3], ab[3], ac[3], ad[3], nabc[3], nacd[3], nadb[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      ao[k] = -S[3].v[k]; ab[k] = S[2].v[k] - S[3].v[k]; ac[k] = S[1].v[k] - S[3].v[k]; ad[k] = S[0].v[k] - S[3].v[k];
+    }
+    cross3(nabc, ab, ac);
+    cross3(nacd, ac, ad);
+    cross3(nadb, ad, ab);
+    const float s1 = dot3(nabc, ad) > 0.f ? -1.f : 1.f, s2 = dot3(nacd, ab) > 0.f ? -1.f : 1.f;
+    const float s3 = dot3(nadb, ac) > 0.f ? -1.f : 1.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { nabc[k] *= s1; nacd[k] *= s2; nadb[k] *= s3; }
+    const bool f1 = dot3(nabc, ao) > 0.f;
+    const bool f2 = !f1 && dot3(nacd, ao) > 0.f;
+    const bool f3 = !f1 && !f2 && dot3(nadb, ao) > 0.f;
+    if (!f1 && !f2 && !f3) return true;
+    const MprSup t0 = S[0], t1 = S[1], t2 = S[2], t3 = S[3];
+    // f1: (C, B, A); f2: (D, C, A); f3: (B, D, A)
+    sup_sel(S[0], t1, f1); sup_sel(S[0], t2, f3);
+    sup_sel(S[1], t2, f1); sup_sel(S[1], t0, f3);
+    sup_sel(S[2], t3, true);
+    n = 3;
+  }
+  if (n == 3) {                                   // A = S[2], B = S[1], C = S[0]
+    float ao[3], ab[3], ac[3], abc[3], e1[3], e2[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { ao[k] = -S[2].v[k]; ab[k] = S[1].v[k] - S[2].v[k]; ac[k] = S[0].v[k] - S[2].v[k]; }
+    cross3(abc, ab, ac);
+    cross3(e1, abc, ac);
+    cross3(e2, ab, abc);
+    const bool ce = dot3(e1, ao) > 0.f;
+    const bool c_ac = ce && dot3(ac, ao) > 0.f;
+    const bool ab_region = (ce && !c_ac) || (!ce && dot3(e2, ao) > 0.f);
+    const bool c_ab = ab_region && dot3(ab, ao) > 0.f;
+    const bool c_pt = ab_region && !c_ab;
+    const bool face = !ce && !ab_region;
+    const bool above = face && dot3(abc, ao) > 0.f;
+    float t[3], dac[3], dab[3];
+    cross3(t, ac, ao);
+    cross3(dac, t, ac);
+    cross3(t, ab, ao);
+    cross3(dab, t, ab);
+#pragma unroll
+    for (int k = 0; k < 3; k++) d[k] = c_ac ? dac[k] : c_ab ? dab[k] : c_pt ? ao[k] : above ? abc[k] : -abc[k];
+    const MprSup t0 = S[0], t1 = S[1], t2 = S[2];
+    // c_ac: (C, A); c_ab: (B, A); c_pt: (A); below: (B, C, A)
+    sup_sel(S[0], t1, c_ab || (face && !above));
+    sup_sel(S[0], t2, c_pt);
+    sup_sel(S[1], t2, c_ac || c_ab);
+    sup_sel(S[1], t0, face && !above);
+    n = (c_ac || c_ab) ? 2 : c_pt ? 1 : 3;
+    return false;
+  }
+  // line: A = S[1], B = S[0]
+  float ao[3], ab[3], t[3], dl[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { ao[k] = -S[1].v[k]; ab[k] = S[0].v[k] - S[1].v[k]; }
+  const bool seg = dot3(ab, ao) > 0.f;
+  cross3(t, ab, ao);
+  cross3(dl, t, ab);
+#pragma unroll
+  for (int k = 0; k < 3; k++) d[k] = seg ? dl[k] : ao[k];
+  const MprSup t1 = S[1];
+  sup_sel(S[0], t1, !seg);
+  n = seg ? 2 : 1;
+  return false;
+}
+
+// GJK (oracle gjk): true when A - B encloses the origin, S then holds the enclosing tetrahedron
+DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, MprSup* S, int lane) {
+  float d[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) d[k] = o.hc[k] - o.c1[k];
+  if (ccd_zero(dot3(d, d))) d[0] = 1.f;
+  int n = 0;
+  for (int it = 0; it < kMprIters; it++) {
+    const float nd = sqrtf(dot3(d, d));
+    if (ccd_zero(nd)) return false;
+    const float du[3] = {d[0] / nd, d[1] / nd, d[2] / nd};
+    MprSup a;
+    mpr_support(m, o, du, a, lane);
+    if (dot3(a.v, du) <= 0.f) return false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) sup_sel(S[k], a, n == k);
+    n++;
+    if (n > 1 && gjk_simplex(S, n, d)) return true;
+    if (n == 1) { d[0] = -a.v[0]; d[1] = -a.v[1]; d[2] = -a.v[2]; }
+  }
+  return false;
+}
+
+// a facet (a, b, c) of the polytope into slot f (oracle epa_face_set); false for a degenerate triangle
+DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const MprSup& A, const MprSup& B, const MprSup& C) {
+  float ab[3], ac[3], n[3];
+  sub3(ab, B.v, A.v);
+  sub3(ac, C.v, A.v);
+  cross3(n, ab, ac);
+  const float l = sqrtf(dot3(n, n));
+  if (ccd_zero(l)) return false;
+  n[0] = n[0] / l; n[1] = n[1] / l; n[2] = n[2] / l;
+  P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A.v));
+  P.fv[f] = (uint32_t)a | (uint32_t)b << 5 | (uint32_t)c << 10;
+  return true;
+}
+
+// the row's 16 lanes: lane l holds list entries l, l + 16, l + 32 (packed a | b << 5)
+DEV uint32_t erow_get(const uint32_t* e, int j) {
+  const uint32_t v0 = (uint32_t)__shfl((int)e[0], j & 15, kLanes), v1 = (uint32_t)__shfl((int)e[1], j & 15, kLanes);
+  const uint32_t v2 = (uint32_t)__shfl((int)e[2], j & 15, kLanes);
+  return j < 16 ? v0 : j < 32 ? v1 : v2;
+}
+DEV void erow_set(uint32_t* e, int j, uint32_t v, int lane) {
+  const bool mine = (j & 15) == lane;
+  e[0] = (mine && j < 16) ? v : e[0];
+  e[1] = (mine && j >= 16 && j < 32) ? v : e[1];
+  e[2] = (mine && j >= 32) ? v : e[2];
+}
+
+// EPA from GJK's tetrahedron (oracle epa_penetration, the same bookkeeping order): true and (depth, dir
+// geom1 -> geom2, pos) on the facet reached.  P: the row's LDS polytope; lane: 0..15 in the row.
+DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup* S, float& depth, float* dir,
+                         float* pos, EpaPoly& P, int lane, int grp) {
+  uint64_t alive = 0ull;                        // live facet slots (row-uniform)
+  // the initial tetrahedron: faces (0,1,2), (0,3,1), (0,2,3), (1,3,2), each outward (away from the 4th vertex)
+  {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int a = i < 3 ? 0 : 1;
+      int b = i == 0 ? 1 : i == 1 ? 3 : i == 2 ? 2 : 3;
+      int c = i == 0 ? 2 : i == 1 ? 1 : i == 2 ? 3 : 2;
+      const int e = 6 - a - b - c;
+      MprSup A = S[0], B = S[0], C = S[0], E = S[0];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        sup_sel(A, S[k], a == k); sup_sel(B, S[k], b == k); sup_sel(C, S[k], c == k); sup_sel(E, S[k], e == k);
+      }
+      float ab[3], ac[3], ae[3], n[3];
+      sub3(ab, B.v, A.v);
+      sub3(ac, C.v, A.v);
+      sub3(ae, E.v, A.v);
+      cross3(n, ab, ac);
+      const bool flip = dot3(n, ae) > 0.f;
+      const MprSup Bt = B;
+      sup_sel(B, C, flip);
+      sup_sel(C, Bt, flip);
+      const int bb = flip ? c : b, cc = flip ? b : c;
+      ok = ok && epa_face_set(P, i, a, bb, cc, A, B, C);
+      alive |= 1ull << i;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) P.vid[k] = S[k].id;
+    if (!ok) return false;
+  }
+  int nv = 4, best = -1;
+  float bn[3] = {0.f, 0.f, 0.f}, bd = 0.f;
+  for (int it = 0; it < kMprIters; it++) {
+    // the nearest live facet: lanes scan slots lane, lane + 16, lane + 32, then a row (dist, slot) min
+    float dmin = __builtin_inff(), nx = 0.f, ny = 0.f, nz = 0.f;
+    int fmin = 0x7fffffff;
+#pragma unroll
+    for (int s3 = 0; s3 < 3; s3++) {
+      const int f = lane + kLanes * s3;
+      if (f < kEpaMaxF && ((alive >> f) & 1ull)) {
+        const float4 pl = P.plane[f];
+        if (pl.w < dmin) { dmin = pl.w; fmin = f; nx = pl.x; ny = pl.y; nz = pl.z; }
+      }
+    }
+    arg_best16<true>(dmin, fmin, nx, ny, nz);
+    if (fmin == 0x7fffffff) return false;
+    best = fmin; bd = dmin; bn[0] = nx; bn[1] = ny; bn[2] = nz;
+    MprSup w;
+    mpr_support(m, o, bn, w, lane);
+    const float gain = dot3(w.v, bn) - bd;
+    if (gain < kMprTol || nv >= kEpaMaxV) break;
+    // the facets that see w (lane-parallel), as a row-uniform 48-bit mask
+    uint64_t vis = 0ull;
+#pragma unroll
+    for (int s3 = 0; s3 < 3; s3++) {
+      const int f = lane + kLanes * s3;
+      bool v = false;
+      if (f < kEpaMaxF && ((alive >> f) & 1ull)) {
+        const float4 pl = P.plane[f];
+        v = (pl.x * w.v[0] + pl.y * w.v[1] + pl.z * w.v[2]) - pl.w > 0.f;
+      }
+      vis |= ((__ballot(v) >> (grp * kLanes)) & 0xFFFFull) << (kLanes * s3);
+    }
+    // the visible facets' edges in slot order, cancelled against their twins: the horizon
+    uint32_t el[3] = {0u, 0u, 0u};
+    int ne = 0;
+    bool over = false;
+    for (uint64_t vm = vis; vm != 0ull && !over; vm &= vm - 1ull) {
+      const int f = __builtin_ctzll(vm);
+      const uint32_t fv = P.fv[f];
+      const int vtx[3] = {(int)(fv & 31u), (int)((fv >> 5) & 31u), (int)((fv >> 10) & 31u)};
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        if (over) break;
+        const uint32_t a = (uint32_t)vtx[k], b = (uint32_t)vtx[(k + 1) % 3];
+        const uint32_t twin_key = b | a << 5;
+        bool hit = false;
+#pragma unroll
+        for (int s3 = 0; s3 < 3; s3++) hit = hit || (lane + kLanes * s3 < ne && el[s3] == twin_key);
+        // the first list index holding the twin: a row ballot per slot group, lowest group first
+        int twin = -1;
+#pragma unroll
+        for (int s3 = 2; s3 >= 0; s3--) {
+          const bool h = lane + kLanes * s3 < ne && el[s3] == twin_key;
+          const uint32_t bm = (uint32_t)((__ballot(h) >> (grp * kLanes)) & 0xFFFFull);
+          twin = bm ? kLanes * s3 + __builtin_ctz(bm) : twin;
+        }
+        (void)hit;
+        if (twin >= 0) {
+          const uint32_t last = erow_get(el, ne - 1);
+          erow_set(el, twin, last, lane);
+          ne--;
+        } else if (ne < kEpaMaxE) {
+          erow_set(el, ne, a | b << 5, lane);
+          ne++;
+        } else {
+          over = true;
+        }
+      }
+    }
+    if (over) break;                               // the horizon does not fit: stop at the nearest facet
+    alive &= ~vis;
+    const int iw = nv;
+    P.vid[nv] = w.id;
+    nv++;
+    for (int j = 0; j < ne; j++) {
+      const uint64_t freem = ~alive & ((1ull << kEpaMaxF) - 1ull);
+      if (freem == 0ull) break;
+      const int slot = __builtin_ctzll(freem);
+      const uint32_t e = erow_get(el, j);
+      const int a = (int)(e & 31u), b = (int)((e >> 5) & 31u);
+      MprSup A, B;
+      sup_from_id(m, o, P.vid[a], A);
+      sup_from_id(m, o, P.vid[b], B);
+      if (epa_face_set(P, slot, a, b, iw, A, B, w)) alive |= 1ull << slot;
+    }
+  }
+  if (best < 0) return false;
+  depth = bd;
+  if (ccd_zero(depth) || depth < 0.f) return false;
+  // witness points: barycentric coordinates of the origin's projection p = n dist on the facet
+  const uint32_t fv = P.fv[best];
+  MprSup A, B, C;
+  sup_from_id(m, o, P.vid[fv & 31u], A);
+  sup_from_id(m, o, P.vid[(fv >> 5) & 31u], B);
+  sup_from_id(m, o, P.vid[(fv >> 10) & 31u], C);
+  const float p[3] = {bn[0] * bd, bn[1] * bd, bn[2] * bd};
+  float l0, l1, l2;
+  {
+    float v0[3], v1[3], v2[3];
+    sub3(v0, B.v, A.v); sub3(v1, C.v, A.v); sub3(v2, p, A.v);
+    const float d00 = dot3(v0, v0), d01 = dot3(v0, v1), d11 = dot3(v1, v1), d20 = dot3(v2, v0), d21 = dot3(v2, v1);
+    const float den = d00 * d11 - d01 * d01;
+    if (ccd_zero(den)) { l0 = 1.f; l1 = 0.f; l2 = 0.f; }
+    else { l1 = (d11 * d20 - d01 * d21) / den; l2 = (d00 * d21 - d01 * d20) / den; l0 = 1.f - l1 - l2; }
+  }
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    float w1 = 0.f, w2 = 0.f;
+    w1 += l0 * A.v1[t]; w2 += l0 * A.v2[t];
+    w1 += l1 * B.v1[t]; w2 += l1 * B.v2[t];
+    w1 += l2 * C.v1[t]; w2 += l2 * C.v2[t];
+    pos[t] = 0.5f * (w1 + w2);
+    dir[t] = bn[t];
+  }
+  return true;
+}
+
+// the mesh pairs' collider of the model (so100_model.convex): GJK + EPA (MuJoCo 3.3.3's default) or MPR
+DEV bool convex_penetration(const DevModel* __restrict__ m, const MprObj& o, float& depth, float* dir, float* pos,
+                            EpaPoly& P, int lane, int grp) {
+  if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(m, o, depth, dir, pos, lane);
+  MprSup S[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int t = 0; t < 3; t++) { S[i].v[t] = 0.f; S[i].v1[t] = 0.f; S[i].v2[t] = 0.f; }
+    S[i].id = 0u;
+  }
+  if (!gjk_enclose(m, o, S, lane)) return false;
+  return epa_penetration(m, o, S, depth, dir, pos, P, lane, grp);
 }
 
 // world frame of a hull's body: an arm link (bodies 2..7, fk_stage's frames in LDS) or the static Base
@@ -1450,7 +1736,10 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
 #endif
   constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 8
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
-  static_assert(kEnvsPerBlock * kConvex <= (int)sizeof(shm[0].con), "the candidate list fits the contact area");
+  // each env's candidates go to its dynamics scratch (RNE cdd + tau: dead from the collision on; the contact
+  // area holds the rows' EPA polytopes)
+  static_assert(kConvex <= (int)(sizeof(shm[0].ser.cdd) + sizeof(shm[0].ser.tau)), "an env's candidate list fits");
+  static_assert(__builtin_offsetof(SerialScratch, cdd) >= sizeof(ConArea), "the candidate lists do not alias the contact area");
   const EnvShared& sh = shm[grp];
   uint64_t env_cand[2] = {0ull, 0ull};
   uint32_t mine = 0u;                           // bit r: this lane's pair of round r is a candidate
@@ -1477,15 +1766,14 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
   total = 0;   // timing experiment only: broadphase without the narrowphase
 #endif
   if (total == 0) return 0;
-  uint8_t* list = reinterpret_cast<uint8_t*>(&shm[0].con[0]);
-  const int pre_own = grp == 0 ? 0 : grp == 1 ? pre1 : grp == 2 ? pre2 : pre3;
+  uint8_t* own_list = reinterpret_cast<uint8_t*>(&shm[grp].ser.cdd[0][0]);
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
     if ((mine >> r) & 1u) {
       const int q = lane + kLanes * r;     // rank = candidates of this env below pair q
       const uint64_t below0 = q >= 64 ? env_cand[0] : (env_cand[0] & ((1ull << q) - 1ull));
       const uint64_t below1 = q >= 64 ? (env_cand[1] & ((1ull << (q - 64)) - 1ull)) : 0ull;
-      list[pre_own + __popcll(below0) + __popcll(below1)] = (uint8_t)q;
+      own_list[__popcll(below0) + __popcll(below1)] = (uint8_t)q;
     }
   }
   __syncthreads();
@@ -1500,11 +1788,12 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
     bool hit = false;
     int p = SO100_PAIR_MPR0;
     if (act) {
-      p = SO100_PAIR_MPR0 + list[item];
+      const int pre_ie = ie == 0 ? 0 : ie == 1 ? pre1 : ie == 2 ? pre2 : pre3;
+      p = SO100_PAIR_MPR0 + reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_ie];
       MprObj o;
       mpr_obj_setup(m, shm[ie], p, o);
       o.cells = kCells;
-      hit = mpr_penetration(m, o, depth, dir, pos, lane);
+      hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp);
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
     const uint64_t hb = __ballot(hit);

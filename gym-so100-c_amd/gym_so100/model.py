@@ -77,6 +77,7 @@ class SO100Model(ctypes.Structure):
         ("ee", ctypes.c_int), ("weld_pos2", _arr(_d, 3)), ("weld_quat2", _arr(_d, 4)), ("weld_solref", _arr(_d, 2)),
         ("weld_solimp", _arr(_d, 5)), ("weld_torquescale", _d), ("weld_invweight0", _arr(_d, 2)),
         ("mocap_pos0", _arr(_d, 3)), ("mocap_quat0", _arr(_d, 4)),
+        ("convex", _i),
     ]
 
 
@@ -105,13 +106,16 @@ def load_model_dict(path=ASSET):
 
 VARIANTS = ("joint", "ee")
 SOLVERS = {"pgs": 0, "newton": 1}      # SO100_SOLVER_* (include/so100_model.h)
+CONVEX = {"mpr": 0, "epa": 1}          # SO100_CONVEX_* (include/so100_model.h)
 
 
-def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton", variant="joint"):
+def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton", variant="joint", convex="epa"):
     """Return an ``SO100Model`` ctypes struct filled from the derived model table.
 
     solver: "newton" (default: MuJoCo's default solver, which the reference's model uses --
     so_arm100.xml:4 sets no solver) or "pgs" (north_star's projected Gauss-Seidel).
+    convex: the collider of the mesh pairs: "epa" (default: GJK + EPA, MuJoCo 3.3.3's default native
+    convex collider, the minimum penetration) or "mpr" (libccd's MPR, MuJoCo behind mjDSBL_NATIVECCD).
     variant: "joint" (so100_transfer_cube.xml, the registered envs) or "ee" (so100_transfer_cube_ee.xml:
     a weld equality pulls ee_site to a per-env mocap pose, so_arm100_ee.xml:155,171-173)."""
     if variant not in VARIANTS:
@@ -123,6 +127,9 @@ def build_model(path=ASSET, iterations=None, nsubstep=None, solver="newton", var
     m.nsubstep = int(round(C.DT / o["timestep"])) if nsubstep is None else int(nsubstep)   # env.py:120-127
     m.iterations = int(o["iterations"] if iterations is None else iterations)
     m.solver = SOLVERS[solver]
+    if convex not in CONVEX:
+        raise ValueError(f"convex {convex!r}: one of {tuple(CONVEX)}")
+    m.convex = CONVEX[convex]
     m.tolerance = o["tolerance"]
     m.impratio = o["impratio"]
     _set(m, "gravity", o["gravity"])

@@ -88,6 +88,9 @@ class SO100VecEnv:
             fused step launches its debug build; set ``debug_enabled = False`` to run the product build.
         reward64: also keep the reward in float64 (``self.reward64``), as the reference returns it; the
             float32 ``reward`` rounds the dense TouchCube shaping (the other ladders are exact in float32).
+        convex: the collider of the mesh pairs (the cube, bin boxes and finger pads against the link hulls, the
+            links against each other and the Base): "epa" (default: GJK + EPA, MuJoCo 3.3.3's default native
+            convex collider: the minimum penetration) or "mpr" (libccd's MPR, MuJoCo's mjDSBL_NATIVECCD path).
         nsubstep: physics substeps per env step (default: the reference's 10, control_timestep / timestep);
             1 makes an env step one mj_step + the final mj_step1 (the parity tests' per-substep checks).
     """
@@ -95,7 +98,7 @@ class SO100VecEnv:
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
                  iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480,
-                 variant="joint", reward64=False, nsubstep=None):
+                 variant="joint", reward64=False, nsubstep=None, convex="epa"):
         torch = _torch()
         if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
             raise NotImplementedError(f"obs_type={obs_type!r}: 'so100_state' or 'so100_pixels_agent_pos'")
@@ -114,7 +117,7 @@ class SO100VecEnv:
         self.env_offset = int(env_offset)
         self.solver = solver
         self.variant = variant
-        self.model = build_model(iterations=iterations, solver=solver, variant=variant, nsubstep=nsubstep)
+        self.model = build_model(iterations=iterations, solver=solver, variant=variant, nsubstep=nsubstep, convex=convex)
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._handle = self.lib.so100_create(ctypes.byref(self.model), self.num_envs, dev_index)
         if not self._handle:

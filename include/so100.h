@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 11  /* 11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 12  /* 12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */

@@ -60,12 +60,14 @@
 #define SO100_CUBE_GEOM 9
 #define SO100_PAIR_TABLE 8          /* ("red_box", "table") — single_arm.py:354 touch_table */
 #define SO100_NPAIR_GRIPPER 8       /* pairs 0..7 — single_arm.py:348-352 touch_gripper   */
-#define SO100_MAXCONPAIR 4          /* contacts kept per box-box pair (deepest + spread)  */
+#define SO100_MAXCONPAIR 8          /* contacts per box-box pair: every clipped point, as mjc_BoxBox */
 #define SO100_MAXCON 16             /* contacts kept per env per position stage           */
 #define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, table/bin-hull pairs are 3 */
 #define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_MAXCON * SO100_CONDIM)
 #define SO100_SOLVER_PGS 0          /* projected Gauss-Seidel on the dual (mj_solPGS)               */
 #define SO100_SOLVER_NEWTON 1       /* primal Newton with exact line search (mj_solNewton)          */
+#define SO100_CONVEX_MPR 0          /* mesh pairs through libccd's MPR (MuJoCo behind mjDSBL_NATIVECCD)  */
+#define SO100_CONVEX_EPA 1          /* mesh pairs through GJK + EPA (MuJoCo 3.3.3's default native ccd)  */
 #define SO100_NOBS 15               /* box(3) bin(3) ee(3) qpos(6) — env.py:137-145      */
 
 #ifdef __cplusplus
@@ -177,6 +179,10 @@ typedef struct so100_model {
   double weld_invweight0[2];        /* body_invweight0 (tran, rot) of the ee_site body; the mocap body's is 0 */
   double mocap_pos0[3];             /* so_arm100_ee.xml:155 mocap body pose (default of the mocap input) */
   double mocap_quat0[4];
+
+  /* the convex collider of the mesh pairs 23..142 (mjc_Convex): SO100_CONVEX_EPA (MuJoCo 3.3.3's default: the
+   * minimum penetration) or SO100_CONVEX_MPR (libccd's MPR: the penetration along the centres' ray) */
+  int    convex;
 } so100_model;
 
 #ifdef __cplusplus

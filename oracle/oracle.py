@@ -96,6 +96,8 @@ class Oracle:
         L.so100o_observe.argtypes = [P, P, P]
         L.so100o_batch_run.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
         L.so100o_batch_run.restype = ctypes.c_long
+        L.so100o_box_box.argtypes = [P, P, P, P, P, P, self.real, P]
+        L.so100o_box_box.restype = ctypes.c_int
 
     # --- helpers -------------------------------------------------------------------------
     @staticmethod

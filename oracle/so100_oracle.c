@@ -359,10 +359,10 @@ static void solve_m(const so100o_data* d, real x[NV], const real y[NV]) {
 
 /* ---------------------------------------------------------------- box-box narrowphase
  * Separating-axis test over the 15 axes, then (face case) clip the incident face against the
- * reference face and keep penetrating points, culled to SO100_MAXCONPAIR by depth + angular spread;
+ * reference face and keep every clipped point within the margin, in clip order: up to 8 contacts per
+ * pair, as MuJoCo's mjc_BoxBox returns them (no culling to 4: that is ODE's dBoxBox option) [3P-unverified];
  * (edge case) one contact between the closest points of the two edges.  Normal points from geom1
- * to geom2; contact position is midway between the surfaces; dist = -depth.  This is the standard
- * box-box algorithm (ODE dBoxBox lineage) that MuJoCo's mjc_BoxBox also implements [3P]. */
+ * to geom2; contact position is midway between the surfaces; dist = -depth. */
 static int clip_rect_quad(const real h[2], const real quad[8], real out[16]) {
   real bufa[16], bufb[16];
   real* q = bufa;
@@ -391,48 +391,6 @@ static int clip_rect_quad(const real h[2], const real quad[8], real out[16]) {
   }
   memcpy(out, q, sizeof(real) * 2 * nq);
   return nq;
-}
-
-static void cull_points(int n, const real p[16], int m, int i0, int iret[]) {
-  real cx, cy;
-  if (n == 1) { cx = p[0]; cy = p[1]; }
-  else if (n == 2) { cx = (real)0.5 * (p[0] + p[2]); cy = (real)0.5 * (p[1] + p[3]); }
-  else {
-    real a = 0, q;
-    cx = 0; cy = 0;
-    for (int i = 0; i < n; i++) {
-      int j = (i + 1) % n;
-      q = p[2 * i] * p[2 * j + 1] - p[2 * j] * p[2 * i + 1];
-      a += q;
-      cx += q * (p[2 * i] + p[2 * j]);
-      cy += q * (p[2 * i + 1] + p[2 * j + 1]);
-    }
-    if (fabs((double)a) > 1e-12) { a = (real)1 / ((real)3 * a); cx *= a; cy *= a; }
-    else {
-      cx = 0; cy = 0;
-      for (int i = 0; i < n; i++) { cx += p[2 * i]; cy += p[2 * i + 1]; }
-      cx /= (real)n; cy /= (real)n;
-    }
-  }
-  real A[8];
-  int avail[8];
-  for (int i = 0; i < n; i++) { A[i] = (real)atan2((double)(p[2 * i + 1] - cy), (double)(p[2 * i] - cx)); avail[i] = 1; }
-  avail[i0] = 0;
-  iret[0] = i0;
-  const real PI = (real)3.14159265358979323846;
-  for (int j = 1; j < m; j++) {
-    real a = (real)j * (2 * PI / (real)m) + A[i0];
-    if (a > PI) a -= 2 * PI;
-    real best = (real)1e9;
-    iret[j] = i0;
-    for (int i = 0; i < n; i++) {
-      if (!avail[i]) continue;
-      real df = (real)fabs((double)(A[i] - a));
-      if (df > PI) df = 2 * PI - df;
-      if (df < best) { best = df; iret[j] = i; }
-    }
-    avail[iret[j]] = 0;
-  }
 }
 
 /* returns number of contacts written (<= SO100_MAXCONPAIR) */
@@ -552,7 +510,7 @@ static int box_box(const real p1[3], const real R1[9], const real A[3], const re
   if (fabs((double)det) < 1e-12) return 0;
   det = 1 / det;
   real i11 = m22 * det, i12 = -m12 * det, i21 = -m21 * det, i22 = m11 * det;
-  real P3[8][3], dep[8], P2[16];
+  real P3[8][3], dep[8];
   int cnum = 0;
   for (int k = 0; k < n; k++) {
     real x = pts[2 * k] - cc1, y = pts[2 * k + 1] - cc2;
@@ -563,30 +521,25 @@ static int box_box(const real p1[3], const real R1[9], const real A[3], const re
     if (dp > -margin) {
       for (int t = 0; t < 3; t++) P3[cnum][t] = pt[t] + pR[t];
       dep[cnum] = dp;
-      P2[2 * cnum] = pts[2 * k];
-      P2[2 * cnum + 1] = pts[2 * k + 1];
       cnum++;
     }
   }
   if (cnum < 1) return 0;
-  int idx[8], nout = cnum;
-  if (cnum > SO100_MAXCONPAIR) {
-    int i0 = 0;
-    for (int k = 1; k < cnum; k++) if (dep[k] > dep[i0]) i0 = k;
-    cull_points(cnum, P2, SO100_MAXCONPAIR, i0, idx);
-    nout = SO100_MAXCONPAIR;
-  } else {
-    for (int k = 0; k < cnum; k++) idx[k] = k;
-  }
-  for (int c = 0; c < nout; c++) {
-    int k = idx[c];
+  for (int c = 0; c < cnum; c++) {
     for (int t = 0; t < 3; t++) {
-      out[c].pos[t] = P3[k][t] + (real)0.5 * dep[k] * nref[t];
+      out[c].pos[t] = P3[c][t] + (real)0.5 * dep[c] * nref[t];
       out[c].frame[t] = normal[t];
     }
-    out[c].dist = -dep[k];
+    out[c].dist = -dep[c];
   }
-  return nout;
+  return cnum;
+}
+
+/* test hook (tests/test_oracle_physics.py): the box-box collider on two boxes given by centre, row-major
+ * rotation and half sizes; returns the contact count, contacts in out[0..n) (frames: the normal only) */
+int so100o_box_box(const so100o_real p1[3], const so100o_real R1[9], const so100o_real A[3], const so100o_real p2[3],
+                   const so100o_real R2[9], const so100o_real B[3], so100o_real margin, so100o_contact out[SO100_MAXCONPAIR]) {
+  return box_box(p1, R1, A, p2, R2, B, margin, out);
 }
 
 /* [3P] mju_makeFrame: tangents from the normal (y-axis candidate (0,1,0) unless near-parallel) */
@@ -869,6 +822,200 @@ static int mpr_penetration(const mpr_obj* o, real* depth, real dir[3], real pos[
     portal_expand(P, &v4);
   }
 }
+/* ---------------------------------------------------------------- convex pairs: GJK + EPA
+ * [3P] MuJoCo 3.3.3's default convex collider: mjc_Convex -> the native mjc_ccd (engine_collision_gjk.c), on by
+ * default since 3.3.0 (libccd's MPR, above, stays behind mjDSBL_NATIVECCD) [3P-unverified].  GJK decides the
+ * overlap and leaves a tetrahedron of Minkowski-difference (A - B) support points enclosing the origin; EPA
+ * expands it towards the facet of A - B nearest the origin, which gives the minimum penetration: depth = the
+ * facet's distance, normal = its outward normal (geom1 -> geom2), and the witness points from the barycentric
+ * coordinates of the origin's projection on the facet; one contact per pair (no multiccd) at the witnesses'
+ * midpoint.  Restated from the published algorithms (GJK: Gilbert, Johnson, Keerthi 1988, simplex cases as in
+ * van den Bergen 2003; EPA: van den Bergen 2001), with MuJoCo's ccd_tolerance 1e-6 and ccd_iterations 50 for
+ * each loop.  MuJoCo's own sub-distance routine (signed volumes) and polytope bookkeeping change the path, not
+ * the converged facet.  Supports: mpr_support (box corner by sign, first maximal hull vertex). */
+/* polytope bounds: 24 vertices (20 EPA iterations), so at most 2 * 24 - 4 = 44 live faces; the horizon's
+ * edge list holds 48 edges.  EPA stops at the current nearest facet when a bound would be passed (the kernel
+ * keeps the polytope of a pair in 1 KB of LDS; measured: <= 13 iterations in random-action rollouts, 23 in
+ * random folded arm poses, tools/dev/mpr_vs_epa.py) */
+#define EPA_MAXV 24
+#define EPA_MAXF 44
+#define EPA_MAXE 48
+typedef struct { int v[3]; real n[3]; real dist; int alive; } epa_face;
+
+
+/* the simplex's sub-simplex nearest the origin, and the next search direction (towards the origin);
+ * returns 1 when the origin is enclosed by the tetrahedron */
+static int gjk_simplex(mpr_sup S[4], int* n, real d[3]) {
+  real ao[3], ab[3], ac[3], ad[3], t[3], abc[3];
+  if (*n == 2) {                                  /* line: A = S[1] (newest), B = S[0] */
+    for (int k = 0; k < 3; k++) { ao[k] = -S[1].v[k]; ab[k] = S[0].v[k] - S[1].v[k]; }
+    if (dot3(ab, ao) > 0) { cross3(t, ab, ao); cross3(d, t, ab); }
+    else { S[0] = S[1]; *n = 1; for (int k = 0; k < 3; k++) d[k] = ao[k]; }
+    return 0;
+  }
+  if (*n == 3) {                                  /* triangle: A = S[2], B = S[1], C = S[0] */
+    for (int k = 0; k < 3; k++) { ao[k] = -S[2].v[k]; ab[k] = S[1].v[k] - S[2].v[k]; ac[k] = S[0].v[k] - S[2].v[k]; }
+    cross3(abc, ab, ac);
+    real e[3];
+    cross3(e, abc, ac);                           /* edge AC's outward normal in the plane */
+    if (dot3(e, ao) > 0) {
+      if (dot3(ac, ao) > 0) { S[1] = S[2]; *n = 2; cross3(t, ac, ao); cross3(d, t, ac); return 0; }
+      goto edge_ab;
+    }
+    cross3(e, ab, abc);                           /* edge AB's outward normal */
+    if (dot3(e, ao) > 0) {
+    edge_ab:
+      if (dot3(ab, ao) > 0) { S[0] = S[1]; S[1] = S[2]; *n = 2; cross3(t, ab, ao); cross3(d, t, ab); return 0; }
+      S[0] = S[2]; *n = 1; for (int k = 0; k < 3; k++) d[k] = ao[k];
+      return 0;
+    }
+    if (dot3(abc, ao) > 0) { for (int k = 0; k < 3; k++) d[k] = abc[k]; }
+    else {                                        /* below: flip the winding so that abc faces the origin */
+      mpr_sup tmp = S[0]; S[0] = S[1]; S[1] = tmp;
+      for (int k = 0; k < 3; k++) d[k] = -abc[k];
+    }
+    return 0;
+  }
+  /* tetrahedron: A = S[3] (newest), B = S[2], C = S[1], D = S[0]; BCD's winding faces away from A */
+  for (int k = 0; k < 3; k++) {
+    ao[k] = -S[3].v[k]; ab[k] = S[2].v[k] - S[3].v[k]; ac[k] = S[1].v[k] - S[3].v[k]; ad[k] = S[0].v[k] - S[3].v[k];
+  }
+  real nabc[3], nacd[3], nadb[3];
+  cross3(nabc, ab, ac);
+  cross3(nacd, ac, ad);
+  cross3(nadb, ad, ab);
+  /* orient each face normal away from the fourth vertex */
+  if (dot3(nabc, ad) > 0) for (int k = 0; k < 3; k++) nabc[k] = -nabc[k];
+  if (dot3(nacd, ab) > 0) for (int k = 0; k < 3; k++) nacd[k] = -nacd[k];
+  if (dot3(nadb, ac) > 0) for (int k = 0; k < 3; k++) nadb[k] = -nadb[k];
+  if (dot3(nabc, ao) > 0) { S[0] = S[1]; S[1] = S[2]; S[2] = S[3]; *n = 3; return gjk_simplex(S, n, d); }
+  if (dot3(nacd, ao) > 0) { S[2] = S[3]; *n = 3; /* D, C, A */ return gjk_simplex(S, n, d); }
+  if (dot3(nadb, ao) > 0) { S[1] = S[0]; S[0] = S[2]; S[2] = S[3]; *n = 3; return gjk_simplex(S, n, d); }
+  return 1;
+}
+
+/* GJK: 1 when A - B encloses the origin (S holds the enclosing tetrahedron), 0 otherwise */
+static int gjk(const mpr_obj* o, mpr_sup S[4]) {
+  real d[3];
+  for (int k = 0; k < 3; k++) d[k] = o->hc[k] - o->c1[k];   /* from the interior point c1 - hc towards the origin */
+  if (ccd_zero(dot3(d, d))) d[0] = 1;
+  int n = 0;
+  for (int it = 0; it < MPR_ITERS; it++) {
+    real nd = (real)sqrt((double)dot3(d, d));
+    if (ccd_zero(nd)) return 0;                    /* the origin on the simplex: touching */
+    real du[3] = {d[0] / nd, d[1] / nd, d[2] / nd};
+    mpr_sup a;
+    mpr_support(o, du, &a);
+    if (dot3(a.v, du) <= 0) return 0;              /* the support does not pass the origin: separated or touching */
+    S[n++] = a;
+    if (n > 1 && gjk_simplex(S, &n, d)) return 1;
+    if (n == 1) for (int k = 0; k < 3; k++) d[k] = -a.v[k];
+  }
+  return 0;
+}
+
+static int epa_face_set(epa_face* f, const mpr_sup* V, int a, int b, int c) {
+  real ab[3], ac[3], n[3];
+  sub3(ab, V[b].v, V[a].v);
+  sub3(ac, V[c].v, V[a].v);
+  cross3(n, ab, ac);
+  real l = (real)sqrt((double)dot3(n, n));
+  if (ccd_zero(l)) return 0;
+  for (int k = 0; k < 3; k++) f->n[k] = n[k] / l;
+  f->v[0] = a; f->v[1] = b; f->v[2] = c;
+  f->dist = dot3(f->n, V[a].v);
+  f->alive = 1;
+  return 1;
+}
+
+/* EPA from GJK's tetrahedron: 1 and (depth, dir geom1 -> geom2, pos) on the facet reached.  Bookkeeping in
+ * the kernel's order (so100_step.hip epa_penetration): faces in slots, the nearest the first alive slot of least
+ * distance; a face is visible from w when n . w - dist > 0; the visible faces' edges, taken in slot order,
+ * cancel against their twins in a list (swap-remove), leaving the horizon in list order; each horizon edge
+ * (a, b) gets the face (a, b, w) in the lowest free slot. */
+static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir[3], real pos[3]) {
+  mpr_sup V[EPA_MAXV];
+  epa_face F[EPA_MAXF];
+  int nv = 4;
+  for (int i = 0; i < EPA_MAXF; i++) F[i].alive = 0;
+  for (int i = 0; i < 4; i++) V[i] = S[i];
+  static const int tet[4][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 3}, {1, 3, 2}};
+  for (int i = 0; i < 4; i++) {
+    int a = tet[i][0], b = tet[i][1], c = tet[i][2], e = 6 - a - b - c;
+    real ab[3], ac[3], n[3], ae[3];
+    sub3(ab, V[b].v, V[a].v);
+    sub3(ac, V[c].v, V[a].v);
+    sub3(ae, V[e].v, V[a].v);
+    cross3(n, ab, ac);
+    if (dot3(n, ae) > 0) { int t = b; b = c; c = t; }   /* outward: away from the fourth vertex */
+    if (!epa_face_set(&F[i], V, a, b, c)) return 0;
+  }
+  int best = -1;
+  for (int it = 0; it < MPR_ITERS; it++) {
+    best = -1;
+    for (int i = 0; i < EPA_MAXF; i++)
+      if (F[i].alive && (best < 0 || F[i].dist < F[best].dist)) best = i;
+    if (best < 0) return 0;
+    mpr_sup w;
+    mpr_support(o, F[best].n, &w);
+    const real gain = dot3(w.v, F[best].n) - F[best].dist;
+    if (gain < MPR_TOL || nv >= EPA_MAXV) break;
+    int edges[EPA_MAXE][2], ne = 0, over = 0;
+    for (int i = 0; i < EPA_MAXF && !over; i++) {
+      if (!F[i].alive || !(dot3(F[i].n, w.v) - F[i].dist > 0)) continue;
+      for (int k = 0; k < 3; k++) {
+        const int a = F[i].v[k], b = F[i].v[(k + 1) % 3];
+        int twin = -1;
+        for (int j = 0; j < ne; j++)
+          if (edges[j][0] == b && edges[j][1] == a) { twin = j; break; }
+        if (twin >= 0) { edges[twin][0] = edges[ne - 1][0]; edges[twin][1] = edges[ne - 1][1]; ne--; }
+        else if (ne < EPA_MAXE) { edges[ne][0] = a; edges[ne][1] = b; ne++; }
+        else { over = 1; break; }
+      }
+    }
+    if (over) break;                                      /* the horizon does not fit: stop at the nearest facet */
+    for (int i = 0; i < EPA_MAXF; i++)
+      if (F[i].alive && dot3(F[i].n, w.v) - F[i].dist > 0) F[i].alive = 0;
+    const int iw = nv;
+    V[nv++] = w;
+    for (int j = 0; j < ne; j++) {
+      int slot = -1;
+      for (int i = 0; i < EPA_MAXF; i++) if (!F[i].alive) { slot = i; break; }
+      if (slot < 0) break;
+      epa_face_set(&F[slot], V, edges[j][0], edges[j][1], iw);
+    }
+  }
+  if (best < 0) return 0;
+  const epa_face* f = &F[best];
+  *depth = f->dist;
+  if (ccd_zero(*depth) || *depth < 0) return 0;           /* touching: no normal (as MPR) */
+  /* barycentric coordinates of the origin's projection p = n dist on the facet */
+  real p[3] = {f->n[0] * f->dist, f->n[1] * f->dist, f->n[2] * f->dist}, l[3];
+  {
+    const real* a = V[f->v[0]].v; const real* b = V[f->v[1]].v; const real* c = V[f->v[2]].v;
+    real v0[3], v1[3], v2[3];
+    sub3(v0, b, a); sub3(v1, c, a); sub3(v2, p, a);
+    real d00 = dot3(v0, v0), d01 = dot3(v0, v1), d11 = dot3(v1, v1), d20 = dot3(v2, v0), d21 = dot3(v2, v1);
+    real den = d00 * d11 - d01 * d01;
+    if (ccd_zero(den)) { l[0] = 1; l[1] = 0; l[2] = 0; }
+    else { l[1] = (d11 * d20 - d01 * d21) / den; l[2] = (d00 * d21 - d01 * d20) / den; l[0] = 1 - l[1] - l[2]; }
+  }
+  for (int t = 0; t < 3; t++) {
+    real w1 = 0, w2 = 0;
+    for (int k = 0; k < 3; k++) { w1 += l[k] * V[f->v[k]].v1[t]; w2 += l[k] * V[f->v[k]].v2[t]; }
+    pos[t] = (real)0.5 * (w1 + w2);
+    dir[t] = f->n[t];
+  }
+  return 1;
+}
+
+static int convex_penetration(const so100_model* m, const mpr_obj* o, real* depth, real dir[3], real pos[3]) {
+  if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(o, depth, dir, pos);
+  mpr_sup S[4];
+  if (!gjk(o, S)) return 0;
+  return epa_penetration(o, S, depth, dir, pos);
+}
+
 /* conservative broadphase for (box, hull k) in H: bounding spheres, then OBB-OBB separating axes
  * (the hull's H-aligned bounding box vs the box; |R| padded by 1e-5) */
 static int mpr_broadphase(const mpr_obj* o, const real hb[3], const real hh[3]) {
@@ -898,7 +1045,14 @@ static int mpr_broadphase(const mpr_obj* o, const real hb[3], const real hh[3]) 
   return 1;
 }
 
-/* one box-box pair (bounding-sphere broadphase, then box_box); pairs 0..13 and the pad-bin pairs */
+/* one box-box pair (bounding-sphere broadphase, then box_box); pairs 0..13 and the pad-bin pairs.
+ * The cube against the table (pair 8, geom2 = the table's mesh, scene_so100.xml:3,20): MuJoCo routes
+ * box-mesh through its convex collider (mjc_Convex: native GJK/EPA in 3.3.3), one contact per pair without
+ * multiccd (so_arm100.xml:4 sets none) [3P-unverified].  The table mesh is an exact box, so the minimum
+ * penetration (normal, depth) is the separating-axis result; the one contact takes the SAT normal, the
+ * deepest point's distance, and the mean of the clipped contact positions (the contact patch's centre: the
+ * face centre for a cube resting flat).  EPA's own witness point depends on its polytope triangulation and
+ * is not restated (DESIGN.md §4 deviation 1). */
 static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
   int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
   real A[3], B[3];
@@ -910,6 +1064,16 @@ static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
   if (norm3(dp) > norm3(A) + norm3(B) + margin) return;
   so100o_contact tmp[SO100_MAXCONPAIR];
   int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin, tmp);
+  if (g2 == 0 && n > 1) {                  /* the table mesh: the convex collider's one contact */
+    real sp[3] = {0, 0, 0}, dmin = tmp[0].dist;
+    for (int c = 0; c < n; c++) {
+      for (int t = 0; t < 3; t++) sp[t] += tmp[c].pos[t];
+      if (tmp[c].dist < dmin) dmin = tmp[c].dist;
+    }
+    for (int t = 0; t < 3; t++) tmp[0].pos[t] = sp[t] / (real)n;
+    tmp[0].dist = dmin;
+    n = 1;
+  }
   for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
 }
 
@@ -1023,7 +1187,7 @@ static void collision(const so100_model* m, so100o_data* d) {
     load3(hh, m->hull_half[k]);
     if (!mpr_broadphase(&o, hb, hh)) continue;
     real depth, dir[3], pos[3];
-    if (!mpr_penetration(&o, &depth, dir, pos)) continue;
+    if (!convex_penetration(m, &o, &depth, dir, pos)) continue;
     so100o_contact con;
     memset(&con, 0, sizeof(con));
     mulmv3(con.frame, RH, dir);

@@ -699,13 +699,14 @@ def test_pad_contact_parity(solver, oracle64, oracle32):
     assert r.drop_gpu.sum() == 0
 
 
-@pytest.mark.parametrize("solver", ["newton", "pgs"])
-def test_mpr_contact_parity(solver, oracle64, oracle32):
-    """Box-hull contacts through the MPR collider (pairs 23..76: the cube and the bin boxes against the
-    arm/jaw hulls): states from fp64-oracle random-action rollouts that hold such
-    contacts, then teacher-forced GPU steps against the oracle at the fp32 floor."""
+@pytest.mark.parametrize("solver,convex", [("newton", "epa"), ("pgs", "epa"), ("newton", "mpr"), ("pgs", "mpr")])
+def test_mpr_contact_parity(solver, convex, oracle64, oracle32):
+    """Box-hull contacts through the convex collider (pairs 23..76: the cube and the bin boxes against the
+    arm/jaw hulls), GJK + EPA (MuJoCo 3.3.3's default) and libccd's MPR: states from fp64-oracle
+    random-action rollouts that hold such contacts, then teacher-forced GPU steps against the oracle at the
+    fp32 floor."""
     from gym_so100.model import PAIR_MPR0, PAIR_PAD0, NHULL, build_model
-    model = build_model(solver=solver)
+    model = build_model(solver=solver, convex=convex)
     rng = np.random.default_rng(21)
     d = oracle64.new_data()
     states, kinds = [], set()
@@ -724,14 +725,14 @@ def test_mpr_contact_parity(solver, oracle64, oracle32):
             break
     n = len(states)
     assert n >= 24 and kinds == {True, False}, (n, kinds)     # both cube-hull and bin-hull contacts
-    env = _new_env(n, solver)
+    env = _new_env(n, solver, convex=convex)
     env.reset(seed=3)
     _set_states(env, states)
     r = _tf_run(env, model, oracle64, oracle32, 3, lambda step: rng.uniform(-1, 1, (n, 6))).arrays()
     env.close()
     mpr_con = np.array([int(((p >= PAIR_MPR0) & (p < PAIR_PAD0)).sum()) for p in r.pairs])
-    print(f"\n{n} envs, GPU MPR contacts per env mean {mpr_con.mean():.2f} (envs with any: {(mpr_con > 0).mean():.2f}); "
-          + r.summary(f"{solver} box-hull (MPR)"))
+    print(f"\n{n} envs, GPU convex contacts per env mean {mpr_con.mean():.2f} (envs with any: {(mpr_con > 0).mean():.2f}); "
+          + r.summary(f"{solver} box-hull ({convex.upper()})"))
     assert (mpr_con[:n] > 0).mean() > 0.3              # the GPU collider sees the contacts too
     # MPR's fp32 branches (different portals) make the tail chaotic for ANY fp32 implementation: the
     # fp32 oracle and the GPU put their large deviations on different states, so the tail is compared by

@@ -1,5 +1,7 @@
-"""Box vs convex hull contacts through the MPR convex collider (pairs 23..76: the cube and the bin boxes
-against every arm/jaw hull) in the oracle.
+"""Box vs convex hull contacts through the convex collider (pairs 23..76: the cube and the bin boxes
+against every arm/jaw hull) in the oracle, with both colliders the model offers: GJK + EPA
+(so100_model.convex = SO100_CONVEX_EPA, MuJoCo 3.3.3's default native collider: the minimum penetration) and
+libccd's MPR (SO100_CONVEX_MPR, MuJoCo's mjDSBL_NATIVECCD path: the penetration along the centres' ray).
 
 MuJoCo is not in this container, so the expected values are restated, not MuJoCo's own:
   * a known answer: a box-shaped "hull" overlapping an aligned cube by delta along one axis;
@@ -13,9 +15,18 @@ MuJoCo is not in this container, so the expected values are restated, not MuJoCo
 import copy
 
 import numpy as np
+import pytest
 from scipy.spatial import ConvexHull
 
-from gym_so100.model import NHULL, PAIR_MPR0, PAIR_PAD0, PAIR_BASE0
+from gym_so100.model import NHULL, PAIR_MPR0, PAIR_PAD0, PAIR_BASE0, build_model
+
+
+@pytest.fixture(params=["epa", "mpr"], scope="module")
+def model(request):
+    """this module's tests run with each convex collider"""
+    m = build_model(convex=request.param)
+    m.convex_name = request.param
+    return m
 
 NV = 12
 CUBE_HALF = 0.02
@@ -146,6 +157,7 @@ def test_mpr_matches_separating_axis_geometry(model, oracle64):
     equal to it for shallow contacts and for most deep ones (MPR approximates the minimum only along its
     centre line), and the shapes still overlap by at least that much along the reported normal."""
     n_miss, ratio, shallow = 0, [], 0
+    m_epa = model.convex_name == "epa"
     for arm, k, box in _random_overlaps(model, oracle64, 160, seed=5):
         d = _state(oracle64, model, arm, box)
         b = model.hull_body[k]
@@ -166,9 +178,12 @@ def test_mpr_matches_separating_axis_geometry(model, oracle64):
         c = got[0]
         depth, nrm = -c.dist, np.array(c.frame[:3])
         assert abs(np.linalg.norm(nrm) - 1) < 1e-12
-        assert depth >= sat - 1e-6, (depth, sat)           # MPR stops within ccd_tolerance
+        assert depth >= sat - 1e-6, (depth, sat)           # MPR / EPA stop within ccd_tolerance
         overlap = (cube_w @ nrm).max() - (hull_w @ nrm).min()
         assert overlap >= depth - 1e-9, (overlap, depth)
+        if m_epa:                                           # EPA converges to the minimum penetration itself
+            assert abs(depth - sat) < 1e-6 + 1e-6 * sat, (depth, sat)
+            assert abs(overlap - depth) < 1e-6 + 1e-6 * sat, (overlap, depth)
         if sat < 2e-3:
             assert abs(depth - sat) < 1e-7 + 1e-4 * sat, (depth, sat)
             shallow += 1

@@ -144,34 +144,90 @@ def test_quaternion_integration_closed_form(model, oracle64):
     np.testing.assert_allclose(q, want, atol=1e-6)   # frictionloss 1e-12 leaves a tiny residual torque
 
 
+def _quat2mat(q):
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
 def _contacts(d):
     return [(d.con[i].pair, np.array(d.con[i].pos[:]), np.array(d.con[i].frame[:3]), d.con[i].dist)
             for i in range(d.ncon)]
 
 
-def test_box_on_table_four_corner_contacts(model, oracle64):
+def test_box_on_table_one_convex_contact(model, oracle64):
+    """The cube against the table's mesh (scene_so100.xml:3,20) goes through MuJoCo's convex collider: one
+    contact per pair without multiccd [3P-unverified]: normal from geom1 (red_box) to geom2 (table), the
+    penetration depth, at the contact patch's centre (the face centre for a cube lying flat), midway in z."""
     pen = 0.001
     d = fresh(oracle64, model, box=(-0.2, 0.45, 0.02 - pen, 1, 0, 0, 0))
     cs = [c for c in _contacts(d) if c[0] == 8]
-    assert len(cs) == 4
-    for pair, pos, n, dist in cs:
-        np.testing.assert_allclose(n, [0, 0, -1], atol=1e-12)       # geom1 (red_box) -> geom2 (table)
-        assert abs(dist + pen) < 1e-12
-        assert abs(pos[2] + pen / 2) < 1e-12                        # midway between the surfaces
-        assert abs(abs(pos[0] + 0.2) - 0.02) < 1e-12 and abs(abs(pos[1] - 0.45) - 0.02) < 1e-12
+    assert len(cs) == 1
+    _, pos, n, dist = cs[0]
+    np.testing.assert_allclose(n, [0, 0, -1], atol=1e-12)
+    assert abs(dist + pen) < 1e-12
+    np.testing.assert_allclose(pos, [-0.2, 0.45, -pen / 2], atol=1e-12)
 
 
-def test_box_on_edge_two_contacts(model, oracle64):
-    # cube rotated 45 deg about x, resting on its edge: two contacts along the edge
+def test_box_on_edge_one_convex_contact(model, oracle64):
+    # cube rotated 45 deg about x, resting on its edge: one contact at the edge's midpoint
     s = math.sin(math.pi / 8)
     c = math.cos(math.pi / 8)
     zc = 0.02 * math.sqrt(2) - 0.0005
     d = fresh(oracle64, model, box=(-0.2, 0.45, zc, c, s, 0, 0))
     cs = [x for x in _contacts(d) if x[0] == 8]
-    assert len(cs) == 2
-    for _, pos, n, dist in cs:
-        assert abs(dist + 0.0005) < 1e-9
-        assert abs(pos[1] - 0.45) < 1e-9
+    assert len(cs) == 1
+    _, pos, n, dist = cs[0]
+    assert abs(dist + 0.0005) < 1e-9
+    assert abs(pos[0] + 0.2) < 1e-9 and abs(pos[1] - 0.45) < 1e-9 and abs(pos[2] + 0.00025) < 1e-9
+
+
+def test_tilted_box_convex_contact_is_the_deepest_penetration(model, oracle64):
+    """A tilted cube dipping into the table: the one contact's depth is the deepest corner's penetration
+    (the exact minimum penetration of two boxes along the top face's normal, checked against the corners),
+    its position the mean of the penetrating points of the incident face, all inside the footprint."""
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = rng.uniform(0, 0.3)
+        q = np.array([math.cos(ang / 2), *(math.sin(ang / 2) * ax)])
+        R = _quat2mat(q)
+        corners = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]) * 0.02 @ R.T
+        zc = -corners[:, 2].min() - rng.uniform(1e-4, 2e-3)
+        d = fresh(oracle64, model, box=(-0.2, 0.45, zc, *q))
+        cs = [c for c in _contacts(d) if c[0] == 8]
+        assert len(cs) == 1
+        _, pos, n, dist = cs[0]
+        deepest = (corners[:, 2] + zc).min()
+        assert abs(dist - deepest) < 1e-9
+        np.testing.assert_allclose(n, [0, 0, -1], atol=1e-9)
+        assert abs(pos[0] + 0.2) < 0.02 * math.sqrt(3) and abs(pos[1] - 0.45) < 0.02 * math.sqrt(3)
+
+
+def test_box_box_keeps_every_clipped_point(oracle64):
+    """mjc_BoxBox keeps every clipped point (up to 8) [3P-unverified], no culling to 4: two equal boxes face to
+    face, one turned 45 deg about the shared normal, overlap in the regular octagon of their two squares."""
+    import ctypes
+    o = oracle64
+    real = o.real
+    arr = lambda v: (real * len(v))(*v)
+    c45 = math.cos(math.pi / 4)
+    pen = 0.002
+    out = (o.Contact * 8)()
+    n = o.lib.so100o_box_box(arr([0, 0, 0]), arr([1, 0, 0, 0, 1, 0, 0, 0, 1]), arr([0.02, 0.02, 0.02]),
+                             arr([0, 0, 0.04 - pen]), arr([c45, -c45, 0, c45, c45, 0, 0, 0, 1]), arr([0.02, 0.02, 0.02]),
+                             real(0.0), ctypes.byref(out))
+    assert n == 8
+    pts = np.array([[out[k].pos[0], out[k].pos[1], out[k].pos[2]] for k in range(n)])
+    for k in range(n):
+        assert abs(out[k].dist + pen) < 1e-12
+        np.testing.assert_allclose(out[k].frame[:3], [0, 0, 1], atol=1e-12)
+    np.testing.assert_allclose(pts[:, 2], 0.02 - pen / 2, atol=1e-12)
+    r = np.hypot(pts[:, 0], pts[:, 1])                      # the octagon's vertices
+    np.testing.assert_allclose(r, 0.02 / math.cos(math.pi / 8), rtol=1e-9)
+    assert len({round(math.degrees(math.atan2(y, x))) % 360 for x, y in pts[:, :2]}) == 8
 
 
 def test_separated_boxes_no_contact(model, oracle64):

@@ -1,0 +1,24 @@
+# round-3 pass C (narrowphase: mjc_BoxBox count, one convex contact for cube-table): GPU suite (product-kernel parity, forces, configs[2]), smoke, bench line, kernel trace,
+# per-step PMC traffic at the bench size (65,536, split) and the 8-GPU shard (8,192, fused)
+export TMPDIR=/tmp
+O=gpurun_out/r03c
+rm -rf $O; mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread -s > $O/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc" >> $O/pytest_gpu.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
+timeout -k 10 300 python bench.py --total-envs 8192 --no-cpu-baseline > $O/bench_8192.json 2> $O/bench_8192.err || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o bench --output-format csv -- python bench.py --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_fused -o fused8192 --output-format csv -- python bench.py --total-envs 8192 --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace_fused.log 2>&1 || exit $?
+for cfg in "split 65536" "fused 8192"; do
+  set -- $cfg
+  B="python bench.py --total-envs $2 --warmup 40 --steps 5 --no-cpu-baseline --no-kernel-timing --contact-steps 0"
+  P=$O/pmc_$1_$2
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $P -o fetch --output-format csv -- $B > $P.fetch.log 2>&1 || exit $?
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $P -o write --output-format csv -- $B > $P.write.log 2>&1 || exit $?
+  timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU -d $P -o sq --output-format csv -- $B > $P.sq.log 2>&1 || exit $?
+  python tools/gpurun/pmc_step_traffic.py $P $2 $1 newton 40 5 $O/r03_pmc_step_$1_newton_$2.json > $P.traffic.log 2>&1 || exit $?
+done
+lscpu > $O/lscpu.txt 2>&1; python -c "import os; print(len(os.sched_getaffinity(0)), os.cpu_count())" > $O/affinity.txt
+echo R03C_DONE
