@@ -22,6 +22,10 @@
 #include "so100_kin.h"
 #include "so100_newton.h"
 
+// hull supports through the direction cells in the split path's stage kernel too (the fused kernel always)
+#ifndef SO100_SPLIT_CELLS
+#define SO100_SPLIT_CELLS 0
+#endif
 namespace so100 {
 
 DEV void cross_motion(float* r, const float* v, const float* u) {
@@ -2263,7 +2267,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
     SSTAMP(6);
-    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, lane, grp, valid);
+    const int nmpr = mpr_contacts<kFused || SO100_SPLIT_CELLS>(m, &sh - grp, lane, grp, valid);
     SSTAMP(7);
     PairContacts pc;
     pc.n = 0;

@@ -1,0 +1,99 @@
+"""The oracle's GJK + EPA mesh collider (MuJoCo 3.3.3's default native convex collider) against
+an independent exact minimum penetration, on every kind of mesh pair: the cube and the bin boxes against the
+link hulls, hull-hull self-collision, the Base hull, the finger pads against link hulls.
+
+The exact minimum penetration of two convex polytopes A (geom1) and B (geom2) is the facet of their Minkowski
+difference A - B nearest the origin (scipy ConvexHull of every vertex difference; a box is its 8 corners):
+its distance is the depth, its outward normal the direction B must move to separate (geom1 -> geom2).  EPA
+converges to that facet to ccd_tolerance (1e-6).  States: random arm poses, the cube dropped near the arm
+(tools/dev/mpr_vs_epa.py measures libccd's MPR against the same reference: 29 % of its rollout contacts have
+normals more than 5 deg off).
+"""
+import math
+
+import numpy as np
+import pytest
+from scipy.spatial import ConvexHull
+
+from gym_so100.model import PAIR_MPR0, PAIR_SELF0, PAIR_BASE0, PAIR_PADLINK0, PAIR_PAD0, build_model
+
+
+def _points(m, d, g):
+    if g >= 0:
+        R = np.array(d.geom_xmat[g][:]).reshape(3, 3)
+        h = np.array(m.geom_size[g][:])
+        s = np.array([[a, b, c] for a in (-1, 1) for b in (-1, 1) for c in (-1, 1)], dtype=float)
+        return (s * h) @ R.T + np.array(d.geom_xpos[g][:])
+    k = -1 - g
+    b = m.hull_body[k]
+    R = np.array(d.xmat[b][:]).reshape(3, 3)
+    s, n = m.hull_start[k], m.hull_count[k]
+    return np.array([m.hull_vert[s + i][:] for i in range(n)]) @ R.T + np.array(d.xpos[b][:])
+
+
+def _exact(A, B):
+    """(depth, normal) of the minimum penetration, and every facet's (distance, normal) for tie checks"""
+    eq = ConvexHull((A[:, None, :] - B[None, :, :]).reshape(-1, 3)).equations
+    dist = -eq[:, 3]
+    f = int(np.argmin(dist))
+    return dist[f], eq[f, :3], dist, eq[:, :3]
+
+
+@pytest.fixture(scope="module")
+def epa_contacts(oracle64):
+    m = build_model(convex="epa")
+    d = oracle64.new_data()
+    rng = np.random.default_rng(29)
+    lo = np.array([r[0] for r in m.jnt_range]); hi = np.array([r[1] for r in m.jnt_range])
+    out = []
+    while len(out) < 240:
+        arm = rng.uniform(lo, hi)
+        oracle64.reset(m, d, np.array([rng.uniform(-0.45, -0.15), rng.uniform(0.35, 0.75), rng.uniform(0.01, 0.2),
+                                       1, 0, 0, 0]))
+        for k in range(6):
+            d.qpos[k] = arm[k]
+        oracle64.call("so100o_fwd_position", m, d)
+        for i in range(d.ncon):
+            c = d.con[i]
+            if PAIR_MPR0 <= c.pair < PAIR_PAD0:
+                A, B = _points(m, d, m.pair_geom1[c.pair]), _points(m, d, m.pair_geom2[c.pair])
+                out.append((c.pair, -c.dist, np.array(c.frame[:3]), np.array(c.pos[:]), A, B))
+    return out
+
+
+def test_epa_depth_is_the_minimum_penetration(epa_contacts):
+    classes = set()
+    for p, depth, n, pos, A, B in epa_contacts:
+        ex, _, _, _ = _exact(A, B)
+        assert abs(depth - ex) <= 1e-6, (p, depth, ex)           # EPA stops within ccd_tolerance
+        classes.add("box-hull" if p < PAIR_SELF0 else "self" if p < PAIR_BASE0 else "Base" if p < PAIR_PADLINK0
+                    else "pad-link")
+    assert classes == {"box-hull", "self", "Base", "pad-link"}
+
+
+def test_epa_normal_is_a_minimum_penetration_direction(epa_contacts):
+    """Along the EPA normal the shapes overlap by exactly the depth (a minimum-penetration direction); it is
+    the nearest facet's normal except where facets tie in depth (deep folds)"""
+    off, angles = 0, []
+    for p, depth, n, pos, A, B in epa_contacts:
+        assert abs(np.linalg.norm(n) - 1) < 1e-12
+        overlap = (A @ n).max() - (B @ n).min()
+        assert abs(overlap - depth) <= 1e-6, (p, overlap, depth)
+        ex, en, dist, normals = _exact(A, B)
+        ang = math.degrees(math.acos(max(-1.0, min(1.0, float(n @ en)))))
+        angles.append(ang)
+        if ang > 0.05:
+            # then a facet of (nearly) the same depth has this normal (deep folds: facets tie)
+            near = normals[dist < ex + 1e-6]
+            assert (near @ n).max() > 1 - 1e-6, (p, ang)
+            off += 1
+    # (EPA stops within ccd_tolerance: on thin facets its normal may lean by ~1e-4 rad)
+    assert off <= 0.02 * len(epa_contacts) and np.median(angles) < 1e-4
+
+
+def test_epa_position_is_between_the_surfaces(epa_contacts):
+    """the witness points' midpoint lies within the overlap along the normal, at mid-depth"""
+    for p, depth, n, pos, A, B in epa_contacts:
+        lo_b, hi_a = (B @ n).min(), (A @ n).max()
+        assert lo_b - 1e-9 <= pos @ n <= hi_a + 1e-9
+        assert abs(pos @ n - 0.5 * (lo_b + hi_a)) < 1e-6 + 1e-3 * depth
