@@ -69,6 +69,8 @@ def parse(argv=None):
     p.add_argument("--contact-steps", type=int, default=10, help="untimed steps sampling contacts/env")
     p.add_argument("--solver", default="newton", choices=["newton", "pgs"],
                    help="constraint solver: newton (MuJoCo's default, which the reference runs; default) or pgs")
+    p.add_argument("--convex", default="epa", choices=["epa", "mpr"],
+                   help="mesh-pair collider: epa (GJK + EPA, MuJoCo 3.3.3's default; default) or mpr (libccd)")
     return p.parse_args(argv)
 
 
@@ -157,7 +159,8 @@ def main(argv=None):
         scaling = "strong"
 
     from gym_so100 import SO100VecEnv
-    env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset, solver=args.solver)
+    env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset, solver=args.solver,
+                      convex=args.convex)
     env.reset(seed=1000 + offset)   # env i <- RandomState(1000 + global id)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed * 1000003 + rank)
@@ -242,7 +245,7 @@ def main(argv=None):
                                     f"({count} per GPU), joint-space ctrl, fp32 state, CubeToBin reward, "
                                     "auto-reset"),
                        "envs_total": total, "envs_per_gpu": count, "task": args.task, "substeps": 10,
-                       "solver": args.solver, "solver_iterations": env.model.iterations,
+                       "solver": args.solver, "solver_iterations": env.model.iterations, "convex": args.convex,
                        "step_mode": mode, "fused_build": env.fused_build if fused else None,
                        "parallelism": f"env-sharded x{world}, no collectives (gloo barrier + MAX for timing)",
                        "actions": "U[-1,1]^6 pool resident in HBM"},

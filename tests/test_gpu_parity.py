@@ -1073,7 +1073,10 @@ def test_config2_benched_split_full_size():
     """configs[2] as bench.py times it on one GPU: 65,536 envs in one process run the split step (4 env
     chunks on concurrent streams, auto mode) with auto-reset; 40 steps of random actions keep the state
     finite and the contract: unit quaternions, obs layout, reward ladder, no divergence, TimeLimit counters,
-    and no contact dropped by the 16-per-env cap (the rate is printed)."""
+    and the 16-per-env contact cap binding as rarely as in the oracle: MuJoCo keeps every box-box point (up to 8
+    per pair), and a jaw jammed into the bin walls collects 20-46 pad-bin contacts, so the cap drops some; the
+    fp64 oracle on this workload drops 3.4e-4 per env step (tools/dev/contact_drops.py, 65,536 x 40), the
+    bar is 1e-3 (DESIGN.md §4 deviation 2)."""
     from gym_so100 import SO100VecEnv
     n = 65536
     env = SO100VecEnv(n, device="cuda:0", seed=0)
@@ -1104,7 +1107,7 @@ def test_config2_benched_split_full_size():
     assert ((env.elapsed == 40) | (env.episode > 1)).all()         # TimeLimit 700 not reached (only successes reset)
     assert rewards <= {0.0, 1.0, 2.0, 2.5, 3.0, 4.0}
     print(f"\n65,536 envs x 40 steps: contacts dropped by the 16-per-env cap: {drops} ({drops / (40 * n):.2e} per env step)")
-    assert drops == 0
+    assert drops / (40 * n) <= 1e-3
     env.close()
 
 

@@ -12,7 +12,7 @@ import torch
 from gym_so100 import SO100VecEnv
 
 n = int(sys.argv[1])
-env = SO100VecEnv(n, device="cuda:0", seed=0, debug=True)
+env = SO100VecEnv(n, device="cuda:0", seed=0, debug=True, convex=os.environ.get("CONVEX", "epa"))
 env.reset(seed=1000)
 g = torch.Generator(device="cuda").manual_seed(0)
 hist = []
