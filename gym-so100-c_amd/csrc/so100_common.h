@@ -116,6 +116,28 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
 #pragma unroll
   for (int i = 0; i < 3; i++) { d[i] = laminv[i]; w[i] = c[i] * d[i]; }
   float s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+#ifndef SO100_QCQP_SECULAR
+  // MuJoCo's iteration (mju_QCQP3; oracle qcqp): Newton on val = |y|^2 - r^2 from la = 0, at most 20 steps,
+  // stops val < 1e-10 or delta < 1e-10; after the 20th step y stays at the la it was evaluated at.  In the
+  // eigenbasis |y|^2 = sum w_i^2 and y' (A + la I)^-1 y = sum w_i^2 d_i, so delta = -val / deriv = val / 2t.
+  if (live && s - r * r >= 1e-10f) {
+    float la = 0.f;
+    for (int it = 0; it < 20; it++) {
+      const float val = s - r * r;
+      if (val < 1e-10f) break;
+      const float t = w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2];
+      const float delta = val / (2.f * t);
+      if (delta < 1e-10f) break;
+      nit++;
+      la += delta;
+      if (it == 19) break;
+#pragma unroll
+      for (int i = 0; i < 3; i++) { d[i] = 1.f / (lam[i] + la); w[i] = c[i] * d[i]; }
+      s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    }
+  }
+#else
+  // Newton on the secular equation 1/|y| = 1/r from a lower bound (round 1-2; DESIGN.md §4 deviation 6)
   if (live && s - r * r >= 1e-10f) {
     const float rinv = __builtin_amdgcn_rcpf(r);
     const float cn = __builtin_amdgcn_sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);   // raw v_sqrt (1 ulp)
@@ -136,6 +158,7 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
       s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     }
   }
+#endif
   // x = D Q w = P' w
 #pragma unroll
   for (int j = 0; j < 3; j++) x[j] = P[j] * w[0] + P[3 + j] * w[1] + P[6 + j] * w[2];

@@ -1374,15 +1374,15 @@ DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, MprSup* S,
 }
 
 // a facet (a, b, c) of the polytope into slot f (oracle epa_face_set); false for a degenerate triangle
-DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const MprSup& A, const MprSup& B, const MprSup& C) {
+DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const float* A, const float* B, const float* C) {
   float ab[3], ac[3], n[3];
-  sub3(ab, B.v, A.v);
-  sub3(ac, C.v, A.v);
+  sub3(ab, B, A);
+  sub3(ac, C, A);
   cross3(n, ab, ac);
   const float l = sqrtf(dot3(n, n));
   if (ccd_zero(l)) return false;
   n[0] = n[0] / l; n[1] = n[1] / l; n[2] = n[2] / l;
-  P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A.v));
+  P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A));
   P.fv[f] = (uint32_t)a | (uint32_t)b << 5 | (uint32_t)c << 10;
   return true;
 }
@@ -1398,6 +1398,29 @@ DEV void erow_set(uint32_t* e, int j, uint32_t v, int lane) {
   e[0] = (mine && j < 16) ? v : e[0];
   e[1] = (mine && j >= 16 && j < 32) ? v : e[1];
   e[2] = (mine && j >= 32) ? v : e[2];
+}
+
+// The polytope's vertex positions (the Minkowski-difference points) across the row's lanes: vertex i on lane
+// i & 15, slot i >> 4 (kEpaMaxV <= 32), so a new facet's two horizon vertices come from 3 row shuffles each
+// instead of two dependent global loads of their supports (sup_from_id): bitwise the same points.
+struct EpaVerts {
+  float x[2], y[2], z[2];
+};
+DEV void everts_set(EpaVerts& V, int i, const float* v, int lane) {
+  const bool mine = (i & 15) == lane;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const bool w = mine && (i >> 4) == s;
+    V.x[s] = w ? v[0] : V.x[s];
+    V.y[s] = w ? v[1] : V.y[s];
+    V.z[s] = w ? v[2] : V.z[s];
+  }
+}
+DEV void everts_get(const EpaVerts& V, int i, float* v) {
+  const bool hi = i >= 16;                        // row-uniform
+  v[0] = __shfl(hi ? V.x[1] : V.x[0], i & 15, kLanes);
+  v[1] = __shfl(hi ? V.y[1] : V.y[0], i & 15, kLanes);
+  v[2] = __shfl(hi ? V.z[1] : V.z[0], i & 15, kLanes);
 }
 
 // EPA from GJK's tetrahedron (oracle epa_penetration, the same bookkeeping order): true and (depth, dir
@@ -1429,13 +1452,18 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
       sup_sel(B, C, flip);
       sup_sel(C, Bt, flip);
       const int bb = flip ? c : b, cc = flip ? b : c;
-      ok = ok && epa_face_set(P, i, a, bb, cc, A, B, C);
+      ok = ok && epa_face_set(P, i, a, bb, cc, A.v, B.v, C.v);
       alive |= 1ull << i;
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) P.vid[k] = S[k].id;
     if (!ok) return false;
   }
+  EpaVerts V;
+#pragma unroll
+  for (int s = 0; s < 2; s++) { V.x[s] = 0.f; V.y[s] = 0.f; V.z[s] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < 4; k++) everts_set(V, k, S[k].v, lane);
   int nv = 4, best = -1;
   float bn[3] = {0.f, 0.f, 0.f}, bd = 0.f;
   for (int it = 0; it < kMprIters; it++) {
@@ -1510,6 +1538,7 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
     alive &= ~vis;
     const int iw = nv;
     P.vid[nv] = w.id;
+    everts_set(V, nv, w.v, lane);
     nv++;
     for (int j = 0; j < ne; j++) {
       const uint64_t freem = ~alive & ((1ull << kEpaMaxF) - 1ull);
@@ -1517,10 +1546,10 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
       const int slot = __builtin_ctzll(freem);
       const uint32_t e = erow_get(el, j);
       const int a = (int)(e & 31u), b = (int)((e >> 5) & 31u);
-      MprSup A, B;
-      sup_from_id(m, o, P.vid[a], A);
-      sup_from_id(m, o, P.vid[b], B);
-      if (epa_face_set(P, slot, a, b, iw, A, B, w)) alive |= 1ull << slot;
+      float av[3], bv[3];
+      everts_get(V, a, av);
+      everts_get(V, b, bv);
+      if (epa_face_set(P, slot, a, b, iw, av, bv, w.v)) alive |= 1ull << slot;
     }
   }
   if (best < 0) return false;

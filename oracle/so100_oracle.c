@@ -894,6 +894,20 @@ static int gjk_simplex(mpr_sup S[4], int* n, real d[3]) {
   return 1;
 }
 
+#ifdef SO100O_STATS
+/* dev probe (tools/dev/narrowphase_stats.py): per position stage (candidates, GJK overlaps, contacts, GJK
+ * iterations, EPA iterations); single-threaded runs only */
+#define SO100O_NSTAT 5
+static long so100o_stat_cur[SO100O_NSTAT];
+static long* so100o_stat_buf;
+static long so100o_stat_n, so100o_stat_cap;
+void so100o_stats_reset(long* buf, long cap) { so100o_stat_buf = buf; so100o_stat_cap = cap; so100o_stat_n = 0; }
+long so100o_stats_count(void) { return so100o_stat_n; }
+#define STAT(k, v) (so100o_stat_cur[k] += (v))
+#else
+#define STAT(k, v) ((void)0)
+#endif
+
 /* GJK: 1 when A - B encloses the origin (S holds the enclosing tetrahedron), 0 otherwise */
 static int gjk(const mpr_obj* o, mpr_sup S[4]) {
   real d[3];
@@ -901,6 +915,7 @@ static int gjk(const mpr_obj* o, mpr_sup S[4]) {
   if (ccd_zero(dot3(d, d))) d[0] = 1;
   int n = 0;
   for (int it = 0; it < MPR_ITERS; it++) {
+    STAT(3, 1);
     real nd = (real)sqrt((double)dot3(d, d));
     if (ccd_zero(nd)) return 0;                    /* the origin on the simplex: touching */
     real du[3] = {d[0] / nd, d[1] / nd, d[2] / nd};
@@ -952,6 +967,7 @@ static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir
   }
   int best = -1;
   for (int it = 0; it < MPR_ITERS; it++) {
+    STAT(4, 1);
     best = -1;
     for (int i = 0; i < EPA_MAXF; i++)
       if (F[i].alive && (best < 0 || F[i].dist < F[best].dist)) best = i;
@@ -1013,6 +1029,7 @@ static int convex_penetration(const so100_model* m, const mpr_obj* o, real* dept
   if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(o, depth, dir, pos);
   mpr_sup S[4];
   if (!gjk(o, S)) return 0;
+  STAT(1, 1);
   return epa_penetration(o, S, depth, dir, pos);
 }
 
@@ -1186,8 +1203,10 @@ static void collision(const so100_model* m, so100o_data* d) {
     load3(hb, m->hull_center[k]);
     load3(hh, m->hull_half[k]);
     if (!mpr_broadphase(&o, hb, hh)) continue;
+    STAT(0, 1);
     real depth, dir[3], pos[3];
     if (!convex_penetration(m, &o, &depth, dir, pos)) continue;
+    STAT(2, 1);
     so100o_contact con;
     memset(&con, 0, sizeof(con));
     mulmv3(con.frame, RH, dir);
@@ -1199,6 +1218,12 @@ static void collision(const so100_model* m, so100o_data* d) {
   /* pairs 143..190: the finger pads vs the table (143..150), then vs the bin boxes (box-box) */
   for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_PADBIN0; p++) pad_table(m, d, p);
   for (int p = SO100_PAIR_PADBIN0; p < SO100_NPAIR; p++) collide_box_pair(m, d, p);
+#ifdef SO100O_STATS
+  if (so100o_stat_buf && so100o_stat_n < so100o_stat_cap)
+    for (int k = 0; k < SO100O_NSTAT; k++) so100o_stat_buf[so100o_stat_n * SO100O_NSTAT + k] = so100o_stat_cur[k];
+  so100o_stat_n++;
+  memset(so100o_stat_cur, 0, sizeof(so100o_stat_cur));
+#endif
 }
 
 uint32_t so100o_contact_bits(const so100o_data* d) {

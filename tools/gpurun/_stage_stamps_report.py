@@ -7,7 +7,8 @@ sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd"))
 import torch
 from gym_so100 import SO100VecEnv
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-env = SO100VecEnv(n, device="cuda:0", debug=True, solver=sys.argv[1] if len(sys.argv) > 1 else "newton")
+env = SO100VecEnv(n, device="cuda:0", debug=True, solver=sys.argv[1] if len(sys.argv) > 1 else "newton",
+                  convex=os.environ.get("CONVEX", "epa"))
 env.reset(seed=1000)
 g = torch.Generator(device="cuda").manual_seed(0)
 for i in range(60):
