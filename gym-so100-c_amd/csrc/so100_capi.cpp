@@ -635,11 +635,24 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   std::vector<float> hv;
   hull_cells_build(model, hc, hv);
   std::memcpy(h.hull_cells, hc.data(), sizeof(h.hull_cells));
+  // the candidate lists, then each cell's list as a fixed block of kCellBlk (padded with its last candidate;
+  // longer lists keep the list path), in one buffer
+  const size_t nlist = hv.size() / 4, ncell = hc.size();
+  std::vector<float> all(hv);
+  all.resize(4 * (nlist + ncell * so100::kCellBlk), 0.f);
+  for (size_t c = 0; c < ncell; c++) {
+    const uint32_t cnt = hc[c] & 255u, start = hc[c] >> 8;
+    for (int i = 0; i < so100::kCellBlk && cnt > 0; i++) {
+      const size_t src = start + std::min<uint32_t>((uint32_t)i, cnt - 1u);
+      std::memcpy(&all[4 * (nlist + c * so100::kCellBlk + i)], &hv[4 * src], 4 * sizeof(float));
+    }
+  }
   float4* dcand = nullptr;
-  e = hipMalloc(&dcand, std::max<size_t>(hv.size(), 4) * sizeof(float));
-  if (e == hipSuccess && !hv.empty()) e = hipMemcpy(dcand, hv.data(), hv.size() * sizeof(float), hipMemcpyHostToDevice);
+  e = hipMalloc(&dcand, all.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(dcand, all.data(), all.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e != hipSuccess) { if (dcand) (void)hipFree(dcand); fail_hip("so100_create: hull cells", e); return nullptr; }
   h.hull_cand = reinterpret_cast<const so100::float4_t*>(dcand);
+  h.hull_blk = reinterpret_cast<const so100::float4_t*>(dcand) + nlist;
   DevModel* dm = nullptr;
   e = hipMalloc(&dm, sizeof(DevModel));
   if (e != hipSuccess) { (void)hipFree(dcand); fail_hip("so100_create: hipMalloc", e); return nullptr; }

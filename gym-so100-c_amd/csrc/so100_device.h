@@ -13,6 +13,7 @@ constexpr int kThreads = kLanes * kEnvsPerBlock;
 constexpr int kNArm = SO100_NHINGE;
 constexpr int kMaxCon = SO100_MAXCON;
 
+constexpr int kCellBlk = 16;   // candidates per support cell block (DevModel::hull_blk): one per lane of a row
 struct DevModel {
   // options
   float timestep;
@@ -87,6 +88,9 @@ struct DevModel {
   // into hull_cand (x, y, z, vertex index bits; count 0: scan the hull)
   uint32_t hull_cells[SO100_NHULL_ALL * SO100_HULL_NCELL];
   const float4_t* hull_cand;
+  // the same lists as fixed blocks of kCellBlk per cell (cell c at c * kCellBlk; lists of <= kCellBlk padded
+  // with their last candidate): a row loads its cell's candidates with one load issued beside the cell entry's
+  const float4_t* hull_blk;
   float table_top, table_lo[2], table_hi[2];
 
   // sites

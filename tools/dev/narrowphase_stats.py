@@ -29,6 +29,8 @@ def main():
     lib.so100o_reset.argtypes = o.lib.so100o_reset.argtypes
     lib.so100o_stats_reset.argtypes = [ctypes.c_void_p, ctypes.c_long]
     lib.so100o_stats_count.restype = ctypes.c_long
+    lib.so100o_items_reset.argtypes = [ctypes.c_void_p, ctypes.c_long]
+    lib.so100o_items_count.restype = ctypes.c_long
     o.lib = lib
     m = build_model()
     datas = (o.Data * nenv)()
@@ -41,8 +43,11 @@ def main():
         o.batch_run(m, datas, nenv, 1, 0, rng.uniform(-1, 1, (1, nenv, 6)).astype(np.float32), nthreads=1)
     buf = np.zeros((steps * nenv * per_step + 16, 5), np.int64)
     lib.so100o_stats_reset(buf.ctypes.data, len(buf))
+    items = np.zeros((4 << 20, 4), np.int64)
+    lib.so100o_items_reset(items.ctypes.data, len(items))
     for s in range(steps):
         o.batch_run(m, datas, nenv, 1, 0, rng.uniform(-1, 1, (1, nenv, 6)).astype(np.float32), nthreads=1)
+    item_report(items[:min(lib.so100o_items_count(), len(items))])
     n = lib.so100o_stats_count()
     assert n == steps * nenv * per_step, (n, steps * nenv * per_step)
     st = buf[:n].reshape(steps, nenv, per_step, 5)[:, :, :m.nsubstep]   # the substeps' position stages
@@ -65,6 +70,15 @@ def main():
     top = np.argsort(sc.ravel())[-max(1, sc.size // 100):]
     print(f"slowest-1% wave-steps by candidates: candidates {sc.ravel()[top].mean():.1f}, overlaps {so.ravel()[top].mean():.1f} "
           f"per step (10 substeps); all: {sc.mean():.2f} / {so.mean():.2f}")
+
+
+def item_report(items):
+    gi, ei, hit = items[:, 0], items[:, 1], items[:, 3]
+    ov = ei > 0
+    print(f"{len(items)} narrowphase items: GJK iterations p50/p90/p99/max {np.percentile(gi, [50, 90, 99, 100])}, "
+          f"EPA iterations (overlapping items) p50/p90/p99/max {np.percentile(ei[ov], [50, 90, 99, 100]) if ov.any() else '-'}")
+    print("  GJK iteration histogram:", np.bincount(gi, minlength=8)[:51].tolist())
+    print("  EPA iteration histogram:", np.bincount(ei[ov], minlength=8)[:51].tolist() if ov.any() else [])
 
 
 if __name__ == "__main__":
