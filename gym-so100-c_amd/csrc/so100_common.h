@@ -100,13 +100,10 @@ DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 // |y| = r (As = D A D, D = diag(mu0, mu0, mu1)).  In the eigenbasis of As (precomputed per substep,
 // with P = Q' D and 1/lam) y_i(la) = c_i / (lam_i + la) with c = -P b, so an iterate costs three
 // reciprocals, and x = D Q w = P' w.
-// Root finding: MuJoCo runs Newton on |y|^2 - r^2 from la = 0, which on this 1/la^2-shaped function
-// advances la by at most x1.5 per step while far from the root (3.5-7 steps per contact-sweep on
-// sliding grasp contacts).  We solve the same equation with Newton on 1/|y(la)| - 1/r (the trust-region
-// secular equation: near-linear and concave in la, exact for one active term), started from the lower
-// bound la0 = max(0, |c|/r - max lam) <= la*: from the left it converges monotonically to the same root,
-// with MuJoCo's exit tests (val < 1e-10, delta < 1e-10) plus an fp32 step test.  1-2 steps typical.
-// Returns the number of Newton steps taken (diagnostics).
+// Root finding: MuJoCo's Newton on |y|^2 - r^2 from la = 0 (its 20-step cap included, so an unconverged
+// search stops where MuJoCo's does).  -DSO100_QCQP_SECULAR keeps rounds 1-2's variant for A/B: Newton on
+// 1/|y(la)| - 1/r (the trust-region secular equation) from the lower bound max(0, |c|/r - max lam), 1-2 steps,
+// converged where MuJoCo stops at its cap.  Returns the number of Newton steps taken.
 DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* laminv, const float* b, float r,
                   bool live = true) {
   int nit = 0;

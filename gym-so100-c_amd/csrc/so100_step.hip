@@ -966,6 +966,18 @@ DEV void sup_sel(MprSup& d, const MprSup& s, bool w) {
   d.id = w ? s.id : d.id;
 }
 
+// A pointer read from the model (hull_cand, hull_blk) is generic to the compiler, so its loads were flat loads,
+// which also count on lgkmcnt: every wait for them drained the LDS traffic too.  ld_global4 makes them global.
+// (Device pass only: address spaces do not exist in the host pass of this translation unit.)
+typedef float f4v __attribute__((ext_vector_type(4)));
+DEV float4 ld_global4(const float4* p, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const f4v v = ((const __attribute__((address_space(1))) f4v*)(const void*)p)[i];
+  return make_float4(v.x, v.y, v.z, v.w);
+#else
+  return p[i];
+#endif
+}
 // a vertex's support score n . v with one fixed rounding (explicit FMAs): the cell block, the cell list and the
 // whole-hull scan must score a vertex bitwise alike, so that near-ties resolve alike (the fused and split paths
 // use different ones and are bitwise equal)
@@ -999,7 +1011,7 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
       const int face = 2 * (fx ? 0 : fy ? 1 : 2) + (na >= 0.f ? 0 : 1);
       const int cell = k * SO100_HULL_NCELL + (face * SO100_HULL_CELLG + cu) * SO100_HULL_CELLG + cv;
       // the cell entry and the lane's candidate of the cell's block, loaded together (one memory latency)
-      const float4 cb = reinterpret_cast<const float4*>(m->hull_blk)[(size_t)cell * kCellBlk + lane];
+      const float4 cb = ld_global4(reinterpret_cast<const float4*>(m->hull_blk), (size_t)cell * kCellBlk + lane);
       e = m->hull_cells[cell];
       const int cn = (int)(e & 255u);
       if (cn > 0 && cn <= kCellBlk) {
@@ -1014,8 +1026,8 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
     if (cc > 0) {
       const float4* __restrict__ cand = reinterpret_cast<const float4*>(m->hull_cand) + (e >> 8);
       for (int base = lane; base < cc; base += 2 * kLanes) {
-        const float4 c0 = cand[base];
-        const float4 c1 = cand[min(base + kLanes, cc - 1)];
+        const float4 c0 = ld_global4(cand, base);
+        const float4 c1 = ld_global4(cand, min(base + kLanes, cc - 1));
         const float s0c = sup_score(n0, n1, n2, c0.x, c0.y, c0.z);
         if (s0c > best) { best = s0c; bi = __float_as_int(c0.w); bx = c0.x; by = c0.y; bz = c0.z; }
         const float s1c = sup_score(n0, n1, n2, c1.x, c1.y, c1.z);

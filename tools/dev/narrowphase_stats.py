@@ -77,6 +77,10 @@ def item_report(items):
     ov = ei > 0
     print(f"{len(items)} narrowphase items: GJK iterations p50/p90/p99/max {np.percentile(gi, [50, 90, 99, 100])}, "
           f"EPA iterations (overlapping items) p50/p90/p99/max {np.percentile(ei[ov], [50, 90, 99, 100]) if ov.any() else '-'}")
+    sep = items[:, 2] > 0
+    print(f"  box-axis SAT (hull's exact projection on the box's 3 face axes) separates {sep.mean():.3f} of all items, "
+          f"{sep[~ov].mean() if (~ov).any() else 0:.3f} of the GJK-separated ones (GJK iterations saved "
+          f"{gi[sep].sum() / max(gi.sum(), 1):.3f}); overlapping items it separates: {int((sep & ov).sum())}")
     print("  GJK iteration histogram:", np.bincount(gi, minlength=8)[:51].tolist())
     print("  EPA iteration histogram:", np.bincount(ei[ov], minlength=8)[:51].tolist() if ov.any() else [])
 

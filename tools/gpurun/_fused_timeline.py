@@ -53,3 +53,10 @@ for name, idx in (("fastest 10%", order[: len(order) // 10]), ("median 10%", ord
     print(f"  {name:12s} dur {dur[idx].mean():7.1f} us  asm {asm[idx].mean()/1e3:6.0f}k newton {newt[idx].mean()/1e3:6.0f}k "
           f"epi {fin[idx].mean()/1e3:5.0f}k  ncon(last) {ncon[idx].mean():4.1f}  iters(last) {iters[idx].mean():4.1f}")
 print("start-time quantiles us:", np.percentile(s, [0, 25, 50, 75, 90, 100]).round(1).tolist())
+# the slowest waves one by one: per-phase kcycles and each env's last-substep contacts / Newton iterations / pairs
+dbg_all = env.debug.cpu().numpy()
+for w in np.argsort(dur)[-5:][::-1]:
+    envs = range(4 * w, min(4 * w + 4, n))
+    desc = "; ".join(f"env {e}: ncon {int(dbg_all[e, 0])} it {int(dbg_all[e, 1])} pairs "
+                     f"{[int(p) for p in dbg_all[e, 48:48 + int(dbg_all[e, 0])]]}" for e in envs)
+    print(f"wave {w}: {dur[w]:.0f} us, asm {asm[w] / 1e3:.0f}k newton {newt[w] / 1e3:.0f}k | {desc}")
