@@ -32,6 +32,9 @@ namespace so100 {
 #define SO100_JREG 8
 #endif
 constexpr int kJReg = SO100_JREG;       // contacts whose J rows stay in VGPRs
+#ifndef SO100_LS_CONE_DIR
+#define SO100_LS_CONE_DIR 1             // line search: cone_dir (0: cone_eval + products, A/B)
+#endif
 constexpr int kJLds = kMaxCon - kJReg;  // the others' J rows: LDS [kJLds][SO100_NV] float4 per env
 struct NewtonRows {
   float qs, warm, fr_aref;              // dof lanes: qacc_smooth, warmstart, frictionloss aref
@@ -85,6 +88,30 @@ DEV void cone_eval(const float* jar, const float* D, float mu, float fr0, float 
       if (k >= 1) v += c2 * fr[k] * fr[l] * ((k == l ? invT : 0.f) - U[k] * U[l] * invT3);
       h[q] = v;
     }
+}
+// The line search's view of a contact block: the cost's first and second derivatives at jar along v, as
+// -f . v and v' H v, without forming H (in the middle zone H is rank one plus the friction rows' curvature, so
+// v' H v = Dm (g.v)^2 + c2 (|fr v|^2 / T - (sum U_k fr_k v_k)^2 / T^3)): the same zones and the same values as
+// cone_eval followed by f . v and v' sym4(h, v), in a third of the dependent operations.
+DEV void cone_dir(const float* jar, const float* v, const float* D, float mu, float fr0, float fr1, float& fv,
+                  float& vhv) {
+  const float U1 = jar[1] * fr0, U2 = jar[2] * fr0, U3 = jar[3] * fr1;
+  const float T = sqrtf(U1 * U1 + U2 * U2 + U3 * U3);
+  const float N = jar[0] * mu;
+  fv = 0.f;
+  vhv = 0.f;
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) return;                          // top zone: no force
+  if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {                            // bottom zone: quadratic
+#pragma unroll
+    for (int k = 0; k < 4; k++) { fv -= D[k] * jar[k] * v[k]; vhv += D[k] * v[k] * v[k]; }
+    return;
+  }
+  const float Dm = D[0] / (mu * mu * (1.f + mu * mu)), NmT = N - mu * T, invT = 1.f / T;
+  const float w1 = fr0 * v[1], w2 = fr0 * v[2], w3 = fr1 * v[3];
+  const float s1 = w1 * w1 + w2 * w2 + w3 * w3, s2 = U1 * w1 + U2 * w2 + U3 * w3;
+  const float gv = mu * v[0] - mu * invT * s2;                               // g . v
+  fv = -Dm * NmT * gv;
+  vhv = Dm * gv * gv - Dm * NmT * mu * (invT * s1 - invT * invT * invT * s2 * s2);
 }
 // frictionloss row (Huber) and joint-limit row (one-sided quadratic) at jar x
 DEV void fr_eval(float x, float fl, float R, float D, float& cost, float& f, float& h) {
@@ -433,13 +460,20 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           lim_eval(jlim + al * slim, lim_on, lim_D, cc, f, h);
           l1 -= f * slim; l2 += h * slim * slim;
           if (own) {
-            float x[4], fcc[4], hcc[10];
+            float x[4], fv, vhv;
 #pragma unroll
             for (int k = 0; k < 4; k++) x[k] = jc[k] + al * jsc[k];
+#if SO100_LS_CONE_DIR
+            cone_dir(x, jsc, c_D, c_mu, c_fr0, c_fr1, fv, vhv);
+#else
+            float fcc[4], hcc[10];
             cone_eval(x, c_D, c_mu, c_fr0, c_fr1, cc, fcc, hcc);
             const float4 v = make_float4(jsc[0], jsc[1], jsc[2], jsc[3]);
-            l1 -= fcc[0] * jsc[0] + fcc[1] * jsc[1] + fcc[2] * jsc[2] + fcc[3] * jsc[3];
-            l2 += dot4(v, sym4(hcc, v));
+            fv = fcc[0] * jsc[0] + fcc[1] * jsc[1] + fcc[2] * jsc[2] + fcc[3] * jsc[3];
+            vhv = dot4(v, sym4(hcc, v));
+#endif
+            l1 -= fv;
+            l2 += vhv;
           }
           d1 = rowsum16(l1) + A1 + al * A2;
           d2 = rowsum16(l2) + A2;
