@@ -47,15 +47,23 @@ struct NewtonRows {
   float4 c_aref, c_R, c_mu;             // lane c < ncon: contact c's aref, R, (cone mu, friction0, friction1)
 };
 
+// The solve's square roots and reciprocals on its serial chains: the hardware v_sqrt / v_rcp (1 ulp) instead of
+// the IEEE sequences (a dozen dependent instructions each); SO100_NEWTON_IEEE=1 keeps the IEEE forms (A/B).
+#ifndef SO100_NEWTON_IEEE
+#define SO100_NEWTON_IEEE 0
+#endif
+DEV float nsqrt(float x) { return SO100_NEWTON_IEEE ? sqrtf(x) : __builtin_amdgcn_sqrtf(x); }
+DEV float nrcp(float x) { return SO100_NEWTON_IEEE ? 1.f / x : __builtin_amdgcn_rcpf(x); }
+
 // MuJoCo mj_constraintUpdate (primal), elliptic contact block at jar: cost, force f = -dc/djar, and the
 // cost Hessian (upper triangle 00 01 02 03 11 12 13 22 23 33).  Oracle block_eval.
-DEV void cone_eval(const float* jar, const float* D, float mu, float fr0, float fr1, float& cost, float* f,
+DEV void cone_eval(const float* jar, const float* D, float Dm, float mu, float fr0, float fr1, float& cost, float* f,
                    float* h) {
   const float fr[4] = {mu, fr0, fr0, fr1};
   float U[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) U[k] = jar[k] * fr[k];
-  const float T = sqrtf(U[1] * U[1] + U[2] * U[2] + U[3] * U[3]);
+  const float T = nsqrt(U[1] * U[1] + U[2] * U[2] + U[3] * U[3]);
   const float N = U[0];
   cost = 0.f;
 #pragma unroll
@@ -70,7 +78,7 @@ DEV void cone_eval(const float* jar, const float* D, float mu, float fr0, float 
     return;
   }
   // middle zone: c = 1/2 Dm (N - mu T)^2, g = d(N - mu T)/djar
-  const float Dm = D[0] / (mu * mu * (1.f + mu * mu)), NmT = N - mu * T, invT = 1.f / T;
+  const float NmT = N - mu * T, invT = nrcp(T);
   float g[4];
   g[0] = mu;
 #pragma unroll
@@ -93,10 +101,10 @@ DEV void cone_eval(const float* jar, const float* D, float mu, float fr0, float 
 // -f . v and v' H v, without forming H (in the middle zone H is rank one plus the friction rows' curvature, so
 // v' H v = Dm (g.v)^2 + c2 (|fr v|^2 / T - (sum U_k fr_k v_k)^2 / T^3)): the same zones and the same values as
 // cone_eval followed by f . v and v' sym4(h, v), in a third of the dependent operations.
-DEV void cone_dir(const float* jar, const float* v, const float* D, float mu, float fr0, float fr1, float& fv,
-                  float& vhv) {
+DEV void cone_dir(const float* jar, const float* v, const float* D, float Dm, float mu, float fr0, float fr1,
+                  float& fv, float& vhv) {
   const float U1 = jar[1] * fr0, U2 = jar[2] * fr0, U3 = jar[3] * fr1;
-  const float T = sqrtf(U1 * U1 + U2 * U2 + U3 * U3);
+  const float T = nsqrt(U1 * U1 + U2 * U2 + U3 * U3);
   const float N = jar[0] * mu;
   fv = 0.f;
   vhv = 0.f;
@@ -106,7 +114,7 @@ DEV void cone_dir(const float* jar, const float* v, const float* D, float mu, fl
     for (int k = 0; k < 4; k++) { fv -= D[k] * jar[k] * v[k]; vhv += D[k] * v[k] * v[k]; }
     return;
   }
-  const float Dm = D[0] / (mu * mu * (1.f + mu * mu)), NmT = N - mu * T, invT = 1.f / T;
+  const float NmT = N - mu * T, invT = nrcp(T);
   const float w1 = fr0 * v[1], w2 = fr0 * v[2], w3 = fr1 * v[3];
   const float s1 = w1 * w1 + w2 * w2 + w3 * w3, s2 = U1 * w1 + U2 * w2 + U3 * w3;
   const float gv = mu * v[0] - mu * invT * s2;                               // g . v
@@ -315,6 +323,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     c_D[0] = 1.f / r.c_R.x; c_D[1] = 1.f / r.c_R.y; c_D[2] = 1.f / r.c_R.z; c_D[3] = 1.f / r.c_R.w;
     c_mu = r.c_mu.x; c_fr0 = r.c_mu.y; c_fr1 = r.c_mu.z;
   }
+  const float c_Dm = c_D[0] / (c_mu * c_mu * (1.f + c_mu * c_mu));   // the middle zone's Dm (oracle block_eval)
 
   // cost of the rows this lane owns at (frictionloss / limit jar of its dof, contact jar)
   auto rows_cost = [&](float xfr, float xlim, const float* xc) {
@@ -322,7 +331,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     if (dof) { fr_eval(xfr, fr_fl, fr_R, fr_D, cc, f, h); cost += cc; }
     lim_eval(xlim, lim_on, lim_D, cc, f, h);
     cost += cc;
-    if (own) { cone_eval(xc, c_D, c_mu, c_fr0, c_fr1, cc, fc, hc); cost += cc; }
+    if (own) { cone_eval(xc, c_D, c_Dm, c_mu, c_fr0, c_fr1, cc, fc, hc); cost += cc; }
     return cost;
   };
 
@@ -364,7 +373,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
       float c0, f_fr = 0.f, h_fr = 0.f, f_lim, h_lim, fc[4], hc[10];
       if (dof) fr_eval(jfr, fr_fl, fr_R, fr_D, c0, f_fr, h_fr);
       lim_eval(jlim, lim_on, lim_D, c0, f_lim, h_lim);
-      cone_eval(jc, c_D, c_mu, c_fr0, c_fr1, c0, fc, hc);
+      cone_eval(jc, c_D, c_Dm, c_mu, c_fr0, c_fr1, c0, fc, hc);
       if (!own) {
 #pragma unroll
         for (int k = 0; k < 4; k++) fc[k] = 0.f;
@@ -380,7 +389,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
       for (int c = kJReg; c < ncon_max; c++)
         grad -= dot4(jx_own(r, c, lane), shfl_row4(make_float4(fc[0], fc[1], fc[2], fc[3]), c));
       grad = dof ? grad : 0.f;
-      const float gn = sqrtf(rowsum16(grad * grad));
+      const float gn = nsqrt(rowsum16(grad * grad));
       STAMP(2);
       if (scale * gn < tolerance) {
         done = true;
@@ -464,10 +473,10 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 #pragma unroll
             for (int k = 0; k < 4; k++) x[k] = jc[k] + al * jsc[k];
 #if SO100_LS_CONE_DIR
-            cone_dir(x, jsc, c_D, c_mu, c_fr0, c_fr1, fv, vhv);
+            cone_dir(x, jsc, c_D, c_Dm, c_mu, c_fr0, c_fr1, fv, vhv);
 #else
             float fcc[4], hcc[10];
-            cone_eval(x, c_D, c_mu, c_fr0, c_fr1, cc, fcc, hcc);
+            cone_eval(x, c_D, c_Dm, c_mu, c_fr0, c_fr1, cc, fcc, hcc);
             const float4 v = make_float4(jsc[0], jsc[1], jsc[2], jsc[3]);
             fv = fcc[0] * jsc[0] + fcc[1] * jsc[1] + fcc[2] * jsc[2] + fcc[3] * jsc[3];
             vhv = dot4(v, sym4(hcc, v));
@@ -498,7 +507,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             derivs(alpha, d1, d2);
             if (fabsf(d1) <= tol_ls) break;
             if (d1 < 0.f) lo = alpha; else hi = alpha;
-            float nxt = d2 > 0.f ? alpha - d1 / d2 : -1.f;
+            float nxt = d2 > 0.f ? alpha - d1 * nrcp(d2) : -1.f;
             if (hi >= 0.f) { if (!(nxt > lo && nxt < hi)) nxt = 0.5f * (lo + hi); }
             else if (!(nxt > lo)) nxt = 2.f * alpha;
             if (nxt == alpha) break;
@@ -540,7 +549,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 #endif
     float cc, f_fr, h, fc[4], hc[10];
     fr_eval(jfr, fr_fl, fr_R, fr_D, cc, f_fr, h);
-    cone_eval(jc, c_D, c_mu, c_fr0, c_fr1, cc, fc, hc);
+    cone_eval(jc, c_D, c_Dm, c_mu, c_fr0, c_fr1, cc, fc, hc);
     diag.f_fr = f_fr;
     diag.f_n = own ? fc[0] : 0.f;
 #pragma unroll

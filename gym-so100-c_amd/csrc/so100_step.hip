@@ -1305,7 +1305,8 @@ constexpr int kEpaMaxV = 24, kEpaMaxF = 44, kEpaMaxE = 48;   // oracle EPA_MAXV 
 // Diagnostic build only (-DSO100_EPA_STAMPS, tools/dev/epa_stamps.py): shader cycles of the convex collider's
 // phases summed over the rows (lane 0) into a device counter array read by so100_dev_epa_cycles.
 #ifdef SO100_EPA_STAMPS
-__device__ unsigned long long so100_epa_cyc[8];   // GJK, EPA, items, EPA items, EPA iters, support, horizon+facets, scan
+__device__ unsigned long long so100_epa_cyc[12];  // GJK, EPA, items, EPA items, EPA iters, support, horizon+facets, scan,
+                                                   // then inside the horizon: visibility + twins, masks, facets
 #define ESTAMP_T() __builtin_amdgcn_s_memtime()
 #define ESTAMP_ADD(k, v) do { if (lane == 0) atomicAdd(&so100_epa_cyc[k], (unsigned long long)(v)); } while (0)
 #else
@@ -1550,6 +1551,7 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
     // the horizon: the edges (a, b) of the visible facets whose twin (b, a) lies on no visible facet, in
     // (slot, edge) order (oracle epa_penetration).  Each lane holds its visible slots' 3 edges; one pass over
     // the visible facets (their vertex triples broadcast from LDS) marks the lanes' edges that have a twin.
+    const unsigned long long eh0 = ESTAMP_T();
     uint32_t twin = 0u;                          // bit 3 s3 + k: edge k of the lane's slot s3 has a twin
     for (uint64_t vm = vis; vm != 0ull; vm &= vm - 1ull) {
       const uint32_t g = P.fv[__builtin_ctzll(vm)];
@@ -1575,6 +1577,8 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
         hm[s3][k] = (uint32_t)((__ballot(mv[s3] && !((twin >> (3 * s3 + k)) & 1u)) >> (grp * kLanes)) & 0xFFFFull);
         ne += __popc(hm[s3][k]);
       }
+    const unsigned long long eh1 = ESTAMP_T();
+    ESTAMP_ADD(8, eh1 - eh0);
     if (ne > kEpaMaxE) break;                      // the horizon does not fit: stop at the nearest facet
     alive &= ~vis;
     const int iw = nv;
@@ -1583,6 +1587,8 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
     nv++;
     // the new facets (a, b, w), one per horizon edge, built by the lanes that own the edges: the j-th
     // non-degenerate one (in horizon order) takes the j-th lowest free slot; slots run out -> the rest none
+    const unsigned long long eh2 = ESTAMP_T();
+    ESTAMP_ADD(9, eh2 - eh1);
     const uint64_t freem = ~alive & ((1ull << kEpaMaxF) - 1ull);
     const int nfree = __popcll(freem);
     const uint32_t below = (1u << lane) - 1u;
@@ -1656,7 +1662,9 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
       }
       alive |= taken;
     }
-    ESTAMP_ADD(6, ESTAMP_T() - et2);
+    const unsigned long long eh3 = ESTAMP_T();
+    ESTAMP_ADD(10, eh3 - eh2);
+    ESTAMP_ADD(6, eh3 - et2);
   }
   if (best < 0) return false;
   depth = bd;
@@ -3346,9 +3354,9 @@ __global__ void so100_contact_count_kernel(const float* __restrict__ hdr, int n,
 #ifdef SO100_EPA_STAMPS
 }  // namespace so100
 extern "C" int so100_dev_epa_cycles(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(so100::so100_epa_cyc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(so100::so100_epa_cyc), sizeof(unsigned long long) * 12) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[12] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(so100::so100_epa_cyc), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

@@ -755,7 +755,14 @@ def test_mpr_contact_parity(solver, convex, oracle64, oracle32):
     assert np.median(r.qv) <= 2 * r.floor("qv", 0.5) + 1e-5
     assert np.mean(r.qv > 1e-4) <= 1.5 * max(np.mean(r.fqv > 1e-4), np.mean(r.pqv > 1e-4)) + 0.05
     assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
-    _force_bars(r)
+    if convex == "epa":
+        _force_bars(r)
+    else:
+        # MPR's portal choice flips on a rounding, so which tenth of the contacts lands in the force tail changes
+        # with any 1-ulp change of the trajectory: its tail is compared by mass, as qvel's above
+        assert np.median(r.force) <= 2 * r.floor("force", 0.5) + 1e-6
+        assert np.mean(r.force > 1e-4) <= 1.5 * max(np.mean(r.fforce > 1e-4), np.mean(r.pforce > 1e-4)) + 0.05
+        assert np.median(r.qa) <= 2 * r.floor("qa", 0.5) + 1e-6
     assert r.drop_gpu.sum() == 0
 
 
