@@ -632,9 +632,9 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
       float n[3] = {0, 0, 0};
       n[i1] = -R[3 * i2 + j];
       n[i2] = R[3 * i1 + j];
-      float l = sqrtf(n[i1] * n[i1] + n[i2] * n[i2]);
-      if (l < 1e-5f) continue;
-      const float linv = 1.0f / l;
+      const float l2 = n[i1] * n[i1] + n[i2] * n[i2];
+      if (l2 < 1e-10f) continue;                   // |n| < 1e-5
+      const float linv = __builtin_amdgcn_rsqf(l2);   // v_rsq (1 ulp): one instruction on the env's chain
       float e = pp[i2] * R[3 * i1 + j] - pp[i1] * R[3 * i2 + j];
       float ex = A[i1] * Q[3 * i2 + j] + A[i2] * Q[3 * i1 + j] + B[j1] * Q[3 * i + j2] + B[j2] * Q[3 * i + j1];
       float s = (fabsf(e) - ex) * linv;
@@ -1412,9 +1412,9 @@ DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, 
   if (ccd_zero(dot3(d, d))) d[0] = 1.f;
   int n = 0;
   for (int it = 0; it < kMprIters; it++) {
-    const float nd = sqrtf(dot3(d, d));
-    if (ccd_zero(nd)) return false;
-    const float ind = 1.f / nd;                     // one IEEE division (oracle gjk)
+    const float dd = dot3(d, d);
+    if (dd < kCcdEps * kCcdEps) return false;       // ccd_zero(|d|)
+    const float ind = __builtin_amdgcn_rsqf(dd);    // 1 / |d| (oracle gjk: one division), v_rsq
     const float du[3] = {d[0] * ind, d[1] * ind, d[2] * ind};
     MprSup as;
     mpr_support(m, o, du, as, lane);
@@ -1438,9 +1438,9 @@ DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const float* A, co
   sub3(ab, B, A);
   sub3(ac, C, A);
   cross3(n, ab, ac);
-  const float l = sqrtf(dot3(n, n));
-  if (ccd_zero(l)) return false;
-  const float il = 1.f / l;                       // one IEEE division (oracle epa_face_set)
+  const float l2 = dot3(n, n);
+  if (l2 < kCcdEps * kCcdEps) return false;       // ccd_zero(|n|)
+  const float il = __builtin_amdgcn_rsqf(l2);     // 1 / |n| (oracle epa_face_set: one division), v_rsq
   n[0] = n[0] * il; n[1] = n[1] * il; n[2] = n[2] * il;
   P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A));
   P.fv[f] = (uint32_t)a | (uint32_t)b << 5 | (uint32_t)c << 10;
@@ -1619,9 +1619,9 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
           sub3(ab, B, A);
           sub3(ac, w.v, A);
           cross3(n, ab, ac);
-          const float l = sqrtf(dot3(n, n));
-          if (!ccd_zero(l)) {
-            const float il = 1.f / l;
+          const float l2 = dot3(n, n);
+          if (!(l2 < kCcdEps * kCcdEps)) {
+            const float il = __builtin_amdgcn_rsqf(l2);
             n[0] = n[0] * il; n[1] = n[1] * il; n[2] = n[2] * il;
             fpl[k] = make_float4(n[0], n[1], n[2], dot3(n, A));
             ok |= 1u << k;
@@ -1983,17 +1983,18 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
   return grp == 0 ? f0 : grp == 1 ? f1 : grp == 2 ? f2 : f3;
 }
 
+// the contact frame (oracle make_frame; MuJoCo mju_makeFrame): the two normalisations by v_rsq (1 ulp)
 DEV void make_frame(float* f) {
   float* n = f;
   float* t1 = f + 3;
-  float nn = sqrtf(dot3(n, n));
-  n[0] /= nn; n[1] /= nn; n[2] /= nn;
+  const float in = __builtin_amdgcn_rsqf(dot3(n, n));
+  n[0] *= in; n[1] *= in; n[2] *= in;
   if (fabsf(n[1]) < 0.5f) { t1[0] = 0.f; t1[1] = 1.f; t1[2] = 0.f; }
   else { t1[0] = 0.f; t1[1] = 0.f; t1[2] = 1.f; }
   float pr = dot3(n, t1);
   t1[0] -= pr * n[0]; t1[1] -= pr * n[1]; t1[2] -= pr * n[2];
-  float tn = sqrtf(dot3(t1, t1));
-  t1[0] /= tn; t1[1] /= tn; t1[2] /= tn;
+  const float it = __builtin_amdgcn_rsqf(dot3(t1, t1));
+  t1[0] *= it; t1[1] *= it; t1[2] *= it;
   cross3(f + 6, n, t1);
 }
 
