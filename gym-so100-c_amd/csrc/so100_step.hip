@@ -58,11 +58,13 @@ DEV float getimpedance(const float* solimp, float pos, float margin) {
   float mid = fminf(fmaxf(solimp[3], kMinImp), kMaxImp);
   float power = fmaxf(solimp[4], 1.0f);
   if (dmin == dmax || width <= kMinVal) return 0.5f * (dmin + dmax);
-  float x = fabsf((pos - margin) / width);
+  float x = fabsf((pos - margin) * __builtin_amdgcn_rcpf(width));
   if (x >= 1.0f) return dmax;
   if (x <= 0.0f) return dmin;
   float y;
   if (power == 1.0f) y = x;
+  else if (power == 2.0f) y = x <= mid ? x * x * __builtin_amdgcn_rcpf(mid)          // the model's solimp power
+                                       : 1.0f - (1.0f - x) * (1.0f - x) * __builtin_amdgcn_rcpf(1.0f - mid);
   else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.0f);
   else y = 1.0f - powf(1.0f - x, power) / powf(1.0f - mid, power - 1.0f);
   return dmin + y * (dmax - dmin);
@@ -409,8 +411,9 @@ DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, f
       float sdiag = S.M[j][j];
 #pragma unroll
       for (int k = 0; k < j; k++) sdiag -= L[j][k] * L[j][k];
-      L[j][j] = sqrtf(fmaxf(sdiag, kMinVal));
-      Linv[j] = 1.0f / L[j][j];
+      const float sd = fmaxf(sdiag, kMinVal);
+      Linv[j] = __builtin_amdgcn_rsqf(sd);          // 1 / L_jj by v_rsq (1 ulp), L_jj = sd / L_jj
+      L[j][j] = sd * Linv[j];
 #pragma unroll
       for (int i = j + 1; i < 6; i++) {
         float t = S.M[i][j];
@@ -2175,7 +2178,8 @@ DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_
     if (nw > kMinVal) {
       float s, c;
       sincosf(0.5f * h * nw, &s, &c);
-      float qr[4] = {c, w[0] / nw * s, w[1] / nw * s, w[2] / nw * s};
+      const float rn = __builtin_amdgcn_rcpf(nw);
+      float qr[4] = {c, w[0] * rn * s, w[1] * rn * s, w[2] * rn * s};
       quat_mul(q, q, qr);
     }
     quat_normalize(q);
@@ -2501,7 +2505,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       const float jar = warm_r - fr_aref;
       if (jar <= -fr_R * fr_fl) fr_f = fr_fl;
       else if (jar >= fr_R * fr_fl) fr_f = -fr_fl;
-      else fr_f = -jar / fr_R;
+      else fr_f = -jar * __builtin_amdgcn_rcpf(fr_R);
       if (!has_fr) fr_f = 0.f;
     }
     float mdiag = invmc;
@@ -2516,10 +2520,10 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       else if (dhi < 0.f) { lim_on = true; lim_s = -1.f; dist = dhi; }
       if (lim_on) {
         const float imp = getimpedance(m->lim_solimp, dist, 0.f);
-        lim_R = fmaxf(kMinVal, (1.f - imp) / imp * m->lim_invw[lane]);
+        lim_R = fmaxf(kMinVal, (1.f - imp) * __builtin_amdgcn_rcpf(imp) * m->lim_invw[lane]);
         lim_aref = -m->lim_B * (lim_s * qvel_r) - m->lim_K * imp * dist;
         const float jar = lim_s * warm_r - lim_aref;
-        lim_f = jar < 0.f ? -jar / lim_R : 0.f;
+        lim_f = jar < 0.f ? -jar * __builtin_amdgcn_rcpf(lim_R) : 0.f;
       }
     }
     const uint64_t lim_mask = __ballot(lim_on && valid);
@@ -2581,13 +2585,14 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
         const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
         float R[4];
-        R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
-        R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
+        // (reciprocals by v_rcp, the square root by v_sqrt: 1 ulp, on the contact's setup chain)
+        R[0] = fmaxf(kMinVal, (1.f - imp) * __builtin_amdgcn_rcpf(imp) * m->pair_tran[p]);
+        R[1] = R[0] * mu0 * mu0 * __builtin_amdgcn_rcpf(mu0 * mu0 * m->impratio);
         R[2] = R[1];
-        R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
+        R[3] = R[0] * mu0 * mu0 * __builtin_amdgcn_rcpf(mu1 * mu1 * m->impratio);
         nr.c_aref = make_float4(-Bd * cVn[0] - K * imp * (dist - m->pair_margin[p]), -Bd * cVn[1], -Bd * cVn[2], -Bd * cVn[3]);
         nr.c_R = make_float4(R[0], R[1], R[2], R[3]);
-        nr.c_mu = make_float4(mu0 * sqrtf(R[1] / R[0]), mu0, mu1, 0.f);
+        nr.c_mu = make_float4(mu0 * __builtin_amdgcn_sqrtf(R[1] * __builtin_amdgcn_rcpf(R[0])), mu0, mu1, 0.f);
       }
       SSTAMP(4);
       nr.qs = lane < SO100_NV ? qs_r : 0.f;
