@@ -8,11 +8,11 @@
 One "step" = one batched env step of every env on every GPU: action prologue, 10 physics substeps
 (kinematics, CRBA/RNE, box-box / hull / MPR contacts, the constraint solve -- primal Newton, MuJoCo's
 default and so the reference's, or --solver pgs -- and semi-implicit Euler), the final position stage,
-reward/obs epilogue, TimeLimit + in-kernel auto-reset.  With Newton (the default) at up to 49,152 envs per GPU
-(the 2-, 4- and 8-GPU shards) the step is ONE fused kernel launch (so100_fused_kernel: every wave runs its 4
-envs through all substeps with the state in registers; waves launched heavy-first by their previous step's
-cost); at 65,536 envs on one GPU, with PGS, or with SO100_FUSED=0 it is 21 launches per env chunk (per
-substep a stage kernel and a solver kernel, then the final stage kernel; 4 chunks on concurrent streams).
+reward/obs epilogue, TimeLimit + in-kernel auto-reset.  With Newton (the default) the step is ONE fused kernel
+launch at every shard size (so100_fused_kernel: every wave runs its 4 envs through all substeps with the state in
+registers; waves launched heavy-first by their previous step's cost); with PGS or SO100_FUSED=0 it is 21 launches
+per env chunk (per substep a stage kernel and a solver kernel, then the final stage kernel; 4 chunks on
+concurrent streams).
 Envs are sharded contiguously (global ids drive the seeds); there is no collective on the data path:
 only the barrier + max-over-ranks timing reduction around the timed region.
 Rank 0 prints ONE JSON line.  See DESIGN.md §6 for the roofline bytes and the CPU baseline.

@@ -108,10 +108,10 @@ static void graph_free(so100_env* env) {
 }
 
 // The fused kernel implements the Newton solver only: PGS always takes the split launches.  Auto mode runs
-// fused up to fused_max envs per GPU (SO100_FUSED_MAX): the fused step is faster at the 2-, 4- and 8-GPU
-// shards (+7 % at 32,768 envs, +37 % at 8,192), the two tie at 49,152 and the split step is 2 % faster at
-// 65,536, where its 21 short launches pack a full chip better (same box).
-constexpr int kFusedAutoMax = 49152;
+// fused up to fused_max envs per GPU (SO100_FUSED_MAX; default: every size): round 3 measured the fused step
+// faster at every shard size of the benchmark, 65,536 envs included (22.0 M vs 21.4 M env steps/s, +20 % at
+// 32,768, +41 % at 16,384).
+constexpr int kFusedAutoMax = 1 << 30;
 static bool step_is_fused(const so100_env* env) {
   if (env->solver != SO100_SOLVER_NEWTON) return false;
   return env->fused < 0 ? env->n <= env->fused_max : env->fused != 0;

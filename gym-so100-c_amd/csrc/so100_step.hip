@@ -2994,6 +2994,9 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 #ifndef SO100_FUSED_WAVES
 #define SO100_FUSED_WAVES 3
 #endif
+#ifndef SO100_FUSED_RELOAD
+#define SO100_FUSED_RELOAD 0
+#endif
 // The whole env step in one launch (Newton solver, the default): each wave runs its 4 envs through the 10
 // substeps — Euler, assembly, the Newton solve with the rows handed over in registers (no HBM record) —
 // and the epilogue, with the state in registers throughout.  The split path's 21 launches end every
@@ -3076,8 +3079,20 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     }
 #endif
     NewtonRows nr;
-    assemble<SO100_SOLVER_NEWTON, true, kDebug>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale,
-                                                fscale, sub, nr);
+#if SO100_FUSED_RELOAD
+    // the env's DR scales re-read per substep (L2-hot, 8 B) instead of carried across the loop body's register
+    // peak (the 3-wave build spilled them with the other loop-carried values)
+    float ms = 1.f, fs = 1.f;
+    if ((args.flags & SO100_FLAG_DR) && args.b.dr_params) {
+      ms = args.b.dr_params[(size_t)e * 4 + 0];
+      fs = args.b.dr_params[(size_t)e * 4 + 1];
+    }
+    (void)mscale; (void)fscale;
+#else
+    const float ms = mscale, fs = fscale;
+#endif
+    assemble<SO100_SOLVER_NEWTON, true, kDebug>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, ms,
+                                                fs, sub, nr);
     TL_MARK(0);
     NewtonDiag diag;
     const bool dbg = kDebug && args.b.debug && sub == nsub - 1;
@@ -3099,7 +3114,16 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     const bool valid = env < args.n;
     EnvShared& sh = shm[grp];
     euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
-    final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+#if SO100_FUSED_RELOAD
+    // the step counters re-read (the prologue's values, not yet written) instead of carried across the loop
+    const int el = args.b.elapsed ? args.b.elapsed[e] : 0;
+    const uint32_t ep = args.b.episode ? args.b.episode[e] : 0u;
+    (void)elapsed0; (void)episode0;
+#else
+    const int el = elapsed0;
+    const uint32_t ep = episode0;
+#endif
+    final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, el, ep);
     if (valid && lane == 0 && args.b.ncon_dropped) args.b.ncon_dropped[env] = (uint32_t)sh.ndrop;
   }
   TL_MARK(2);

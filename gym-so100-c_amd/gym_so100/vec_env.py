@@ -397,8 +397,8 @@ class SO100VecEnv:
     @property
     def fused(self):
         """True when a step is one fused kernel launch (Newton solver); False: the split stage/solver
-        launches (always for PGS).  Set True / False to force a mode, None for auto (the default: fused up
-        to 49,152 envs per GPU, SO100_FUSED_MAX overrides; include/so100.h so100_set_step_mode)."""
+        launches (always for PGS).  Set True / False to force a mode, None for auto (the default: fused at
+        every size, SO100_FUSED_MAX=n splits above n envs; include/so100.h so100_set_step_mode)."""
         return bool(self.lib.so100_step_mode(self._handle))
 
     @fused.setter

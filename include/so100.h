@@ -126,7 +126,7 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
 /* Step mode (Newton solver): 1 = the whole env step as ONE fused kernel launch over all N envs, the
  * substep's constraint rows handed from the assembly to the solve in registers; 0 = the split path, per
  * substep a stage kernel and a solver kernel exchanging an HBM record (2 nsubstep + 1 launches per env
- * chunk); -1 = auto (default): fused for N <= 49,152 (SO100_FUSED_MAX overrides), split above.  Both give
+ * chunk); -1 = auto (default): fused at every N (SO100_FUSED_MAX=n: split above n).  Both give
  * the same results bit for bit.  The PGS solver always runs split.  so100_step_mode returns the mode in
  * effect (0/1).  In fused mode so100_profile_read reports the fused launches as the solver launches
  * (stage: 0) and so100_chunk_info reports 1 chunk of N envs. */

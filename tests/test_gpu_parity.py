@@ -463,8 +463,8 @@ def test_fused_step_matches_split(variant, task, dr):
 
 
 def test_step_mode_switch():
-    """PGS always runs split; auto mode (the default) runs fused up to 49,152 envs; the mode can be switched
-    between steps (Newton), and the contact counter reads the record of the mode that ran."""
+    """PGS always runs split; auto mode (the default) runs fused at every size (65,536 envs included); the mode
+    can be switched between steps (Newton), and the contact counter reads the record of the mode that ran."""
     from gym_so100 import SO100VecEnv
     big = SO100VecEnv(32768, device="cuda:0")
     assert big.fused and big.chunk_info() == (1, 32768)
@@ -472,7 +472,7 @@ def test_step_mode_switch():
     assert not big.fused and big.chunk_info()[0] == 4
     big.close()
     big = SO100VecEnv(65536, device="cuda:0")
-    assert not big.fused and big.chunk_info()[0] == 4
+    assert big.fused and big.chunk_info() == (1, 65536)
     big.close()
     pgs = SO100VecEnv(8, device="cuda:0", solver="pgs")
     assert not pgs.fused
@@ -1096,9 +1096,11 @@ def test_product_builds_bitwise(n):
     assert ncon.mean() > 2 and ncon.max() > 8 and mpr > 100 and resets >= n
 
 
-def test_config2_benched_split_full_size():
-    """configs[2] as bench.py times it on one GPU: 65,536 envs in one process run the split step (4 env
-    chunks on concurrent streams, auto mode) with auto-reset; 40 steps of random actions keep the state
+@pytest.mark.parametrize("fused", [True, False])
+def test_config2_benched_full_size(fused):
+    """configs[2] as bench.py times it on one GPU: 65,536 envs in one process, the fused step (auto mode, the
+    benched path) and the split step (4 env chunks on concurrent streams), with auto-reset; 40 steps of random
+    actions keep the state
     finite and the contract: unit quaternions, obs layout, reward ladder, no divergence, TimeLimit counters,
     and the 16-per-env contact cap binding as rarely as in the oracle: MuJoCo keeps every box-box point (up to 8
     per pair), and a jaw jammed into the bin walls collects 20-46 pad-bin contacts, so the cap drops some; the
@@ -1107,7 +1109,9 @@ def test_config2_benched_split_full_size():
     from gym_so100 import SO100VecEnv
     n = 65536
     env = SO100VecEnv(n, device="cuda:0", seed=0)
-    assert not env.fused and env.chunk_info()[0] == 4
+    assert env.fused                                            # auto mode at this size
+    env.fused = fused
+    assert env.chunk_info()[0] == (1 if fused else 4)
     env.reset(seed=1000)
     g = torch.Generator(device="cuda").manual_seed(0)
     drops, rewards = 0, set()
