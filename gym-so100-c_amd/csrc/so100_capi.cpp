@@ -199,6 +199,9 @@ static so100_buffers offset_buffers(const so100_buffers& b, int s) {
   o.mocap = off(b.mocap, 7);
   o.reward64 = off(b.reward64, 1);
   o.ncon_dropped = off(b.ncon_dropped, 1);
+  o.ep_return = off(b.ep_return, 1);
+  o.ep_final = off(b.ep_final, 2);
+  o.ep_accum = off(b.ep_accum, 4);
   return o;
 }
 

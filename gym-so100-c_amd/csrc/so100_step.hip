@@ -2883,6 +2883,23 @@ DEV void final_stage(const StageArgs& args, EnvShared& sh, int lane, int grp, in
       if (B.diverged) B.diverged[env] = diverged;
       if (B.contact_bits) B.contact_bits[env] = bits;
       if (goal && B.total_steps) B.total_steps[env] = B.total_steps[env] + 1;
+      if (B.ep_return) {
+        // episode statistics (RecordEpisodeStatistics): the running float64 return, and at the episode's end
+        // its return and length into ep_final and the env's running totals
+        const double ret = B.ep_return[env] + reward;
+        B.ep_return[env] = doneflag ? 0.0 : ret;
+        if (doneflag && B.ep_final) {
+          B.ep_final[(size_t)env * 2] = ret;
+          B.ep_final[(size_t)env * 2 + 1] = (double)elapsed;
+        }
+        if (doneflag && B.ep_accum) {
+          double* a = B.ep_accum + (size_t)env * 4;
+          a[0] += 1.0;
+          a[1] += success ? 1.0 : 0.0;
+          a[2] += ret;
+          a[3] += (double)elapsed;
+        }
+      }
     }
     if (goal && B.achieved_goal && lane < 3) B.achieved_goal[(size_t)env * 3 + lane] = cube_f[lane];
     if (B.obs) write_obs(m, sh, lane, qv_obs, B.obs + (size_t)env * SO100_NOBS);
@@ -2983,8 +3000,19 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 #define SO100_LAUNDER 2
 #endif
 #ifndef SO100_LAUNDER_IDS
-#define SO100_LAUNDER_IDS 1
+#define SO100_LAUNDER_IDS 2
 #endif
+// the fused kernel's lane / env ids inside the substep loop and the epilogue, from an opaque read of the lane's
+// position in its wave (one wave per workgroup) and the workgroup's group index (scalar)
+static_assert(kThreads == 64, "fresh_ids: one wave per workgroup");
+DEV void fresh_ids(int group, int n, int& lane, int& grp, int& env, int& e) {
+  int t;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(t));
+  lane = t & (kLanes - 1);
+  grp = t / kLanes;
+  env = group * kEnvsPerBlock + grp;
+  e = env < n ? env : 0;
+}
 #ifndef SO100_PRIO
 #define SO100_PRIO 1
 #endif
@@ -3004,7 +3032,7 @@ __global__ void __launch_bounds__(kThreads, SO100_STAGE_WAVES) so100_stage_kerne
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
 // functions on the same values.  kDebug: the instantiation that also fills the debug buffer (launched when
 // the caller passes one); the other has no debug code, which costs registers in the substep loop.
-// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, 32 B/lane of spills) when
+// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, 76 B/lane of spill slots) when
 // the grid exceeds 2 waves per SIMD; a grid of at most 2 waves per SIMD (8,192 envs on 256 CUs: all waves
 // resident at once) takes the 2-wave build (186 VGPRs, no scratch; +0.8 % there, -7 % at 16,384 envs).
 // Register allocation only: both give the same results bit for bit.
@@ -3060,8 +3088,14 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     // the lane / env ids laundered per substep too: what derives from them (masks, addresses, per-lane
     // model values) is recomputed in each substep instead of hoisted and held live across the loop
     int lane = lane0, grp = grp0, env = env0, e = e0;
+#if SO100_LAUNDER_IDS == 2
+    // recomputed from the wave's lane id (an opaque v_mbcnt pair, which LICM cannot hoist) and the
+    // workgroup's scalar group index: no vector value of the ids is carried across the loop
+    fresh_ids(group, args.n, lane, grp, env, e);
+#else
     if constexpr (SO100_LAUNDER_IDS && !(kWaves == 2 && SO100_W2_NOLAUNDER))
       asm volatile("" : "+v"(lane), "+v"(grp), "+v"(env), "+v"(e));
+#endif
     const bool valid = env < args.n;
     EnvShared& sh = shm[grp];
     TL_MARK(-1);
@@ -3110,7 +3144,11 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     // fresh ids again: the epilogue's store addresses must not be the prologue's load addresses (CSE would
     // hold those across the substep loop)
     int lane = lane0, grp = grp0, env = env0, e = e0;
+#if SO100_LAUNDER_IDS == 2
+    fresh_ids(group, args.n, lane, grp, env, e);
+#else
     asm volatile("" : "+v"(lane), "+v"(grp), "+v"(env), "+v"(e));
+#endif
     const bool valid = env < args.n;
     EnvShared& sh = shm[grp];
     euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
@@ -3185,6 +3223,7 @@ __global__ void __launch_bounds__(kThreads) so100_reset_kernel(ResetArgs args) {
     if (lane == 0) {
       if (B.elapsed) B.elapsed[env] = 0;
       if (B.episode) B.episode[env] = episode;
+      if (B.ep_return) B.ep_return[env] = 0.0;
     }
     if (args.task == SO100_TASK_GOAL && B.desired_goal && lane < 3) {
       const int tsteps = B.total_steps ? B.total_steps[env] : 0;

@@ -22,7 +22,8 @@ class SO100Buffers(ctypes.Structure):
     _fields_ = [(n, _P) for n in (
         "qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "action",
         "obs", "reward", "terminated", "truncated", "success", "final_obs", "diverged", "contact_bits",
-        "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64", "ncon_dropped")]
+        "achieved_goal", "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64", "ncon_dropped",
+        "ep_return", "ep_final", "ep_accum")]
 
 
 SO100_MAX_LIGHTS = 4
@@ -44,7 +45,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 12         # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 13         # include/so100.h SO100_ABI_VERSION
 HULL_CELLG = 8           # SO100_HULL_CELLG
 HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 

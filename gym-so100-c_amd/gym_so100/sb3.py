@@ -19,6 +19,8 @@ When stable-baselines3 is importable the class derives from its ``VecEnv`` (so `
 GPU; this layer only moves the [N,15] observation and the per-env scalars to host numpy, which SB3's
 numpy interface requires.
 """
+import time
+
 import numpy as np
 
 from . import spaces
@@ -43,7 +45,8 @@ class SO100SB3VecEnv(_VecEnvBase):
                  domain_randomization=None, env_offset=0, iterations=None, solver="newton"):
         self.venv = SO100VecEnv(num_envs, task=task, device=device, seed=seed, max_episode_steps=max_episode_steps,
                                 autoreset=True, domain_randomization=domain_randomization, env_offset=env_offset,
-                                iterations=iterations, solver=solver)
+                                iterations=iterations, solver=solver, episode_stats=True)
+        self._t0 = time.time()
         n = self.venv.num_envs
         obs_box = spaces.Box(low=-np.inf, high=np.inf, shape=(15,), dtype=np.float32)
         if self.venv.is_goal:
@@ -112,6 +115,12 @@ class SO100SB3VecEnv(_VecEnvBase):
                     term_obs = final[k]
                 infos[i]["terminal_observation"] = term_obs
                 infos[i]["TimeLimit.truncated"] = bool(truncated[i] and not terminated[i])
+            # VecMonitor's info["episode"], from the kernel's episode statistics (return in float64, as the
+            # reference's rewards)
+            ep = _np(v.ep_final[done_t])
+            t = round(time.time() - self._t0, 6)
+            for k, i in enumerate(idx):
+                infos[i]["episode"] = {"r": float(ep[k, 0]), "l": int(ep[k, 1]), "t": t}
         return self._obs_np(obs), rewards, dones, infos
 
     def step(self, actions):

@@ -91,6 +91,11 @@ class SO100VecEnv:
         convex: the collider of the mesh pairs (the cube, bin boxes and finger pads against the link hulls, the
             links against each other and the Base): "epa" (default: GJK + EPA, MuJoCo 3.3.3's default native
             convex collider: the minimum penetration) or "mpr" (libccd's MPR, MuJoCo's mjDSBL_NATIVECCD path).
+        episode_stats: keep device-side episode statistics (RecordEpisodeStatistics): the running float64
+            return ``ep_return`` [N], the last finished episode's (return, length) ``ep_final`` [N,2] and the
+            per-env totals ``ep_accum`` [N,4] (episodes, successes, sum of returns, sum of lengths), written
+            by the step kernel's epilogue; ``info["episode"]`` then carries r / l of the envs that finished
+            (mask ``info["_episode"]``), and ``episode_statistics()`` reduces the totals on demand.
         nsubstep: physics substeps per env step (default: the reference's 10, control_timestep / timestep);
             1 makes an env step one mj_step + the final mj_step1 (the parity tests' per-substep checks).
     """
@@ -98,7 +103,7 @@ class SO100VecEnv:
     def __init__(self, num_envs, task="so100_cube_to_bin", obs_type="so100_state", device="cuda:0", seed=0,
                  max_episode_steps=None, autoreset=True, domain_randomization=None, env_offset=0,
                  iterations=None, debug=False, solver="newton", observation_width=640, observation_height=480,
-                 variant="joint", reward64=False, nsubstep=None, convex="epa"):
+                 variant="joint", reward64=False, nsubstep=None, convex="epa", episode_stats=False):
         torch = _torch()
         if obs_type not in ("so100_state", "so100_pixels_agent_pos"):
             raise NotImplementedError(f"obs_type={obs_type!r}: 'so100_state' or 'so100_pixels_agent_pos'")
@@ -148,6 +153,10 @@ class SO100VecEnv:
         self.total_steps = torch.zeros(n, dtype=i32, device=d) if self.is_goal else None
         self.debug = torch.zeros(n, _native.SO100_DBG_STRIDE, dtype=f32, device=d) if debug else None
         self.reward64 = torch.zeros(n, dtype=torch.float64, device=d) if reward64 else None
+        f64 = torch.float64
+        self.ep_return = torch.zeros(n, dtype=f64, device=d) if episode_stats else None
+        self.ep_final = torch.zeros(n, 2, dtype=f64, device=d) if episode_stats else None
+        self.ep_accum = torch.zeros(n, 4, dtype=f64, device=d) if episode_stats else None
         self.mocap = None
         if variant == "ee":          # mj_resetData's mocap pose: the mocap body's (so_arm100_ee.xml:155)
             m0 = list(self.model.mocap_pos0) + list(self.model.mocap_quat0)
@@ -173,7 +182,8 @@ class SO100VecEnv:
         b = self._buf
         for name in ("qpos", "qvel", "qacc_warmstart", "elapsed", "episode", "obs", "reward", "terminated",
                      "truncated", "success", "final_obs", "diverged", "contact_bits", "achieved_goal",
-                     "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64", "ncon_dropped"):
+                     "desired_goal", "total_steps", "dr_params", "debug", "mocap", "reward64", "ncon_dropped",
+                     "ep_return", "ep_final", "ep_accum"):
             setattr(b, name, P(getattr(self, name)))
         if not getattr(self, "_debug_enabled", True):
             b.debug = None
@@ -281,6 +291,9 @@ class SO100VecEnv:
             info["_final_observation"] = done
         if self.is_goal:
             info["TimeLimit.truncated"] = self.truncated
+        if self.ep_final is not None:                  # RecordEpisodeStatistics' info["episode"] / "_episode"
+            info["episode"] = {"r": self.ep_final[:, 0], "l": self.ep_final[:, 1]}
+            info["_episode"] = done
         return self._observation(), self.reward, self.terminated, self.truncated, info
 
     def set_action_buffer(self, actions):
@@ -309,6 +322,18 @@ class SO100VecEnv:
                                                s), "so100_reset")
         self.renderer.render()
         return done
+
+    def episode_statistics(self, clear=False):
+        """Totals of the episodes finished since construction (or the last ``clear``), reduced over the envs
+        on the device and read once: episodes, successes, success_rate, mean_return, mean_length."""
+        if self.ep_accum is None:
+            raise ValueError("episode statistics need episode_stats=True")
+        t = self.ep_accum.sum(dim=0).cpu().tolist()
+        if clear:
+            self.ep_accum.zero_()
+        n = t[0]
+        return {"episodes": int(n), "successes": int(t[1]), "success_rate": t[1] / n if n else float("nan"),
+                "mean_return": t[2] / n if n else float("nan"), "mean_length": t[3] / n if n else float("nan")}
 
     def step_async_raw(self):
         """Launch one env step on the current stream using the actions already in ``self.actions``

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 12  /* 12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 13  /* 13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -74,6 +74,17 @@ typedef struct so100_buffers {
   /* [N] contacts the 16-per-env cap (SO100_MAXCON) left out, summed over the step's substeps: the counterpart
    * of the oracle's ncon_dropped (MuJoCo has no such cap; 0 is the bar).  NULL = not written */
   uint32_t* ncon_dropped;
+  /* Device-side episode statistics (what gymnasium's RecordEpisodeStatistics / SB3's VecMonitor keep on the
+   * host, reference scripts/train_sac.py:290; SURVEY §5 Metrics), written by the step epilogue; the host reads
+   * them only on demand.  ep_final and ep_accum are written only when ep_return is given.  NULL = not kept.
+   *   ep_return [N]   return of the running episode: the sum of its float64 rewards so far; set to 0 when the
+   *                   episode ends (terminated or truncated, with or without auto-reset) and by so100_reset;
+   *   ep_final  [N,2] return and length (steps) of the env's last finished episode, written at its end;
+   *   ep_accum  [N,4] over the env's finished episodes: count, successes (ended with is_success), sum of
+   *                   returns, sum of lengths; never cleared by the library (the caller zeroes it). */
+  double*   ep_return;
+  double*   ep_final;
+  double*   ep_accum;
 } so100_buffers;
 
 /* Debug record per env (floats), written by the last substep of a step when `debug` is not NULL:
