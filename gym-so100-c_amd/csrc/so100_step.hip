@@ -1870,16 +1870,56 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
   return true;
 }
 
+// Broadphase bounding spheres (oracle mpr_broadphase stage 1), one per collision object: hull k at k (< 10,
+// the Base hull at 9), geom g (1..14: pads, cube, bin boxes) at 9 + g.  World centre (hull: its bounding box
+// centre; box: its centre) and radius (hull_half.w / geom_rbound), by the arithmetic mpr_sphere uses.
+constexpr int kSphObj = SO100_NHULL_ALL + SO100_NGEOM - 1;   // 24
+DEV float4 sphere_obj(const DevModel* __restrict__ m, const EnvShared& sh, int o) {
+  float c[3], r;
+  if (o < SO100_NHULL_ALL) {
+    float R[9], P[3], w[3];
+    hull_frame(m, sh, m->hull_body[o], R, P);
+    const float4 b4 = reinterpret_cast<const float4*>(m->hull_center)[o];
+    const float bl[3] = {b4.x, b4.y, b4.z};
+    mulmv3(w, R, bl);
+#pragma unroll
+    for (int t = 0; t < 3; t++) c[t] = w[t] + P[t];
+    r = reinterpret_cast<const float4*>(m->hull_half)[o].w;
+  } else {
+    const int g = o - (SO100_NHULL_ALL - 1);
+    if (g == SO100_CUBE_GEOM) {
+#pragma unroll
+      for (int t = 0; t < 3; t++) c[t] = sh.cube_pos[t];
+    } else if (m->geom_body[g] == 0) {               // a bin box (static)
+#pragma unroll
+      for (int t = 0; t < 3; t++) c[t] = m->geom_pos[g][t];
+    } else {                                         // a finger pad on a jaw
+      float Rp[9];
+      geom_pose(m, sh, g, c, Rp);
+    }
+    r = m->geom_rbound[g];
+  }
+  return make_float4(c[0], c[1], c[2], r);
+}
+
 // The MPR pairs 23..142 of one substep ((cube | bin box, hull), hull-hull self-collision, the Base hull, the
 // finger pads vs the arm's link hulls),
 // contacts staged in sh.mpr in pair order.
-//  * broadphase, lane-parallel: lane l of the env's row tests pairs 23 + l + 16 r (r < 8);
+//  * broadphase stage 1, bounding spheres: lane l of the env's row computes objects l and l + 16 of the
+//    env's sphere table (sphere_obj, in its MPR staging area, dead until the narrowphase's hits), then tests
+//    pairs 23 + l + 16 r (r < 8) by two table reads each; the survivors form a wave-wide list (env by env,
+//    pairs ascending);
+//  * broadphase stage 2, OBB separating axes (mpr_broadphase), one list item per lane of the wave (64 per
+//    batch; round 2 ran both stages on the env's own row, 8 rounds of 16 pairs, each round paying the sphere
+//    and OBB paths of every pair class: 28 % of the average wave's assembly); the OBB survivors go to their
+//    env's candidate list in pair order;
 //  * narrowphase, shared across the wave: the 4 envs' candidates form one list (env by env, pairs ascending,
 //    in the LDS contact area of env 0, dead until the compaction); each round the 4 rows take the next 4
 //    items, whichever env they belong to, and run MPR on that env's frames.  A wave whose envs hold c_e
 //    candidates runs ceil(sum c_e / 4) rounds: the envs' own rows share a heavy env's pairs (this was one
 //    pair of the wave's union per round, on the rows holding it: 60 % of the slowest waves' assembly);
 //  * each round's hits go to their env's staging slots in list order, so each env keeps its pair order.
+// The candidate lists are the pairs passing both stages, in pair order, as before: the same contacts.
 // Returns the env's number of MPR contacts (uniform across its row; those beyond kMaxCon are not staged and
 // count as dropped).
 template <bool kCells>
@@ -1898,42 +1938,93 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
   // area holds the rows' EPA polytopes)
   static_assert(kConvex <= (int)(sizeof(shm[0].ser.cdd) + sizeof(shm[0].ser.tau)), "an env's candidate list fits");
   static_assert(__builtin_offsetof(SerialScratch, cdd) >= sizeof(ConArea), "the candidate lists do not alias the contact area");
+  // the sphere table and the sphere survivors' list in the env's MPR staging area
+  static_assert(kSphObj * sizeof(float4) + kConvex <= sizeof(shm[0].mpr), "sphere table + list fit the staging area");
   const EnvShared& sh = shm[grp];
-  uint64_t env_cand[2] = {0ull, 0ull};
-  uint32_t mine = 0u;                           // bit r: this lane's pair of round r is a candidate
+  {
+    float4* tab = reinterpret_cast<float4*>(&shm[grp].mpr[0]);
 #pragma unroll
-  for (int r = 0; r < kRounds; r++) {
-    const int q = lane + kLanes * r;
-    bool cand = false;
-    if (valid && q < kConvex && mpr_sphere(m, sh, SO100_PAIR_MPR0 + q)) {
-      MprObj o;
-      mpr_obj_setup(m, sh, SO100_PAIR_MPR0 + q, o);
-      cand = mpr_broadphase(m, o, -1 - m->pair_g2[SO100_PAIR_MPR0 + q]);
+    for (int pass = 0; pass < 2; pass++) {
+      const int o = lane + kLanes * pass;
+      if (o < kSphObj) tab[o] = sphere_obj(m, sh, o);
     }
-    const uint64_t b = __ballot(cand);
-    mine |= cand ? 1u << r : 0u;
-    env_cand[r / 4] |= ((b >> (grp * 16)) & 0xFFFFull) << (16 * (r % 4));
   }
-  // the wave's candidate list: env e's at [pre_e, pre_e + c_e)
-  const int cnt = __popcll(env_cand[0]) + __popcll(env_cand[1]);
-  const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
-  const int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
+  __syncthreads();
+  uint64_t env_cand[2] = {0ull, 0ull};
+  uint32_t mine = 0u;                           // bit r: this lane's pair of round r passes the spheres
+  {
+    const float4* tab = reinterpret_cast<const float4*>(&shm[grp].mpr[0]);
+#pragma unroll
+    for (int r = 0; r < kRounds; r++) {
+      const int q = lane + kLanes * r;
+      bool cand = false;
+      if (valid && q < kConvex) {
+        const int g = m->pair_g1[SO100_PAIR_MPR0 + q], k = -1 - m->pair_g2[SO100_PAIR_MPR0 + q];
+        const float4 a = tab[g >= 0 ? SO100_NHULL_ALL - 1 + g : -1 - g], b = tab[k];
+        const float T[3] = {a.x - b.x, a.y - b.y, a.z - b.z};
+        const float rs = b.w + a.w;
+        cand = dot3(T, T) <= rs * rs;
+      }
+      const uint64_t bl = __ballot(cand);
+      mine |= cand ? 1u << r : 0u;
+      env_cand[r / 4] |= ((bl >> (grp * 16)) & 0xFFFFull) << (16 * (r % 4));
+    }
+  }
+  // the wave's list of sphere survivors: env e's at [spre_e, spre_e + s_e), in its own staging area
+  const int scnt = __popcll(env_cand[0]) + __popcll(env_cand[1]);
+  const int s0c = __builtin_amdgcn_readlane(scnt, 0), s1c = __builtin_amdgcn_readlane(scnt, 16);
+  const int s2c = __builtin_amdgcn_readlane(scnt, 32), s3c = __builtin_amdgcn_readlane(scnt, 48);
+  const int spre1 = s0c, spre2 = s0c + s1c, spre3 = s0c + s1c + s2c, stotal = spre3 + s3c;
+  if (stotal == 0) return 0;
+  {
+    uint8_t* slist = reinterpret_cast<uint8_t*>(&shm[grp].mpr[0]) + kSphObj * sizeof(float4);
+#pragma unroll
+    for (int r = 0; r < kRounds; r++) {
+      if ((mine >> r) & 1u) {
+        const int q = lane + kLanes * r;     // rank = sphere survivors of this env below pair q
+        const uint64_t below0 = q >= 64 ? env_cand[0] : (env_cand[0] & ((1ull << q) - 1ull));
+        const uint64_t below1 = q >= 64 ? (env_cand[1] & ((1ull << (q - 64)) - 1ull)) : 0ull;
+        slist[__popcll(below0) + __popcll(below1)] = (uint8_t)q;
+      }
+    }
+  }
+  __syncthreads();
+  // stage 2 over the survivors, one per lane of the wave; the OBB survivors to their env's list in order
+  int c0 = 0, c1 = 0, c2 = 0, c3 = 0;           // candidates per env (wave-uniform)
+  {
+    const int tid = grp * kLanes + lane;
+    const uint64_t below_me = (1ull << tid) - 1ull;
+    for (int b0 = 0; b0 < stotal; b0 += kThreads) {
+      const int item = b0 + tid;
+      const bool act = item < stotal;
+      const int ie = item >= spre3 ? 3 : item >= spre2 ? 2 : item >= spre1 ? 1 : 0;
+      int q = 0;
+      bool pass = false;
+      if (act) {
+        const int spre_ie = ie == 0 ? 0 : ie == 1 ? spre1 : ie == 2 ? spre2 : spre3;
+        q = (reinterpret_cast<const uint8_t*>(&shm[ie].mpr[0]) + kSphObj * sizeof(float4))[item - spre_ie];
+        MprObj o;
+        mpr_obj_setup(m, shm[ie], SO100_PAIR_MPR0 + q, o);
+        pass = mpr_broadphase(m, o, -1 - m->pair_g2[SO100_PAIR_MPR0 + q]);
+      }
+      const uint64_t pb = __ballot(pass);
+      const uint64_t e0 = __ballot(act && ie == 0), e1 = __ballot(act && ie == 1);
+      const uint64_t e2 = __ballot(act && ie == 2), e3 = __ballot(act && ie == 3);
+      if (pass) {
+        const uint64_t mie = ie == 0 ? e0 : ie == 1 ? e1 : ie == 2 ? e2 : e3;
+        const int base = ie == 0 ? c0 : ie == 1 ? c1 : ie == 2 ? c2 : c3;
+        reinterpret_cast<uint8_t*>(&shm[ie].ser.cdd[0][0])[base + __popcll(pb & mie & below_me)] = (uint8_t)q;
+      }
+      c0 += __popcll(pb & e0); c1 += __popcll(pb & e1); c2 += __popcll(pb & e2); c3 += __popcll(pb & e3);
+    }
+  }
   const int pre1 = c0, pre2 = c0 + c1, pre3 = c0 + c1 + c2;
   int total = pre3 + c3;
 #ifdef SO100_EXPERIMENT_MPR_BROAD_ONLY
+  asm volatile("" ::"v"(total));   // keeps the broadphase live
   total = 0;   // timing experiment only: broadphase without the narrowphase
 #endif
   if (total == 0) return 0;
-  uint8_t* own_list = reinterpret_cast<uint8_t*>(&shm[grp].ser.cdd[0][0]);
-#pragma unroll
-  for (int r = 0; r < kRounds; r++) {
-    if ((mine >> r) & 1u) {
-      const int q = lane + kLanes * r;     // rank = candidates of this env below pair q
-      const uint64_t below0 = q >= 64 ? env_cand[0] : (env_cand[0] & ((1ull << q) - 1ull));
-      const uint64_t below1 = q >= 64 ? (env_cand[1] & ((1ull << (q - 64)) - 1ull)) : 0ull;
-      own_list[__popcll(below0) + __popcll(below1)] = (uint8_t)q;
-    }
-  }
   __syncthreads();
   int f0 = 0, f1 = 0, f2 = 0, f3 = 0;           // staged contacts per env (wave-uniform)
   const int rounds = (total + kEnvsPerBlock - 1) / kEnvsPerBlock;
@@ -2191,12 +2282,13 @@ DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_
 // write one box-box pair's contacts into slots base, base+1, ... (slots >= kMaxCon are dropped, as the
 // oracle's add_contact drops contacts beyond SO100_MAXCON)
 DEV void put_box_contacts(EnvShared& sh, const PairContacts& pc, int base, int p) {
+  // one frame per pair (every contact of a box pair shares its normal)
+  float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
+  if (pc.n > 0) make_frame(fr);
 #pragma unroll
   for (int c = 0; c < SO100_MAXCONPAIR; c++) {
     const int slot = base + c;
     if (c < pc.n && slot < kMaxCon) {
-      float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
-      make_frame(fr);
 #pragma unroll
       for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
       sh.con[slot].g.pos[0] = pc.pos[c][0]; sh.con[slot].g.pos[1] = pc.pos[c][1];
@@ -2428,6 +2520,9 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     PairContacts pc;
     pc.n = 0;
     if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
+#ifdef SO100_STAMP_BOXBOX
+    SSTAMP(0);            // stamps diagnostic: the box-box pairs alone in slot 0 (Euler's, empty in the stage kernel)
+#endif
     sh.cnt[lane] = pc.n;
     __syncthreads();
     {
