@@ -598,8 +598,11 @@ DEV void col3(float* o, const float* R, int c) {          // column c of a row-m
   for (int t = 0; t < 3; t++) o[t] = R[3 * t] * w[0] + R[3 * t + 1] * w[1] + R[3 * t + 2] * w[2];
 }
 
+// collapse: the pair is the cube against the table's mesh, one contact (MuJoCo's convex collider; the oracle's
+// collide_box_pair): the mean of the kept points' positions and the deepest distance, summed in clip order as
+// the kept points would be, without their compaction and 8-slot output (bitwise the same contact)
 DEV void box_box(const float* p1, const float* R1, const float* A, const float* p2, const float* R2,
-                 const float* B, float margin, PairContacts& out) {
+                 const float* B, float margin, PairContacts& out, bool collapse) {
   out.n = 0;
   float pd[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]}, pp[3], R[9], Q[9];
   mulmtv3(pp, R1, pd);
@@ -761,6 +764,36 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   if (fabsf(det) < 1e-12f) return;
   det = 1.f / det;
   const float i11 = m22 * det, i12 = -m12 * det, i21 = -m21 * det, i22 = m11 * det;
+  if (collapse) {
+    float sp[3] = {0.f, 0.f, 0.f}, dmin = 0.f;
+    int cnum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (k < n) {
+        const float x = P.x[k] - cc1, y = P.y[k] - cc2;
+        const float s1 = i11 * x + i12 * y, s2 = i21 * x + i22 * y;
+        float pt[3];
+        for (int t = 0; t < 3; t++) pt[t] = center[t] + s1 * v1[t] + s2 * v2[t];
+        const float dp = srcN - dot3(nref, pt);
+        if (dp > -margin) {
+#pragma unroll
+          for (int t = 0; t < 3; t++) sp[t] += pt[t] + pR[t] + 0.5f * dp * nref[t];
+          dmin = (cnum == 0 || -dp < dmin) ? -dp : dmin;
+          cnum++;
+        }
+      }
+    }
+    if (cnum < 1) return;
+    const float nf = (float)cnum;
+#pragma unroll
+    for (int c = 0; c < SO100_MAXCONPAIR; c++) {     // every slot (no run-time slot index: see below)
+#pragma unroll
+      for (int t = 0; t < 3; t++) out.pos[c][t] = sp[t] / nf;
+      out.dist[c] = dmin;
+    }
+    out.n = 1;
+    return;
+  }
   // keep the penetrating points (compacted in order; 2D coords in K, depth in D)
   Poly8 K;
   K.n = 0;
@@ -835,25 +868,9 @@ DEV void collide_pair(const DevModel* __restrict__ m, const EnvShared& sh, int p
   float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   const float margin = m->pair_margin[p];
   if (sqrtf(dot3(d, d)) > sqrtf(dot3(A, A)) + sqrtf(dot3(B, B)) + margin) return;
-  box_box(p1, R1, A, p2, R2, B, margin, pc);
   // the cube against the table's mesh (geom2 = geom 0): MuJoCo's convex collider, one contact per pair (the
   // oracle's collide_box_pair): the SAT normal, the deepest distance, the mean of the clipped positions
-  if (g2 == 0 && pc.n > 1) {
-    float sp[3] = {0.f, 0.f, 0.f}, dmin = pc.dist[0];
-#pragma unroll
-    for (int c = 0; c < SO100_MAXCONPAIR; c++) {
-      if (c < pc.n) {
-#pragma unroll
-        for (int t = 0; t < 3; t++) sp[t] += pc.pos[c][t];
-        dmin = pc.dist[c] < dmin ? pc.dist[c] : dmin;
-      }
-    }
-    const float nf = (float)pc.n;
-#pragma unroll
-    for (int t = 0; t < 3; t++) pc.pos[0][t] = sp[t] / nf;
-    pc.dist[0] = dmin;
-    pc.n = 1;
-  }
+  box_box(p1, R1, A, p2, R2, B, margin, pc, g2 == 0);
 }
 
 // Arm/jaw hulls vs the table top (pairs SO100_NPAIR_BOX + k; oracle collision()): hull k's lowest
