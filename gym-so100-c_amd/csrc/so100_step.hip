@@ -947,6 +947,9 @@ struct MprSup {
   uint32_t id;                      // the supports: obj1 box corner signs (bits 0..2) or hull vertex (0..9), obj2 hull
                                     // vertex << 10 (EPA rebuilds a vertex from it: sup_from_id)
 };
+#ifndef SO100_SMALL_HULL_REG
+#define SO100_SMALL_HULL_REG 0
+#endif
 struct MprObj {
   float c[3], ax[9], h[3];          // obj1 frame in H: origin (box centre / hull body origin), axes
                                     // (columns of ax); box half sizes
@@ -957,6 +960,9 @@ struct MprObj {
   int s1, n1;                       // obj1 hull vertex range
   int k, s0, n;                     // obj2: hull index, vertex range
   bool cells;                       // hull supports through the direction cells (fused kernel) or full scans
+#if SO100_SMALL_HULL_REG
+  float4 v2r;                       // obj2 hull of at most 16 vertices: the lane's vertex, held for the item
+#endif
 };
 constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
 constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
@@ -1075,6 +1081,18 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
   return make_float4(bx, by, bz, __int_as_float(bi));
 }
 
+#if SO100_SMALL_HULL_REG
+// the support of a hull of at most 16 vertices from the row's register-held vertices (lane l: vertex min(l, n - 1)):
+// the whole-hull scan's arithmetic and tie rule (first maximal vertex), without a memory access per support
+DEV float4 hull_support_reg(float4 v, int idx, float n0, float n1, float n2) {
+  float best = -__builtin_inff(), bx = 0.f, by = 0.f, bz = 0.f;
+  int bi = 0x7fffffff;
+  const float sc = sup_score(n0, n1, n2, v.x, v.y, v.z);
+  if (sc > best) { best = sc; bi = idx; bx = v.x; by = v.y; bz = v.z; }
+  arg_best16<false>(best, bi, bx, by, bz);
+  return make_float4(bx, by, bz, __int_as_float(bi));
+}
+#endif
 DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const float* d, MprSup& s, int lane) {
   uint32_t id = 0u;
 #pragma unroll
@@ -1099,7 +1117,12 @@ DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const floa
 #pragma unroll
     for (int t = 0; t < 3; t++) s.v1[t] += w[t];
   }
+#if SO100_SMALL_HULL_REG
+  const float4 v = o.n <= kLanes ? hull_support_reg(o.v2r, min(lane, o.n - 1), -d[0], -d[1], -d[2])
+                                 : hull_support(m, o.cells, o.k, o.s0, o.n, -d[0], -d[1], -d[2], lane);
+#else
   const float4 v = hull_support(m, o.cells, o.k, o.s0, o.n, -d[0], -d[1], -d[2], lane);
+#endif
   s.v2[0] = v.x; s.v2[1] = v.y; s.v2[2] = v.z;
   s.id = id | (uint32_t)__float_as_int(v.w) << 10;
   sub3(s.v, s.v1, s.v2);
@@ -2059,6 +2082,10 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
       MprObj o;
       mpr_obj_setup(m, shm[ie], p, o);
       o.cells = kCells;
+#if SO100_SMALL_HULL_REG
+      o.v2r = o.n <= kLanes ? ld_global4(reinterpret_cast<const float4*>(m->hull_vert), o.s0 + min(lane, o.n - 1))
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
       hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp);
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
