@@ -452,6 +452,10 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->pair_margin[p] = (float)s->pair_margin[p];
     const int b1 = s->pair_body1[p], b2 = s->pair_body2[p];
     if (b1 < 0 || b1 >= SO100_NBODY || b2 < 0 || b2 >= SO100_NBODY) return fail("model: pair body out of range");
+    // the kernels' box pairs take a geom's body from the pair (geom_pose_b)
+    if ((s->pair_geom1[p] >= 0 && s->geom_body[s->pair_geom1[p]] != b1) ||
+        (s->pair_geom2[p] >= 0 && s->geom_body[s->pair_geom2[p]] != b2))
+      return fail("model: pair bodies must be their geoms' bodies");
     d->pair_b1[p] = b1;
     d->pair_b2[p] = b2;
     d->pair_cond4[p] = s->pair_condim[p] == 4;

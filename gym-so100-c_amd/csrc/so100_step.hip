@@ -1073,9 +1073,9 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   out.n = cnum;
 }
 
-// geom world pose from the staged body frames
-DEV void geom_pose(const DevModel* __restrict__ m, const EnvShared& sh, int g, float* pos, float* mat) {
-  int b = m->geom_body[g];
+// geom world pose from the staged body frames; b = the geom's body (a pair's body id, pair_b1 / pair_b2, loaded
+// beside its geom id instead of after it: so100_create checks pair_b = geom_body[pair_g])
+DEV void geom_pose_b(const DevModel* __restrict__ m, const EnvShared& sh, int g, int b, float* pos, float* mat) {
   if (b == 0) {
 #pragma unroll
     for (int k = 0; k < 3; k++) pos[k] = m->geom_pos[g][k];
@@ -1093,13 +1093,16 @@ DEV void geom_pose(const DevModel* __restrict__ m, const EnvShared& sh, int g, f
   for (int k = 0; k < 3; k++) pos[k] = bp[k] + t[k];
   mulmm3(mat, bm, m->geom_mat[g]);
 }
+DEV void geom_pose(const DevModel* __restrict__ m, const EnvShared& sh, int g, float* pos, float* mat) {
+  geom_pose_b(m, sh, g, m->geom_body[g], pos, mat);
+}
 
 DEV void collide_pair(const DevModel* __restrict__ m, const EnvShared& sh, int p, PairContacts& pc) {
   pc.n = 0;
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   float p1[3], R1[9], p2[3], R2[9];
-  geom_pose(m, sh, g1, p1, R1);
-  geom_pose(m, sh, g2, p2, R2);
+  geom_pose_b(m, sh, g1, m->pair_b1[p], p1, R1);
+  geom_pose_b(m, sh, g2, m->pair_b2[p], p2, R2);
   const float* A = m->geom_size[g1];
   const float* B = m->geom_size[g2];
   float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
@@ -2597,7 +2600,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
   float tx = 0.f, ty = 0.f, tz = 0.f;
   if (valid && lane < SO100_NPAD) {
     const int p = SO100_PAIR_PAD0 + lane, g = m->pair_g1[p];
-    const int b = m->geom_body[g];
+    const int b = m->pair_b1[p];                  // = geom_body[g] (so100_create), loaded beside g
     const float* bm = sh.jaw_mat[b - 6];
     const float* gm = m->geom_mat[g];
     const float top = m->table_top, margin = m->pair_margin[p];
@@ -2626,7 +2629,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
     int cnt = 0;
     if (cz - ext - top < margin + 1e-4f) {
     float c[3], R[9];
-    geom_pose(m, sh, g, c, R);
+    geom_pose_b(m, sh, g, b, c, R);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const float l0 = (k & 1 ? 1.f : -1.f) * m->geom_size[g][0];
