@@ -3411,7 +3411,7 @@ DEV void fresh_ids(int group, int n, int& lane, int& grp, int& env, int& e) {
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
 // functions on the same values.  kDebug: the instantiation that also fills the debug buffer (launched when
 // the caller passes one); the other has no debug code, which costs registers in the substep loop.
-// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, 76 B/lane of spill slots) when
+// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, 72 B/lane of spill slots) when
 // the grid exceeds 2 waves per SIMD; a grid of at most 2 waves per SIMD (8,192 envs on 256 CUs: all waves
 // resident at once) takes the 2-wave build (186 VGPRs, no scratch; +0.8 % there, -7 % at 16,384 envs).
 // Register allocation only: both give the same results bit for bit.
