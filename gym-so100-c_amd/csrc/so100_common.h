@@ -101,9 +101,8 @@ DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 // with P = Q' D and 1/lam) y_i(la) = c_i / (lam_i + la) with c = -P b, so an iterate costs three
 // reciprocals, and x = D Q w = P' w.
 // Root finding: MuJoCo's Newton on |y|^2 - r^2 from la = 0 (its 20-step cap included, so an unconverged
-// search stops where MuJoCo's does).  -DSO100_QCQP_SECULAR keeps rounds 1-2's variant for A/B: Newton on
-// 1/|y(la)| - 1/r (the trust-region secular equation) from the lower bound max(0, |c|/r - max lam), 1-2 steps,
-// converged where MuJoCo stops at its cap.  Returns the number of Newton steps taken.
+// search stops where MuJoCo's does; rounds 1-2 solved the secular equation instead).
+// Returns the number of Newton steps taken.
 DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* laminv, const float* b, float r,
                   bool live = true) {
   int nit = 0;
@@ -113,7 +112,6 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
 #pragma unroll
   for (int i = 0; i < 3; i++) { d[i] = laminv[i]; w[i] = c[i] * d[i]; }
   float s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-#ifndef SO100_QCQP_SECULAR
   // MuJoCo's iteration (mju_QCQP3; oracle qcqp): Newton on val = |y|^2 - r^2 from la = 0, at most 20 steps,
   // stops val < 1e-10 or delta < 1e-10; after the 20th step y stays at the la it was evaluated at.  In the
   // eigenbasis |y|^2 = sum w_i^2 and y' (A + la I)^-1 y = sum w_i^2 d_i, so delta = -val / deriv = val / 2t.
@@ -133,29 +131,6 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
       s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     }
   }
-#else
-  // Newton on the secular equation 1/|y| = 1/r from a lower bound (round 1-2; DESIGN.md §4 deviation 6)
-  if (live && s - r * r >= 1e-10f) {
-    const float rinv = __builtin_amdgcn_rcpf(r);
-    const float cn = __builtin_amdgcn_sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);   // raw v_sqrt (1 ulp)
-    float la = fmaxf(0.f, cn * rinv - fmaxf(lam[0], fmaxf(lam[1], lam[2])));
-#pragma unroll
-    for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
-    s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    for (int it = 0; it < 20; it++) {
-      if (s - r * r < 1e-10f) break;
-      nit++;
-      // d|y|^2/dla = -2 sum w_i^2 d_i;  Newton on g = 1/|y|: delta = (1/r - g) / g' = s (|y|/r - 1) / t
-      const float t = w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2];
-      const float delta = s * (__builtin_amdgcn_sqrtf(s) * rinv - 1.f) * __builtin_amdgcn_rcpf(t);
-      if (delta < 1e-10f || delta <= 4e-7f * la) break;
-      la += delta;
-#pragma unroll
-      for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
-      s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    }
-  }
-#endif
   // x = D Q w = P' w
 #pragma unroll
   for (int j = 0; j < 3; j++) x[j] = P[j] * w[0] + P[3 + j] * w[1] + P[6 + j] * w[2];

@@ -28,13 +28,7 @@
 namespace so100 {
 
 // One lane's share of a substep's Newton problem (its rows of the record).
-#ifndef SO100_JREG
-#define SO100_JREG 8
-#endif
-constexpr int kJReg = SO100_JREG;       // contacts whose J rows stay in VGPRs
-#ifndef SO100_LS_CONE_DIR
-#define SO100_LS_CONE_DIR 1             // line search: cone_dir (0: cone_eval + products, A/B)
-#endif
+constexpr int kJReg = 8;               // contacts whose J rows stay in VGPRs
 constexpr int kJLds = kMaxCon - kJReg;  // the others' J rows: LDS [kJLds][SO100_NV] float4 per env
 struct NewtonRows {
   float qs, warm, fr_aref;              // dof lanes: qacc_smooth, warmstart, frictionloss aref
@@ -48,12 +42,9 @@ struct NewtonRows {
 };
 
 // The solve's square roots and reciprocals on its serial chains: the hardware v_sqrt / v_rcp (1 ulp) instead of
-// the IEEE sequences (a dozen dependent instructions each); SO100_NEWTON_IEEE=1 keeps the IEEE forms (A/B).
-#ifndef SO100_NEWTON_IEEE
-#define SO100_NEWTON_IEEE 0
-#endif
-DEV float nsqrt(float x) { return SO100_NEWTON_IEEE ? sqrtf(x) : __builtin_amdgcn_sqrtf(x); }
-DEV float nrcp(float x) { return SO100_NEWTON_IEEE ? 1.f / x : __builtin_amdgcn_rcpf(x); }
+// the IEEE sequences (a dozen dependent instructions each).
+DEV float nsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+DEV float nrcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // MuJoCo mj_constraintUpdate (primal), elliptic contact block at jar: cost, force f = -dc/djar, and the
 // cost Hessian (upper triangle 00 01 02 03 11 12 13 22 23 33).  Oracle block_eval.
@@ -472,15 +463,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             float x[4], fv, vhv;
 #pragma unroll
             for (int k = 0; k < 4; k++) x[k] = jc[k] + al * jsc[k];
-#if SO100_LS_CONE_DIR
             cone_dir(x, jsc, c_D, c_Dm, c_mu, c_fr0, c_fr1, fv, vhv);
-#else
-            float fcc[4], hcc[10];
-            cone_eval(x, c_D, c_Dm, c_mu, c_fr0, c_fr1, cc, fcc, hcc);
-            const float4 v = make_float4(jsc[0], jsc[1], jsc[2], jsc[3]);
-            fv = fcc[0] * jsc[0] + fcc[1] * jsc[1] + fcc[2] * jsc[2] + fcc[3] * jsc[3];
-            vhv = dot4(v, sym4(hcc, v));
-#endif
             l1 -= fv;
             l2 += vhv;
           }

@@ -6,9 +6,7 @@
 
 namespace so100 {
 
-#ifndef SO100_NEWTON_WAVES
-#define SO100_NEWTON_WAVES 3
-#endif
+constexpr int kNewtonWaves = 3;   // waves per SIMD the register budget is sized for
 
 struct NewtonArgs {
   const DevModel* m;
@@ -19,7 +17,7 @@ struct NewtonArgs {
   int last;                      // last substep of the env step: write the debug record
 };
 
-__global__ void __launch_bounds__(kThreads, SO100_NEWTON_WAVES) so100_newton_kernel(NewtonArgs a) {
+__global__ void __launch_bounds__(kThreads, kNewtonWaves) so100_newton_kernel(NewtonArgs a) {
   const int tid = threadIdx.x, grp = tid >> 4, lane = tid & 15;
   const int env = blockIdx.x * kEnvsPerBlock + grp;
   const bool valid = env < a.n;

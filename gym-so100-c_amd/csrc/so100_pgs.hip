@@ -18,9 +18,7 @@
 
 namespace so100 {
 
-#ifndef SO100_PGS_WAVES
-#define SO100_PGS_WAVES 3        // waves per SIMD the register budget is sized for
-#endif
+constexpr int kPgsWaves = 3;         // waves per SIMD the register budget is sized for
 
 struct PgsArgs {
   const DevModel* m;
@@ -101,7 +99,7 @@ DEV void contact_update(const float4 (&v)[kBlk], const float4 (&J)[3], float (&q
 
 }
 
-__global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs a) {
+__global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
   __shared__ float4 blk[kResident][kPgsEnvs][kBlk];
   const DevModel* __restrict__ m = a.m;
   const int tid = threadIdx.x;
@@ -114,9 +112,6 @@ __global__ void __launch_bounds__(64, SO100_PGS_WAVES) so100_pgs_kernel(PgsArgs 
   if ((int)blockIdx.x < a.nheavy_slots) {
     const int cnt = min(a.w.hcount[a.par], kHeavyCap);
     if ((int)blockIdx.x >= cnt) return;
-#ifdef SO100_EXPERIMENT_SKIP_HEAVY
-    return;   // timing experiment only: heavy groups left unsolved
-#endif
     grp = a.w.hlist[a.par * kHeavyCap + blockIdx.x];
   } else {
     grp = blockIdx.x - a.nheavy_slots;
