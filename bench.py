@@ -71,6 +71,8 @@ def parse(argv=None):
                    help="constraint solver: newton (MuJoCo's default, which the reference runs; default) or pgs")
     p.add_argument("--convex", default="epa", choices=["epa", "mpr"],
                    help="mesh-pair collider: epa (GJK + EPA, MuJoCo 3.3.3's default; default) or mpr (libccd)")
+    p.add_argument("--dump-state", default="",
+                   help="test hook: each rank saves its shard's final state to <dir>/state_rank<r>.npz")
     return p.parse_args(argv)
 
 
@@ -146,8 +148,11 @@ def main(argv=None):
         # host-side barrier and MAX over ranks only: the env shards exchange nothing, so RCCL is never
         # initialised (north_star: no RCCL on the data path)
         dist.init_process_group("gloo", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU: rank -> device LOCAL_RANK.  SO100_BENCH_DEVICE (test hook only,
+    # tests/test_gpu_multirank.py) puts every rank on one device to rehearse the multi-rank path on one GPU.
+    device_index = int(os.environ.get("SO100_BENCH_DEVICE", local))
+    torch.cuda.set_device(device_index)
+    dev = torch.device("cuda", device_index)
 
     if args.envs_per_gpu > 0:
         count, offset = args.envs_per_gpu, rank * args.envs_per_gpu
@@ -162,9 +167,12 @@ def main(argv=None):
     env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset, solver=args.solver,
                       convex=args.convex)
     env.reset(seed=1000 + offset)   # env i <- RandomState(1000 + global id)
+    # the action pool is drawn for all `total` envs from one seed and sliced to this shard, so env i's actions
+    # (and its trajectory) do not depend on the number of ranks
     g = torch.Generator(device=dev)
-    g.manual_seed(args.seed * 1000003 + rank)
-    pool = [torch.rand(count, 6, generator=g, device=dev) * 2 - 1 for _ in range(args.action_pool)]
+    g.manual_seed(args.seed * 1000003)
+    pool = [(torch.rand(total, 6, generator=g, device=dev) * 2 - 1)[offset:offset + count].contiguous()
+            for _ in range(args.action_pool)]
     stream = torch.cuda.current_stream(dev)
 
     for i in range(args.warmup):
@@ -213,6 +221,12 @@ def main(argv=None):
 
     # sanity: the state stayed finite
     assert torch.isfinite(env.qpos).all().item(), "non-finite state after the benchmark"
+    if args.dump_state:
+        import numpy as np
+        os.makedirs(args.dump_state, exist_ok=True)
+        np.savez(os.path.join(args.dump_state, f"state_rank{rank}.npz"), offset=offset, count=count,
+                 qpos=env.qpos.cpu().numpy(), qvel=env.qvel.cpu().numpy(), obs=env.obs.cpu().numpy(),
+                 reward=env.reward.cpu().numpy(), episode=env.episode.cpu().numpy())
 
     if rank == 0:
         env_steps = total * args.steps

@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <exception>
+#include <new>
 #include <vector>
 #include "so100.h"
 #include "so100_device.h"
@@ -22,6 +24,7 @@ hipError_t launch_step(const DevModel*, int, int, int, int, Workspace&, const so
                        uint64_t, int, hipStream_t, hipEvent_t*);
 int fused_build(int n, int waves, bool debug);
 hipError_t launch_contact_count(const Workspace&, int, uint64_t*, hipStream_t);
+hipError_t launch_contact_counts(const Workspace&, int, int32_t*, hipStream_t);
 hipError_t launch_render(const DevModel*, const float4*, const int*, const uint32_t*, int, const float*,
                          const uint8_t*, const so100_camera&, int, int, int, uint8_t*, hipStream_t);
 hipError_t alloc_workspace(int, Workspace*);
@@ -211,14 +214,15 @@ static void profile_free(so100_env* env) {
   env->prof_cap = env->prof_used = 0;
 }
 
-static thread_local std::string g_err;
+// the last error of this thread: a fixed buffer, so reporting an error never allocates (or throws)
+static thread_local char g_err[512];
 
 static int fail(const char* msg) {
-  g_err = msg;
+  snprintf(g_err, sizeof(g_err), "%s", msg);
   return -1;
 }
 static int fail_hip(const char* where, hipError_t e) {
-  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  snprintf(g_err, sizeof(g_err), "%s: %s", where, hipGetErrorString(e));
   return -2;
 }
 
@@ -441,6 +445,9 @@ int build_device_model(const so100_model* s, DevModel* d) {
     }
   }
   for (int p = 0; p < SO100_NPAIR; p++) {
+    // geoms: 0 <= g < SO100_NGEOM, or a hull -1 - k with 0 <= k < SO100_NHULL_ALL
+    for (int g : {s->pair_geom1[p], s->pair_geom2[p]})
+      if (g >= SO100_NGEOM || (g < 0 && -1 - g >= SO100_NHULL_ALL)) return fail("model: pair geom out of range");
     d->pair_g1[p] = s->pair_geom1[p];
     d->pair_g2[p] = s->pair_geom2[p];
     solref_kb(s->pair_solref[p], s->pair_solimp[p], s->timestep, &K, &B);
@@ -465,6 +472,10 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->pair_rot[p] = (float)(s->body_invweight0[b1][1] + s->body_invweight0[b2][1]);
   }
   for (int k = 0; k < SO100_NHULL_ALL; k++) {
+    // the convex collider's support ids hold a vertex index in 10 bits (so100_convex.h sup_from_id)
+    if (s->hull_start[k] < 0 || s->hull_count[k] < 1 || s->hull_count[k] > 1024 ||
+        s->hull_start[k] + s->hull_count[k] > SO100_HULL_NVERT)
+      return fail("model: hull vertex range out of bounds (at most 1024 vertices per hull)");
     d->hull_body[k] = s->hull_body[k];
     d->hull_start[k] = s->hull_start[k];
     d->hull_count[k] = s->hull_count[k];
@@ -527,10 +538,25 @@ int build_device_model(const so100_model* s, DevModel* d) {
 }
 }  // namespace
 
-extern "C" {
+// Every exported entry point runs its implementation inside try / catch: host-side allocations (std::vector, new)
+// can throw std::bad_alloc, and no C++ exception may cross the C-ABI (include/so100.h).  The error becomes status
+// -3 (NULL for so100_create) with the message in so100_last_error().
+static int caught(const char* where) {
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    snprintf(g_err, sizeof(g_err), "%s: out of host memory", where);
+  } catch (const std::exception& e) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", where, e.what());
+  } catch (...) {
+    snprintf(g_err, sizeof(g_err), "%s: unknown C++ exception", where);
+  }
+  return -3;
+}
 
-int so100_abi_version(void) { return SO100_ABI_VERSION; }
-const char* so100_last_error(void) { return g_err.c_str(); }
+
+static int so100_abi_version_impl(void) { return SO100_ABI_VERSION; }
+static const char* so100_last_error_impl(void) { return g_err; }
 
 // ---- support-direction cells of the hulls (so100_hull_cells, include/so100.h).  For each cube-map cell
 // (face f: axis f / 2, sign f % 2; cell (cu, cv) of u = n_a / |n_axis|, v = n_b / |n_axis|, a < b the other
@@ -604,7 +630,7 @@ static void hull_cells_build(const so100_model* s, std::vector<uint32_t>& cells,
   }
 }
 
-int so100_hull_cells(const so100_model* model, uint32_t* cells, float* cand, int cap) {
+static int so100_hull_cells_impl(const so100_model* model, uint32_t* cells, float* cand, int cap) {
   if (!model) return fail("so100_hull_cells: model is NULL");
   for (int k = 0; k < SO100_NHULL_ALL; k++)
     if (model->hull_start[k] < 0 || model->hull_count[k] < 1 || model->hull_start[k] + model->hull_count[k] > SO100_HULL_NVERT)
@@ -621,13 +647,13 @@ int so100_hull_cells(const so100_model* model, uint32_t* cells, float* cand, int
   return nc;
 }
 
-int so100_struct_sizes(int* model_bytes, int* buffers_bytes) {
+static int so100_struct_sizes_impl(int* model_bytes, int* buffers_bytes) {
   if (model_bytes) *model_bytes = (int)sizeof(so100_model);
   if (buffers_bytes) *buffers_bytes = (int)sizeof(so100_buffers);
   return 0;
 }
 
-so100_env* so100_create(const so100_model* model, int n_envs, int device) {
+static so100_env* so100_create_impl(const so100_model* model, int n_envs, int device) {
   if (!model) { fail("so100_create: model is NULL"); return nullptr; }
   if (n_envs <= 0) { fail("so100_create: n_envs must be > 0"); return nullptr; }
   int ndev = 0;
@@ -674,9 +700,12 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
     const int w = atoi(v);
     env->fused_waves = (w == 2 || w == 3) ? w : 0;
   }
-  e = make_chunks(env, default_chunks(n_envs));
+  // the split path's per-chunk workspaces (solver records) are allocated when the split path is first used
+  // (here for PGS or a split default; else by so100_set_step_mode): each holds every env's whole contact list
+  if (!step_is_fused(env)) e = make_chunks(env, default_chunks(n_envs));
   if (e == hipSuccess && env->solver == SO100_SOLVER_NEWTON) {
-    // the fused launches: the record header (only its contact counts are written) and the wave order
+    // the fused launches: the record header (only its contact counts are written), the wave order, and the
+    // contact record of the contacts beyond the kMaxCon held on chip
     e = so100::alloc_fused_workspace(n_envs, &env->fws);
   }
   if (e != hipSuccess) {
@@ -690,7 +719,7 @@ so100_env* so100_create(const so100_model* model, int n_envs, int device) {
   return env;
 }
 
-int so100_destroy(so100_env* env) {
+static int so100_destroy_impl(so100_env* env) {
   if (!env) return 0;
   DeviceGuard g(env->device);
   profile_free(env);
@@ -709,9 +738,9 @@ int so100_destroy(so100_env* env) {
   return e == hipSuccess ? 0 : fail_hip("so100_destroy", e);
 }
 
-int so100_num_envs(const so100_env* env) { return env ? env->n : -1; }
+static int so100_num_envs_impl(const so100_env* env) { return env ? env->n : -1; }
 
-int so100_configure(so100_env* env, int task, int max_episode_steps, uint64_t base_seed, int env_offset) {
+static int so100_configure_impl(so100_env* env, int task, int max_episode_steps, uint64_t base_seed, int env_offset) {
   if (!env) return fail("so100_configure: env is NULL");
   if (task < SO100_TASK_CUBE_TO_BIN || task > SO100_TASK_GOAL) return fail("so100_configure: unknown task");
   env->task = task;
@@ -729,7 +758,7 @@ static int check_state(const so100_buffers* b) {
   return 0;
 }
 
-int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, const uint32_t* seeds, void* stream) {
+static int so100_reset_impl(so100_env* env, const so100_buffers* b, const uint8_t* mask, const uint32_t* seeds, void* stream) {
   if (!env) return fail("so100_reset: env is NULL");
   if (check_state(b)) return -1;
   if (env->task == SO100_TASK_GOAL && !b->desired_goal) return fail("so100_reset: GoalEnv needs desired_goal");
@@ -748,6 +777,7 @@ static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags
     return so100::launch_step(env->d_model, env->nsubstep, env->solver, 1, env->fused_waves, env->fws, *b, env->n, env->task, flags,
                               env->max_steps, env->base_seed, env->env_offset, s, ev);
   }
+  if (env->chunks.empty()) return hipErrorNotReady;      // (so100_set_step_mode allocates them)
   if (env->chunks.size() == 1) {
     Chunk& c = env->chunks[0];
     return so100::launch_step(env->d_model, env->nsubstep, env->solver, 0, 0, c.ws, *b, c.count, env->task, flags, env->max_steps,
@@ -771,8 +801,13 @@ static hipError_t enqueue_step(so100_env* env, const so100_buffers* b, int flags
 }
 
 // Capture the step for (b, flags) on the private capture stream and instantiate it into g.
+// the split path's substep-counter parity (its PGS heavy-group lists alternate by it); the fused step has none
+static uint32_t step_parity(const so100_env* env) {
+  return (step_is_fused(env) || env->chunks.empty()) ? 0u : env->chunks[0].ws.sub_count & 1u;
+}
+
 static hipError_t build_step_graph(so100_env* env, const so100_buffers* b, int flags, StepGraph& g) {
-  const uint32_t par = env->chunks[0].ws.sub_count & 1u;
+  const uint32_t par = step_parity(env);
   hipError_t e = hipSuccess;
   if (!env->cap_s) e = hipStreamCreateWithFlags(&env->cap_s, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&g.done, hipEventDisableTiming);
@@ -794,7 +829,7 @@ static hipError_t build_step_graph(so100_env* env, const so100_buffers* b, int f
 
 // Replay the step graph for (b, flags) on s, capturing it first if it is not cached.
 static hipError_t graph_step(so100_env* env, const so100_buffers* b, int flags, hipStream_t s) {
-  const uint32_t par = env->chunks[0].ws.sub_count & 1u;
+  const uint32_t par = step_parity(env);
   StepGraph* hit = nullptr;
   for (StepGraph& g : env->graphs)
     if (g.flags == flags && g.par == par && memcmp(&g.buf, b, sizeof(so100_buffers)) == 0) { hit = &g; break; }
@@ -822,7 +857,7 @@ static hipError_t graph_step(so100_env* env, const so100_buffers* b, int flags, 
   return e;
 }
 
-int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) {
+static int so100_step_impl(so100_env* env, const so100_buffers* b, int flags, void* stream) {
   if (!env) return fail("so100_step: env is NULL");
   if (check_state(b)) return -1;
   if (!b->action) return fail("so100_step: action is NULL");
@@ -842,7 +877,7 @@ int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) 
   return e == hipSuccess ? 0 : fail_hip("so100_step", e);
 }
 
-int so100_profile_enable(so100_env* env, int max_steps) {
+static int so100_profile_enable_impl(so100_env* env, int max_steps) {
   if (!env) return fail("so100_profile_enable: env is NULL");
   if (max_steps < 0) return fail("so100_profile_enable: max_steps < 0");
   DeviceGuard g(env->device);
@@ -858,7 +893,7 @@ int so100_profile_enable(so100_env* env, int max_steps) {
   return 0;
 }
 
-int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms, int* stage_launches) {
+static int so100_profile_read_impl(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms, int* stage_launches) {
   if (!env || !solver_ms || !solver_launches || !stage_ms || !stage_launches) return fail("so100_profile_read: bad arguments");
   DeviceGuard g(env->device);
   *solver_ms = *stage_ms = 0.0;
@@ -889,22 +924,32 @@ int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, 
   return 0;
 }
 
-int so100_set_step_mode(so100_env* env, int fused) {
+static int so100_set_step_mode_impl(so100_env* env, int fused) {
   if (!env) return fail("so100_set_step_mode: env is NULL");
   if (fused < -1 || fused > 1) return fail("so100_set_step_mode: mode must be -1 (auto), 0 (split) or 1 (fused)");
   if (env->prof_cap > 0) return fail("so100_set_step_mode: disable profiling first");
   DeviceGuard g(env->device);
   graph_free(env);                     // captured graphs hold the other mode's launches
+  const int prev = env->fused;
   env->fused = fused;
+  if (!step_is_fused(env) && env->chunks.empty()) {
+    // first use of the split path: its chunk workspaces (one synchronising allocation, here, never in a step)
+    hipError_t e = make_chunks(env, default_chunks(env->n));
+    if (e != hipSuccess) {
+      (void)free_chunks(env);
+      env->fused = prev;
+      return fail_hip("so100_set_step_mode: split workspace", e);
+    }
+  }
   return 0;
 }
 
-int so100_step_mode(const so100_env* env) {
+static int so100_step_mode_impl(const so100_env* env) {
   if (!env) return fail("so100_step_mode: env is NULL");
   return step_is_fused(env) ? 1 : 0;
 }
 
-int so100_set_fused_build(so100_env* env, int waves) {
+static int so100_set_fused_build_impl(so100_env* env, int waves) {
   if (!env) return fail("so100_set_fused_build: env is NULL");
   if (waves != 0 && waves != 2 && waves != 3) return fail("so100_set_fused_build: waves must be 0 (auto), 2 or 3");
   if (env->prof_cap > 0) return fail("so100_set_fused_build: disable profiling first");
@@ -914,13 +959,13 @@ int so100_set_fused_build(so100_env* env, int waves) {
   return 0;
 }
 
-int so100_fused_build(const so100_env* env, int debug) {
+static int so100_fused_build_impl(const so100_env* env, int debug) {
   if (!env) return fail("so100_fused_build: env is NULL");
   DeviceGuard g(env->device);
   return so100::fused_build(env->n, env->fused_waves, debug != 0);
 }
 
-int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs) {
+static int so100_chunk_info_impl(const so100_env* env, int* nchunks, int* profiled_envs) {
   if (!env) return fail("so100_chunk_info: env is NULL");
   if (nchunks) *nchunks = (int)env->chunks.size();
   if (step_is_fused(env)) {     // one launch over all envs
@@ -928,11 +973,12 @@ int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs) {
     if (profiled_envs) *profiled_envs = env->n;
     return 0;
   }
+  if (nchunks && env->chunks.empty()) *nchunks = default_chunks(env->n);
   if (profiled_envs) *profiled_envs = env->chunks.empty() ? 0 : env->chunks[0].count;
   return 0;
 }
 
-int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
+static int so100_contact_count_impl(so100_env* env, uint64_t* accum, void* stream) {
   if (!env || !accum) return fail("so100_contact_count: bad arguments");
   DeviceGuard g(env->device);
   hipError_t e = hipSuccess;
@@ -945,7 +991,20 @@ int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
   return e == hipSuccess ? 0 : fail_hip("so100_contact_count", e);
 }
 
-int so100_goal_reward(so100_env* env, int n, const float* a, const float* d, float* out, void* stream) {
+static int so100_contact_counts_impl(so100_env* env, int32_t* out, void* stream) {
+  if (!env || !out) return fail("so100_contact_counts: bad arguments");
+  DeviceGuard g(env->device);
+  hipError_t e = hipSuccess;
+  if (env->last_fused) {
+    if (env->fws.hdr) e = so100::launch_contact_counts(env->fws, env->n, out, (hipStream_t)stream);
+  } else {
+    for (const Chunk& c : env->chunks)
+      if (e == hipSuccess) e = so100::launch_contact_counts(c.ws, c.count, out + c.start, (hipStream_t)stream);
+  }
+  return e == hipSuccess ? 0 : fail_hip("so100_contact_counts", e);
+}
+
+static int so100_goal_reward_impl(so100_env* env, int n, const float* a, const float* d, float* out, void* stream) {
   if (!env || !a || !d || !out || n < 0) return fail("so100_goal_reward: bad arguments");
   if (n == 0) return 0;
   DeviceGuard g(env->device);
@@ -953,7 +1012,7 @@ int so100_goal_reward(so100_env* env, int n, const float* a, const float* d, flo
   return e == hipSuccess ? 0 : fail_hip("so100_goal_reward", e);
 }
 
-int so100_eval_reward(so100_env* env, int task, int n, const float* cube, const float* ee, const uint32_t* bits,
+static int so100_eval_reward_impl(so100_env* env, int task, int n, const float* cube, const float* ee, const uint32_t* bits,
                       float* out, void* stream) {
   if (!env || !cube || !ee || !bits || !out || n < 0) return fail("so100_eval_reward: bad arguments");
   if (task < SO100_TASK_CUBE_TO_BIN || task > SO100_TASK_GOAL) return fail("so100_eval_reward: unknown task");
@@ -963,7 +1022,7 @@ int so100_eval_reward(so100_env* env, int task, int n, const float* cube, const 
   return e == hipSuccess ? 0 : fail_hip("so100_eval_reward", e);
 }
 
-int so100_spawn_pose(so100_env* env, int n, const uint32_t* seeds, double* pose, void* stream) {
+static int so100_spawn_pose_impl(so100_env* env, int n, const uint32_t* seeds, double* pose, void* stream) {
   if (!env || !seeds || !pose || n < 0) return fail("so100_spawn_pose: bad arguments");
   if (n == 0) return 0;
   DeviceGuard g(env->device);
@@ -971,7 +1030,7 @@ int so100_spawn_pose(so100_env* env, int n, const uint32_t* seeds, double* pose,
   return e == hipSuccess ? 0 : fail_hip("so100_spawn_pose", e);
 }
 
-int so100_unnormalize(so100_env* env, int n, const float* action, float* ctrl, void* stream) {
+static int so100_unnormalize_impl(so100_env* env, int n, const float* action, float* ctrl, void* stream) {
   if (!env || !action || !ctrl || n < 0) return fail("so100_unnormalize: bad arguments");
   if (n == 0) return 0;
   DeviceGuard g(env->device);
@@ -980,7 +1039,7 @@ int so100_unnormalize(so100_env* env, int n, const float* action, float* ctrl, v
 }
 
 
-int so100_render_mesh(so100_env* env, const float* tri, const int* body, const float* rgb, int ntri) {
+static int so100_render_mesh_impl(so100_env* env, const float* tri, const int* body, const float* rgb, int ntri) {
   if (!env || !tri || !body || !rgb || ntri <= 0) return fail("so100_render_mesh: bad arguments");
   std::vector<float4> t((size_t)ntri * 3);
   std::vector<uint32_t> c((size_t)ntri);
@@ -1013,7 +1072,7 @@ int so100_render_mesh(so100_env* env, const float* tri, const int* body, const f
   return 0;
 }
 
-int so100_render(so100_env* env, const float* qpos, const uint8_t* mask, const so100_camera* cam, int width,
+static int so100_render_impl(so100_env* env, const float* qpos, const uint8_t* mask, const so100_camera* cam, int width,
                  int height, uint8_t* out, void* stream) {
   if (!env || !qpos || !cam || !out) return fail("so100_render: bad arguments");
   if (env->r_ntri <= 0) return fail("so100_render: no render mesh (so100_render_mesh)");
@@ -1025,6 +1084,206 @@ int so100_render(so100_env* env, const float* qpos, const uint8_t* mask, const s
   hipError_t e = so100::launch_render(env->d_model, env->r_tri, env->r_body, env->r_rgb, env->r_ntri, qpos, mask, *cam,
                                       env->n, width, height, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : fail_hip("so100_render", e);
+}
+
+
+extern "C" {
+
+int so100_abi_version(void) {
+  try {
+    return so100_abi_version_impl();
+  } catch (...) {
+    return caught("so100_abi_version");
+  }
+}
+
+const char* so100_last_error(void) { return so100_last_error_impl(); }
+
+int so100_hull_cells(const so100_model* model, uint32_t* cells, float* cand, int cap) {
+  try {
+    return so100_hull_cells_impl(model, cells, cand, cap);
+  } catch (...) {
+    return caught("so100_hull_cells");
+  }
+}
+
+int so100_struct_sizes(int* model_bytes, int* buffers_bytes) {
+  try {
+    return so100_struct_sizes_impl(model_bytes, buffers_bytes);
+  } catch (...) {
+    return caught("so100_struct_sizes");
+  }
+}
+
+so100_env* so100_create(const so100_model* model, int n_envs, int device) {
+  try {
+    return so100_create_impl(model, n_envs, device);
+  } catch (...) {
+    caught("so100_create");
+    return nullptr;
+  }
+}
+
+int so100_destroy(so100_env* env) {
+  try {
+    return so100_destroy_impl(env);
+  } catch (...) {
+    return caught("so100_destroy");
+  }
+}
+
+int so100_num_envs(const so100_env* env) {
+  try {
+    return so100_num_envs_impl(env);
+  } catch (...) {
+    return caught("so100_num_envs");
+  }
+}
+
+int so100_configure(so100_env* env, int task, int max_episode_steps, uint64_t base_seed, int env_offset) {
+  try {
+    return so100_configure_impl(env, task, max_episode_steps, base_seed, env_offset);
+  } catch (...) {
+    return caught("so100_configure");
+  }
+}
+
+int so100_reset(so100_env* env, const so100_buffers* b, const uint8_t* mask, const uint32_t* seeds, void* stream) {
+  try {
+    return so100_reset_impl(env, b, mask, seeds, stream);
+  } catch (...) {
+    return caught("so100_reset");
+  }
+}
+
+int so100_step(so100_env* env, const so100_buffers* b, int flags, void* stream) {
+  try {
+    return so100_step_impl(env, b, flags, stream);
+  } catch (...) {
+    return caught("so100_step");
+  }
+}
+
+int so100_profile_enable(so100_env* env, int max_steps) {
+  try {
+    return so100_profile_enable_impl(env, max_steps);
+  } catch (...) {
+    return caught("so100_profile_enable");
+  }
+}
+
+int so100_profile_read(so100_env* env, double* solver_ms, int* solver_launches, double* stage_ms, int* stage_launches) {
+  try {
+    return so100_profile_read_impl(env, solver_ms, solver_launches, stage_ms, stage_launches);
+  } catch (...) {
+    return caught("so100_profile_read");
+  }
+}
+
+int so100_set_step_mode(so100_env* env, int fused) {
+  try {
+    return so100_set_step_mode_impl(env, fused);
+  } catch (...) {
+    return caught("so100_set_step_mode");
+  }
+}
+
+int so100_step_mode(const so100_env* env) {
+  try {
+    return so100_step_mode_impl(env);
+  } catch (...) {
+    return caught("so100_step_mode");
+  }
+}
+
+int so100_set_fused_build(so100_env* env, int waves) {
+  try {
+    return so100_set_fused_build_impl(env, waves);
+  } catch (...) {
+    return caught("so100_set_fused_build");
+  }
+}
+
+int so100_fused_build(const so100_env* env, int debug) {
+  try {
+    return so100_fused_build_impl(env, debug);
+  } catch (...) {
+    return caught("so100_fused_build");
+  }
+}
+
+int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs) {
+  try {
+    return so100_chunk_info_impl(env, nchunks, profiled_envs);
+  } catch (...) {
+    return caught("so100_chunk_info");
+  }
+}
+
+int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
+  try {
+    return so100_contact_count_impl(env, accum, stream);
+  } catch (...) {
+    return caught("so100_contact_count");
+  }
+}
+
+int so100_contact_counts(so100_env* env, int32_t* out, void* stream) {
+  try {
+    return so100_contact_counts_impl(env, out, stream);
+  } catch (...) {
+    return caught("so100_contact_counts");
+  }
+}
+
+int so100_goal_reward(so100_env* env, int n, const float* a, const float* d, float* out, void* stream) {
+  try {
+    return so100_goal_reward_impl(env, n, a, d, out, stream);
+  } catch (...) {
+    return caught("so100_goal_reward");
+  }
+}
+
+int so100_eval_reward(so100_env* env, int task, int n, const float* cube, const float* ee, const uint32_t* bits,
+                      float* out, void* stream) {
+  try {
+    return so100_eval_reward_impl(env, task, n, cube, ee, bits, out, stream);
+  } catch (...) {
+    return caught("so100_eval_reward");
+  }
+}
+
+int so100_spawn_pose(so100_env* env, int n, const uint32_t* seeds, double* pose, void* stream) {
+  try {
+    return so100_spawn_pose_impl(env, n, seeds, pose, stream);
+  } catch (...) {
+    return caught("so100_spawn_pose");
+  }
+}
+
+int so100_unnormalize(so100_env* env, int n, const float* action, float* ctrl, void* stream) {
+  try {
+    return so100_unnormalize_impl(env, n, action, ctrl, stream);
+  } catch (...) {
+    return caught("so100_unnormalize");
+  }
+}
+
+int so100_render_mesh(so100_env* env, const float* tri, const int* body, const float* rgb, int ntri) {
+  try {
+    return so100_render_mesh_impl(env, tri, body, rgb, ntri);
+  } catch (...) {
+    return caught("so100_render_mesh");
+  }
+}
+
+int so100_render(so100_env* env, const float* qpos, const uint8_t* mask, const so100_camera* cam, int width,
+                 int height, uint8_t* out, void* stream) {
+  try {
+    return so100_render_impl(env, qpos, mask, cam, width, height, out, stream);
+  } catch (...) {
+    return caught("so100_render");
+  }
 }
 
 }  // extern "C"

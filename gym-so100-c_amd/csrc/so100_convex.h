@@ -1007,10 +1007,10 @@ DEV float4 sphere_obj(const DevModel* __restrict__ m, const EnvShared& sh, int o
 //    pair of the wave's union per round, on the rows holding it: 60 % of the slowest waves' assembly);
 //  * each round's hits go to their env's staging slots in list order, so each env keeps its pair order.
 // The candidate lists are the pairs passing both stages, in pair order, as before: the same contacts.
-// Returns the env's number of MPR contacts (uniform across its row; those beyond kMaxCon are not staged and
-// count as dropped).
+// Returns the env's number of convex contacts (uniform across its row).  Staged contacts j >= kMaxCon go to the
+// env's HBM contact record (slot j, kMprStageOff; crec0: the record of the wave's first env).
 template <bool kCells>
-DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, int grp, bool valid) {
+DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec0, int lane, int grp, bool valid) {
   constexpr int kConvex = SO100_NPAIR_CONVEX;
   constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 8
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
@@ -1129,17 +1129,23 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, int lane, i
       const bool h = it < total && ((hb >> (16 * g)) & 1ull);
       if (g < grp && h && env_of(it) == ie) slot++;
     }
-    if (hit && lane == 0 && slot < kMaxCon) {
+    if (hit && lane == 0) {
       const int k = -1 - m->pair_g2[p];
       float RH[9], pH[3], wn[3], wp[3];
       hull_frame(m, shm[ie], m->hull_body[k], RH, pH);
       mulmv3(wn, RH, dir);
       mulmv3(wp, RH, pos);
-      MprStage& st = shm[ie].mpr[slot];
-      st.pos[0] = wp[0] + pH[0]; st.pos[1] = wp[1] + pH[1];
-      st.pos[2] = wp[2] + pH[2]; st.pos[3] = -depth;
-      st.nrm[0] = wn[0]; st.nrm[1] = wn[1]; st.nrm[2] = wn[2];
-      st.nrm[3] = __int_as_float(p);
+      const float4 sp = make_float4(wp[0] + pH[0], wp[1] + pH[1], wp[2] + pH[2], -depth);
+      const float4 sn = make_float4(wn[0], wn[1], wn[2], __int_as_float(p));
+      if (slot < kMaxCon) {
+        MprStage& st = shm[ie].mpr[slot];
+        st.pos[0] = sp.x; st.pos[1] = sp.y; st.pos[2] = sp.z; st.pos[3] = sp.w;
+        st.nrm[0] = sn.x; st.nrm[1] = sn.y; st.nrm[2] = sn.z; st.nrm[3] = sn.w;
+      } else {                                // rare: the env's staging beyond kMaxCon, in its HBM record
+        float4* stg = reinterpret_cast<float4*>(crec0 + (size_t)ie * kConEnv + (size_t)slot * kConStride + kMprStageOff);
+        stg[0] = sp;
+        stg[1] = sn;
+      }
     }
 #pragma unroll
     for (int g = 0; g < kEnvsPerBlock; g++) {

@@ -11,7 +11,8 @@ constexpr int kLanes = 16;            // lanes per env ("env lane-group" = one D
 constexpr int kEnvsPerBlock = 4;      // one wave64 per workgroup
 constexpr int kThreads = kLanes * kEnvsPerBlock;
 constexpr int kNArm = SO100_NHINGE;
-constexpr int kMaxCon = SO100_MAXCON;
+constexpr int kMaxCon = SO100_MAXCON;     // contacts an env holds on chip (lane c of its row owns contact c)
+constexpr int kConCap = SO100_NCON_MAX;   // the env's whole contact list: every pair at its collider's maximum
 
 constexpr int kCellBlk = 16;   // candidates per support cell block (DevModel::hull_blk): one per lane of a row
 struct DevModel {
@@ -122,7 +123,9 @@ struct DevModel {
 // the constraint rows, the PGS kernel (4 lanes per env, 3 dofs per lane) solves them.  The hand-off
 // is a per-env record in HBM, laid out for the solver's lanes:
 //   hdr[env][q][kHdrLane]  lane q owns dofs 3q..3q+2 (q = 0,1: arm, q = 2,3: cube)
-//   con[env][c][kConRec]   solver block (kBlk float4) then J[dof][row] (12 x 4 floats)
+//   con[env][c][kConStride] for every contact c < kConCap: solver block (kBlk float4), J[dof][row] (12 x 4
+//                           floats), then (contacts c >= kMaxCon only) the contact's geometry
+// The fused step uses the same per-env contact record for the contacts beyond the kMaxCon it holds on chip.
 constexpr int kHdrLane = 40;
 constexpr int kHdrEnv = 4 * kHdrLane;
 // Solver block of one contact, read by the PGS as kBlk x ds_read_b128 (float index: content):
@@ -136,6 +139,17 @@ constexpr int kBlkAref = 8;       // float4 slots
 constexpr int kBlkF = 9;
 constexpr int kJOff = 4 * kBlk;   // float offset of the J rows in the record
 constexpr int kConRec = kJOff + 48;
+// Contacts c >= kMaxCon (the rest of the list, which does not fit on chip): their geometry follows J in the
+// record slot (ConGeom: pos + dist, frame; then the pair id as int bits and the dist), and the Newton solve
+// keeps its per-contact state in the block's floats 12..23 (jar at the iterate, J s, force); the convex
+// collider stages such contacts in floats 24..31 (dead from the compaction on)
+constexpr int kGeoOff = kConRec;            // 16 floats: pos[4] (pos[3] = dist), frame[12]
+constexpr int kGeoPair = kGeoOff + 16;      // pair index (int bits)
+constexpr int kGeoDist = kGeoOff + 17;
+constexpr int kConStride = kGeoOff + 24;    // 112 floats = 448 B per contact slot
+constexpr int kOvfJc = 12, kOvfJs = 16, kOvfF = 20;   // Newton overflow state (floats of the block)
+constexpr int kMprStageOff = 24;            // convex-collider staging (MprStage) of staged contacts >= kMaxCon
+constexpr size_t kConEnv = (size_t)kConCap * kConStride;   // floats per env
 enum HdrField : int {
   H_QACC = 0,       // qacc at the solver start (qacc_smooth, plus M^-1 J' f of the kept warmstart)
   H_FRAREF = 3,     // frictionloss rows: aref = -B vel

@@ -17,12 +17,17 @@
 //   * every dof lane holds J of its dof for contacts 0..kJReg-1 (one float4 per contact), so J x is a DPP
 //     row reduction and J' f, J' H J come from DPP row broadcasts.  Contacts kJReg.. (rare: 0.4 % of envs
 //     have more than 4) keep J in LDS (NewtonRows.jx) and take rolled loops with LDS broadcast reads and
-//     ds_bpermute row shuffles: 32 fewer VGPRs, which the fused kernel needs for 3 waves per SIMD.
+//     ds_bpermute row shuffles: 32 fewer VGPRs, which the fused kernel needs for 3 waves per SIMD;
+//   * contacts kMaxCon.. (the list holds every contact, up to kConCap; beyond 16 is rare, a jaw jammed into
+//     the bin walls) live in the env's HBM contact record, in blocks of 16 (lane k owns contact kMaxCon + 16 b
+//     + k): J, aref / R / cone coefficients, and the solve's per-contact state (jar, J s, force), read back
+//     through L2 in rolled loops behind wave-uniform branches that the common case skips.
 //
 // The problem arrives as NewtonRows, one lane's share of it.  The fused step kernel (so100_step.hip
 // so100_fused_kernel) hands it over in registers from the assembly of the same wave; the split path
 // stores it in the HBM record (so100_device.h NewtonHdr) and so100_newton_kernel loads it back.
 #pragma once
+#include "so100.h"
 #include "so100_common.h"
 
 namespace so100 {
@@ -138,6 +143,54 @@ DEV float mul_m(const float* mrow, float mcd, float x) {
   for (int j = 0; j < 6; j++) acc += mrow[j] * bcast_row(x, j);
   return acc;
 }
+// ---------------------------------------------------------------- contacts beyond kMaxCon (the HBM record)
+// slot of contact c in the env's contact record (so100_device.h: kConStride floats per contact)
+DEV float* ovf_slot(float* crec, int c) { return crec + (size_t)c * kConStride; }
+// J of contact c >= kMaxCon for dof `lane` (0 on the non-dof lanes and beyond the env's ncon: slots past the
+// env's own contacts hold an earlier substep's rows)
+DEV float4 ovf_j(const float* crec, int c, int lane, int ncon) {
+  return (lane < SO100_NV && c < ncon) ? reinterpret_cast<const float4*>(crec + (size_t)c * kConStride + kJOff)[lane]
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// contact c's Newton data from its record slot (as the resident contacts' NewtonRows fields: aref, D = 1 / R, the
+// cone's mu, friction coefficients and middle-zone Dm)
+struct OvfCon {
+  float aref[4], D[4], mu, fr0, fr1, Dm;
+};
+DEV void ovf_load(const float* slot, OvfCon& o) {
+  const float4 a = reinterpret_cast<const float4*>(slot)[0], R = reinterpret_cast<const float4*>(slot)[1];
+  const float4 u = reinterpret_cast<const float4*>(slot)[2];
+  o.aref[0] = a.x; o.aref[1] = a.y; o.aref[2] = a.z; o.aref[3] = a.w;
+  o.D[0] = 1.f / R.x; o.D[1] = 1.f / R.y; o.D[2] = 1.f / R.z; o.D[3] = 1.f / R.w;
+  o.mu = u.x; o.fr0 = u.y; o.fr1 = u.z;
+  o.Dm = o.D[0] / (o.mu * o.mu * (1.f + o.mu * o.mu));
+}
+DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+DEV void st4(float* p, const float* v) { *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]); }
+// J x of the block of contacts b0 .. b0 + 15 on their owning lanes k = c - b0
+DEV float4 ovf_rows(const float* crec, int b0, float x, int lane, int ncon, int ncon_max) {
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+  for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
+    const float4 j = ovf_j(crec, b0 + k, lane, ncon);
+    const float a0 = rowsum16(j.x * x), a1 = rowsum16(j.y * x), a2 = rowsum16(j.z * x), a3 = rowsum16(j.w * x);
+    if (lane == k) r = make_float4(a0, a1, a2, a3);
+  }
+  return r;
+}
+// J x (and J y) of the block of contacts b0 .. b0 + 15 on their owning lanes k = c - b0
+DEV void ovf_rows2(const float* crec, int b0, float x, float y, int lane, int ncon, int ncon_max, float4& rx, float4& ry) {
+  rx = make_float4(0.f, 0.f, 0.f, 0.f);
+  ry = rx;
+#pragma unroll 1
+  for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
+    const float4 j = ovf_j(crec, b0 + k, lane, ncon);
+    const float a0 = rowsum16(j.x * x), a1 = rowsum16(j.y * x), a2 = rowsum16(j.z * x), a3 = rowsum16(j.w * x);
+    const float c0 = rowsum16(j.x * y), c1 = rowsum16(j.y * y), c2 = rowsum16(j.z * y), c3 = rowsum16(j.w * y);
+    if (lane == k) { rx = make_float4(a0, a1, a2, a3); ry = make_float4(c0, c1, c2, c3); }
+  }
+}
+
 // J of contact c >= kJReg for this lane's dof (LDS; 0 on the non-dof lanes)
 DEV float4 jx_own(const NewtonRows& r, int c, int lane) {
   return lane < SO100_NV ? r.jx[(c - kJReg) * SO100_NV + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -158,7 +211,7 @@ DEV float4 contact_rows(const NewtonRows& rw, float x, int lane, int ncon_max) {
       if (lane == c) r = make_float4(v0, v1, v2, v3);
     }
   }
-  for (int c = kJReg; c < ncon_max; c++) {
+  for (int c = kJReg; c < ncon_max && c < kMaxCon; c++) {
     const float4 j = jx_own(rw, c, lane);
     const float v0 = rowsum16(j.x * x), v1 = rowsum16(j.y * x), v2 = rowsum16(j.z * x), v3 = rowsum16(j.w * x);
     if (lane == c) r = make_float4(v0, v1, v2, v3);
@@ -179,7 +232,7 @@ DEV void contact_rows2(const NewtonRows& rw, float x, float y, int lane, int nco
       if (lane == c) { rx = make_float4(a0, a1, a2, a3); ry = make_float4(b0, b1, b2, b3); }
     }
   }
-  for (int c = kJReg; c < ncon_max; c++) {
+  for (int c = kJReg; c < ncon_max && c < kMaxCon; c++) {
     const float4 j = jx_own(rw, c, lane);
     const float a0 = rowsum16(j.x * x), a1 = rowsum16(j.y * x), a2 = rowsum16(j.z * x), a3 = rowsum16(j.w * x);
     const float b0 = rowsum16(j.x * y), b1 = rowsum16(j.y * y), b2 = rowsum16(j.z * y), b3 = rowsum16(j.w * y);
@@ -201,9 +254,9 @@ DEV void newton_mass_store(const Workspace& w, int e, int lane, const NewtonRows
 }
 DEV void newton_rows_store(const Workspace& w, int e, int lane, const NewtonRows& r) {
   float* hd = w.hdr + (size_t)e * kHdrEnv;
-  float* crec = w.con + (size_t)e * kMaxCon * kConRec;
+  float* crec = w.con + (size_t)e * kConEnv;
   if (lane < r.ncon) {
-    float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
+    float4* cs = reinterpret_cast<float4*>(crec + lane * kConStride);
     cs[0] = r.c_aref;
     cs[1] = r.c_R;
     cs[2] = r.c_mu;
@@ -234,15 +287,15 @@ DEV void newton_rows_load(const Workspace& w, int e, int lane, bool valid, float
   ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
   ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
   ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
-  const float* __restrict__ crec = w.con + (size_t)e * kMaxCon * kConRec;
+  const float* __restrict__ crec = w.con + (size_t)e * kConEnv;
 #pragma unroll
   for (int c = 0; c < kJReg; c++) {
     r.J[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < ncon_max && c < r.ncon && dof) r.J[c] = reinterpret_cast<const float4*>(crec + c * kConRec + kJOff)[lane];
+    if (c < ncon_max && c < r.ncon && dof) r.J[c] = reinterpret_cast<const float4*>(crec + c * kConStride + kJOff)[lane];
   }
-  for (int c = kJReg; c < ncon_max; c++) {
+  for (int c = kJReg; c < ncon_max && c < kMaxCon; c++) {
     float4 j = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < r.ncon && dof) j = reinterpret_cast<const float4*>(crec + c * kConRec + kJOff)[lane];
+    if (c < r.ncon && dof) j = reinterpret_cast<const float4*>(crec + c * kConStride + kJOff)[lane];
     if (dof) jx[(c - kJReg) * SO100_NV + lane] = j;
   }
   r.jx = jx;
@@ -250,7 +303,7 @@ DEV void newton_rows_load(const Workspace& w, int e, int lane, bool valid, float
   r.c_R = make_float4(1.f, 1.f, 1.f, 1.f);
   r.c_mu = make_float4(1.f, 1.f, 1.f, 0.f);
   if (lane < r.ncon) {
-    const float4* cb = reinterpret_cast<const float4*>(crec + lane * kConRec);
+    const float4* cb = reinterpret_cast<const float4*>(crec + lane * kConStride);
     r.c_aref = cb[0];
     r.c_R = cb[1];
     r.c_mu = cb[2];
@@ -284,11 +337,32 @@ DEV void newton_diag_write(float* dbg, int lane, bool valid, float qacc, const N
   if (lane == 0) { dbg[1] = (float)d.iters; dbg[2] = d.impr; }
 }
 
+// The debug record's entries of the contacts beyond kMaxCon (include/so100.h SO100_DBG_STRIDE: from
+// SO100_DBG_OVF, 6 floats per contact: dist, pair, normal force, 3 friction forces), from the env's contact record
+// after the last solve: the forces at the final iterate's jar, as newton_diag_write's for the resident contacts.
+DEV void newton_diag_write_ovf(float* dbg, const float* crec, int ncon, int lane) {
+  for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
+    const float* sl = crec + (size_t)c * kConStride;
+    OvfCon o;
+    ovf_load(sl, o);
+    const float4 j4 = ld4(sl + kOvfJc);
+    const float x[4] = {j4.x, j4.y, j4.z, j4.w};
+    float cc, fo[4], ho[10];
+    cone_eval(x, o.D, o.Dm, o.mu, o.fr0, o.fr1, cc, fo, ho);
+    float* d = dbg + SO100_DBG_OVF + 6 * (c - kMaxCon);
+    d[0] = sl[kGeoDist];
+    d[1] = (float)__float_as_int(sl[kGeoPair]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[2 + k] = fo[k];
+  }
+}
+
 // Solve one env's substep problem (its 16 lanes); returns qacc on the dof lanes.  want_diag: fill diag, the
 // diagnostics for the debug row, written by the caller (the row's address is then not held live across
-// the solve).
+// the solve).  rec(): the env's HBM contact record (contacts >= kMaxCon), computed only where such contacts exist.
+template <class RecFn>
 DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, bool want_diag,
-                       NewtonDiag& diag) {
+                       NewtonDiag& diag, RecFn rec) {
   const bool dof = lane < SO100_NV;
   STAMP_DECL
   STAMP(-1);
@@ -339,9 +413,42 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     const float ew = warm - qs;
     const float mew = mul_m(mrow, mcd, ew);
     const float gw = 0.5f * rowsum16(dof ? ew * mew : 0.f);
-    const float cw = gw + rowsum16(rows_cost(warm - fr_aref, lim_s * warm - lim_aref, xw));
-    const float cs = rowsum16(rows_cost(qs - fr_aref, lim_s * qs - lim_aref, xs));
+    float cwl = rows_cost(warm - fr_aref, lim_s * warm - lim_aref, xw);
+    float csl = rows_cost(qs - fr_aref, lim_s * qs - lim_aref, xs);
+    if (ncon_max > kMaxCon) {
+      // contacts beyond kMaxCon: their jar at both candidates, the block's costs on the owning lanes; the
+      // candidates go to the record (the chosen one becomes the iterate's jar below)
+      float* crec = rec();
+      for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
+        float4 ow, os;
+        ovf_rows2(crec, b0, warm, qs, lane, ncon, ncon_max, ow, os);
+        const int c = b0 + lane;
+        if (c < ncon) {
+          float* sl = ovf_slot(crec, c);
+          OvfCon o;
+          ovf_load(sl, o);
+          const float yw[4] = {ow.x - o.aref[0], ow.y - o.aref[1], ow.z - o.aref[2], ow.w - o.aref[3]};
+          const float ys[4] = {os.x - o.aref[0], os.y - o.aref[1], os.z - o.aref[2], os.w - o.aref[3]};
+          float cc, fc[4], hc[10];
+          cone_eval(yw, o.D, o.Dm, o.mu, o.fr0, o.fr1, cc, fc, hc);
+          cwl += cc;
+          cone_eval(ys, o.D, o.Dm, o.mu, o.fr0, o.fr1, cc, fc, hc);
+          csl += cc;
+          st4(sl + kOvfJc, yw);
+          st4(sl + kOvfJs, ys);
+        }
+      }
+    }
+    const float cw = gw + rowsum16(cwl);
+    const float cs = rowsum16(csl);
     const bool use_w = cw < cs;
+    if (ncon_max > kMaxCon && !use_w) {
+      float* crec = rec();
+      for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
+        float* sl = ovf_slot(crec, c);
+        *reinterpret_cast<float4*>(sl + kOvfJc) = ld4(sl + kOvfJs);
+      }
+    }
     qacc = use_w ? warm : qs;
 #pragma unroll
     for (int k = 0; k < 4; k++) jc[k] = use_w ? xw[k] : xs[k];
@@ -377,8 +484,29 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
       for (int c = 0; c < kJReg; c++) {
         if (c < ncon_max) grad -= dot4(J[c], bcast_row4(make_float4(fc[0], fc[1], fc[2], fc[3]), c));
       }
-      for (int c = kJReg; c < ncon_max; c++)
+      for (int c = kJReg; c < ncon_max && c < kMaxCon; c++)
         grad -= dot4(jx_own(r, c, lane), shfl_row4(make_float4(fc[0], fc[1], fc[2], fc[3]), c));
+      if (ncon_max > kMaxCon) {
+        // contacts beyond kMaxCon: forces at the iterate's jar (kept in the record for c'(0) below), J' f
+        float* crec = rec();
+        for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
+          const int c = b0 + lane;
+          float fo[4] = {0.f, 0.f, 0.f, 0.f};
+          if (c < ncon) {
+            float* sl = ovf_slot(crec, c);
+            OvfCon o;
+            ovf_load(sl, o);
+            const float4 j4 = ld4(sl + kOvfJc);
+            const float x[4] = {j4.x, j4.y, j4.z, j4.w};
+            float cc, hc[10];
+            cone_eval(x, o.D, o.Dm, o.mu, o.fr0, o.fr1, cc, fo, hc);
+            st4(sl + kOvfF, fo);
+          }
+#pragma unroll 1
+          for (int k = 0; k < kLanes && b0 + k < ncon_max; k++)
+            grad -= dot4(ovf_j(crec, b0 + k, lane, ncon), shfl_row4(make_float4(fo[0], fo[1], fo[2], fo[3]), k));
+        }
+      }
       grad = dof ? grad : 0.f;
       const float gn = nsqrt(rowsum16(grad * grad));
       STAMP(2);
@@ -405,7 +533,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             for (int j = 0; j < SO100_NV; j++) H[j] += dot4(w, bcast_row4(J[c], j));
           }
         }
-        for (int c = kJReg; c < ncon_max; c++) {       // J from LDS: one broadcast read per dof
+        for (int c = kJReg; c < ncon_max && c < kMaxCon; c++) {       // J from LDS: one broadcast read per dof
           float hb[10];
 #pragma unroll
           for (int k = 0; k < 10; k++) hb[k] = __shfl(hc[k], c, kLanes);
@@ -413,6 +541,36 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           const float4 w = sym4(hb, jx_own(r, c, lane));
 #pragma unroll
           for (int j = 0; j < SO100_NV; j++) H[j] += dot4(w, jc_l[j]);
+        }
+        if (ncon_max > kMaxCon) {
+          // contacts beyond kMaxCon: J' H_c J with J from the record (the Hessian re-evaluated at the iterate)
+          float* crec = rec();
+          for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
+            const int c = b0 + lane;
+            float ho[10];
+#pragma unroll
+            for (int k = 0; k < 10; k++) ho[k] = 0.f;
+            if (c < ncon) {
+              float* sl = ovf_slot(crec, c);
+              OvfCon o;
+              ovf_load(sl, o);
+              const float4 j4 = ld4(sl + kOvfJc);
+              const float x[4] = {j4.x, j4.y, j4.z, j4.w};
+              float cc, fo[4];
+              cone_eval(x, o.D, o.Dm, o.mu, o.fr0, o.fr1, cc, fo, ho);
+            }
+#pragma unroll 1
+            for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
+              float hb[10];
+#pragma unroll
+              for (int t = 0; t < 10; t++) hb[t] = __shfl(ho[t], k, kLanes);
+              const float4 w = sym4(hb, ovf_j(crec, b0 + k, lane, ncon));
+              const bool live = b0 + k < ncon;          // this env's contact (else J is 0)
+              const float4* jrow = reinterpret_cast<const float4*>(crec + (size_t)(b0 + k) * kConStride + kJOff);
+#pragma unroll
+              for (int j = 0; j < SO100_NV; j++) H[j] += live ? dot4(w, jrow[j]) : 0.f;
+            }
+          }
         }
         STAMP(3);
         // ---- Cholesky H = L L' (lane i: row i of L; lc: column i, gathered from the broadcasts)
@@ -454,6 +612,20 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
         const float4 js4 = contact_rows(r, sv, lane, ncon_max);
         const float jsc[4] = {js4.x, js4.y, js4.z, js4.w};
         const float sfr = sv, slim = lim_s * sv;
+        float ovf_l10 = 0.f;                   // contacts beyond kMaxCon: -f . J s at alpha = 0
+        if (ncon_max > kMaxCon) {
+          float* crec = rec();
+          for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
+            const float4 s4 = ovf_rows(crec, b0, sv, lane, ncon, ncon_max);
+            const int c = b0 + lane;
+            if (c < ncon) {
+              float* sl = ovf_slot(crec, c);
+              const float4 f4 = ld4(sl + kOvfF);
+              ovf_l10 -= f4.x * s4.x + f4.y * s4.y + f4.z * s4.z + f4.w * s4.w;
+              *reinterpret_cast<float4*>(sl + kOvfJs) = s4;
+            }
+          }
+        }
         auto derivs = [&](float al, float& d1, float& d2) {
           float l1 = 0.f, l2 = 0.f, cc, f, h;
           if (dof) { fr_eval(jfr + al * sfr, fr_fl, fr_R, fr_D, cc, f, h); l1 -= f * sfr; l2 += h * sfr * sfr; }
@@ -467,6 +639,21 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             l1 -= fv;
             l2 += vhv;
           }
+          if (ncon_max > kMaxCon) {
+            float* crec = rec();
+            for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
+              float* sl = ovf_slot(crec, c);
+              OvfCon o;
+              ovf_load(sl, o);
+              const float4 j4 = ld4(sl + kOvfJc), s4 = ld4(sl + kOvfJs);
+              const float x[4] = {j4.x + al * s4.x, j4.y + al * s4.y, j4.z + al * s4.z, j4.w + al * s4.w};
+              const float v[4] = {s4.x, s4.y, s4.z, s4.w};
+              float fv, vhv;
+              cone_dir(x, v, o.D, o.Dm, o.mu, o.fr0, o.fr1, fv, vhv);
+              l1 -= fv;
+              l2 += vhv;
+            }
+          }
           d1 = rowsum16(l1) + A1 + al * A2;
           d2 = rowsum16(l2) + A2;
         };
@@ -477,6 +664,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           l1 -= f_fr * sfr;
           l1 -= f_lim * slim;
           l1 -= fc[0] * jsc[0] + fc[1] * jsc[1] + fc[2] * jsc[2] + fc[3] * jsc[3];
+          if (ncon_max > kMaxCon) l1 += ovf_l10;
           d10 = rowsum16(l1) + A1;
         }
         float alpha = 0.f;
@@ -512,7 +700,23 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 #pragma unroll
           for (int k = 0; k < 4; k++) jc[k] += alpha * jsc[k];
           gauss += alpha * A1 + 0.5f * alpha * alpha * A2;
-          const float nc = gauss + rowsum16(rows_cost(jfr, jlim, jc));
+          float ncl = rows_cost(jfr, jlim, jc);
+          if (ncon_max > kMaxCon) {
+            // contacts beyond kMaxCon: jar += alpha J s in the record, their cost at the new iterate
+            float* crec = rec();
+            for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
+              float* sl = ovf_slot(crec, c);
+              OvfCon o;
+              ovf_load(sl, o);
+              const float4 j4 = ld4(sl + kOvfJc), s4 = ld4(sl + kOvfJs);
+              const float x[4] = {j4.x + alpha * s4.x, j4.y + alpha * s4.y, j4.z + alpha * s4.z, j4.w + alpha * s4.w};
+              st4(sl + kOvfJc, x);
+              float cc, fo[4], ho[10];
+              cone_eval(x, o.D, o.Dm, o.mu, o.fr0, o.fr1, cc, fo, ho);
+              ncl += cc;
+            }
+          }
+          const float nc = gauss + rowsum16(ncl);
           const float improvement = scale * (cost - nc);
           cost = nc;
           last_impr = improvement;

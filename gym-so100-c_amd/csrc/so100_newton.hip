@@ -28,8 +28,12 @@ __global__ void __launch_bounds__(kThreads, kNewtonWaves) so100_newton_kernel(Ne
   __syncthreads();
   NewtonDiag diag;
   const bool dbg = a.last && a.debug;
-  const float qacc = newton_solve(a.m, r, lane, valid, dbg, diag);
-  if (dbg) newton_diag_write(a.debug + (size_t)env * SO100_DBG_STRIDE, lane, valid, qacc, diag);
+  float* const crec = a.w.con + (size_t)e * kConEnv;      // contacts beyond kMaxCon (rare)
+  const float qacc = newton_solve(a.m, r, lane, valid, dbg, diag, [&]() { return crec; });
+  if (dbg) {
+    newton_diag_write(a.debug + (size_t)env * SO100_DBG_STRIDE, lane, valid, qacc, diag);
+    if (valid) newton_diag_write_ovf(a.debug + (size_t)env * SO100_DBG_STRIDE, crec, r.ncon, lane);
+  }
   // qacc -> HBM (the next stage's Euler input and the next substep's warmstart)
   if (valid && lane < SO100_NV) a.qacc_out[(size_t)env * SO100_NV + lane] = qacc;
 }

@@ -11,8 +11,9 @@
 //   * the arm and cube trees are decoupled (M block-diagonal, cube M diagonal: COM at the free-joint
 //     origin, principal axes = body axes), so arm frictionloss row j and cube row 6+j update together;
 //   * the first kResident contacts keep J in VGPRs and the solver block in LDS (10 KB per wave) for all
-//     sweeps; further contacts (rare: >4 per env) stream both from the HBM record every sweep, loaded at
-//     use so the register peak stays at 168 (3 waves/SIMD), forces written back to the record.
+//     sweeps; further contacts (rare: >4 per env; the list holds up to kConCap) stream both from the HBM
+//     record every sweep, loaded at use so the register peak stays at 168 (3 waves/SIMD), forces written
+//     back to the record.
 #include "so100_common.h"
 #include "so100.h"
 
@@ -176,12 +177,12 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
 
   // every env owns kMaxCon record slots: loads of slots >= ncon are in bounds but stale (or never
   // written); J of such slots is zeroed so that masked lanes contribute exactly 0 to g = J d
-  float* const crec = a.w.con + (size_t)e * kMaxCon * kConRec;
+  float* const crec = a.w.con + (size_t)e * kConEnv;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 J[kResident][3];
 #pragma unroll
   for (int c = 0; c < kResident; c++) {
-    const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
+    const float4* rec = reinterpret_cast<const float4*>(crec + c * kConStride);
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       const float4 t = rec[kBlk + 3 * q + i];
@@ -264,7 +265,7 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
     if (ncon_max > kResident) {
       for (int c = kResident; c < ncon_max; c++) {
         float4 v[kBlk], Jo[3];
-        const float4* rec = reinterpret_cast<const float4*>(crec + c * kConRec);
+        const float4* rec = reinterpret_cast<const float4*>(crec + c * kConStride);
 #pragma unroll
         for (int k = 0; k < kBlk; k++) v[k] = rec[k];
 #pragma unroll
@@ -276,7 +277,7 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
         const bool arm = __ballot(c < ncon && v[kBlkFlags].y != 0.f) != 0ull;
         float4 fn;
         contact_update(v, Jo, qacc, mrow, act, q == 0, arm, impr, fn, newton);
-        if (act && q == 0) reinterpret_cast<float4*>(crec + c * kConRec)[kBlkF] = fn;
+        if (act && q == 0) reinterpret_cast<float4*>(crec + c * kConStride)[kBlkF] = fn;
       }
       __threadfence_block();   // the forces are re-read by all 4 lanes next sweep
     }
@@ -328,11 +329,19 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
         dbg[2] = last_impr;
         for (int c = 0; c < kMaxCon; c++) {
           float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (c < ncon) f = c < kResident ? blk[c][ew][kBlkF] : reinterpret_cast<const float4*>(crec + c * kConRec)[kBlkF];
+          if (c < ncon) f = c < kResident ? blk[c][ew][kBlkF] : reinterpret_cast<const float4*>(crec + c * kConStride)[kBlkF];
           dbg[32 + c] = f.x;
           dbg[96 + 3 * c] = f.y;
           dbg[97 + 3 * c] = f.z;
           dbg[98 + 3 * c] = f.w;
+        }
+        for (int c = kMaxCon; c < ncon; c++) {      // the contacts beyond kMaxCon: geometry and force from the record
+          const float* sl = crec + (size_t)c * kConStride;
+          const float4 f = reinterpret_cast<const float4*>(sl)[kBlkF];
+          float* d = dbg + SO100_DBG_OVF + 6 * (c - kMaxCon);
+          d[0] = sl[kGeoDist];
+          d[1] = (float)__float_as_int(sl[kGeoPair]);
+          d[2] = f.x; d[3] = f.y; d[4] = f.z; d[5] = f.w;
         }
       }
     }

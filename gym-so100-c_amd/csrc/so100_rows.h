@@ -36,12 +36,11 @@ DEV float4 minv_times(float4 J, const float* minv_row, float invmc, int lane) {
   return acc;
 }
 
-// contact c's Jacobian column for dof `lane` (rows: normal, t1, t2 on the point velocity; torsion on
-// the angular velocity); J = frame . (jac(body of geom2) - jac(body of geom1)) at the contact point
-DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int c, int lane) {
-  const int p = sh.con_pair[c];
-  const float* cp = sh.con[c].g.pos;
-  const float* fr = sh.con[c].g.frame;
+// the Jacobian column for dof `lane` of the contact of pair p at point cp with frame fr (rows: normal, t1, t2
+// on the point velocity; torsion on the angular velocity); J = frame . (jac(body of geom2) - jac(body of
+// geom1)) at the contact point
+DEV float4 contact_jac_at(const DevModel* __restrict__ m, const EnvShared& sh, int p, const float* cp, const float* fr,
+                          int lane) {
   float jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
 #pragma unroll
   for (int side = 0; side < 2; side++) {
@@ -75,6 +74,20 @@ DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int 
   const float jt = m->pair_cond4[p] ? fr[0] * jr[0] + fr[1] * jr[1] + fr[2] * jr[2] : 0.f;
   return make_float4(fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2], fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2],
                      fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2], jt);
+}
+// contact c < kMaxCon (on chip)
+DEV float4 contact_jac(const DevModel* __restrict__ m, const EnvShared& sh, int c, int lane) {
+  return contact_jac_at(m, sh, sh.con_pair[c], sh.con[c].g.pos, sh.con[c].g.frame, lane);
+}
+// contact c >= kMaxCon: its geometry from the env's HBM contact record (so100_step.hip store_contact)
+DEV float4 contact_jac_ovf(const DevModel* __restrict__ m, const EnvShared& sh, const float* crec, int c, int lane) {
+  const float* g = crec + (size_t)c * kConStride + kGeoOff;
+  float cp[3], fr[9];
+#pragma unroll
+  for (int t = 0; t < 3; t++) cp[t] = g[t];
+#pragma unroll
+  for (int t = 0; t < 9; t++) fr[t] = g[4 + t];
+  return contact_jac_at(m, sh, __float_as_int(g[16]), cp, fr, lane);
 }
 
 // Symmetric 3x3 eigen-decomposition by cyclic Jacobi (5 sweeps: quadratic convergence reaches fp32

@@ -29,6 +29,102 @@
 
 namespace so100 {
 
+// Newton data of a contact of pair p at distance dist with J qvel = cv (MuJoCo mj_makeImpedance / mj_diagApprox /
+// mj_referenceConstraint for an elliptic contact): aref, R (normal, friction rows: impratio), and the cone's mu
+// with the friction coefficients (DR friction scale on the cube's pairs)
+DEV void newton_contact_rows(const DevModel* __restrict__ m, int p, float dist, const float* cv, float fscale, float4& aref,
+                             float4& Rv, float4& mu) {
+  const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
+  const float K = m->pair_K[p], Bd = m->pair_B[p];
+  const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
+  const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
+  float R[4];
+  // (reciprocals by v_rcp, the square root by v_sqrt: 1 ulp, on the contact's setup chain)
+  R[0] = fmaxf(kMinVal, (1.f - imp) * __builtin_amdgcn_rcpf(imp) * m->pair_tran[p]);
+  R[1] = R[0] * mu0 * mu0 * __builtin_amdgcn_rcpf(mu0 * mu0 * m->impratio);
+  R[2] = R[1];
+  R[3] = R[0] * mu0 * mu0 * __builtin_amdgcn_rcpf(mu1 * mu1 * m->impratio);
+  aref = make_float4(-Bd * cv[0] - K * imp * (dist - m->pair_margin[p]), -Bd * cv[1], -Bd * cv[2], -Bd * cv[3]);
+  Rv = make_float4(R[0], R[1], R[2], R[3]);
+  mu = make_float4(mu0 * __builtin_amdgcn_sqrtf(R[1] * __builtin_amdgcn_rcpf(R[0])), mu0, mu1, 0.f);
+}
+
+// PGS data of one contact (pair p, distance dist; the row reductions cA = (J M^-1 J')_upper, cV = J qvel,
+// cAc = J qacc_smooth, cW = J qacc_warmstart): impedance, regularisers, the warmstart force by MuJoCo's dual map,
+// the eigen-decomposition of the cone-scaled friction block for the QCQP; the solver block to cs (record slot,
+// layout so100_device.h), the warmstart force to cf and its dual cost to cost_part
+DEV void pgs_contact_block(const DevModel* __restrict__ m, int p, float dist, float fscale, const float* cA, const float* cV,
+                           const float* cAc, const float* cW, float4* cs, float* cf, float& cost_part) {
+  const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
+  const float K = m->pair_K[p], Bd = m->pair_B[p];
+  const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
+  const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
+  float R[4];
+  R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
+  R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
+  R[2] = R[1];
+  R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
+  float aref[4];
+  aref[0] = -Bd * cV[0] - K * imp * (dist - m->pair_margin[p]);
+  aref[1] = -Bd * cV[1]; aref[2] = -Bd * cV[2]; aref[3] = -Bd * cV[3];
+  // A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
+  float ar[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) ar[k] = cA[k];
+  ar[0] += R[0]; ar[4] += R[1]; ar[7] += R[2]; ar[9] += R[3];
+  // warmstart force: dual map of jar = J qacc_warmstart - aref (elliptic zones)
+  float jar[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) jar[r] = cW[r] - aref[r];
+  const float mus[3] = {mu0, mu0, mu1};
+  {
+    const float mu = mu0 * sqrtf(R[1] / R[0]);
+    float U[4], T = 0.f;
+    U[0] = jar[0] * mu;
+#pragma unroll
+    for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
+    T = sqrtf(T);
+    const float N = U[0];
+    if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
+      cf[0] = cf[1] = cf[2] = cf[3] = 0.f;
+    } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) cf[k] = -jar[k] / R[k];
+    } else {
+      const float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
+      const float NmT = N - mu * T;
+      cf[0] = -Dm * NmT * mu;
+#pragma unroll
+      for (int k = 1; k < 4; k++) cf[k] = -cf[0] / T * U[k] * mus[k - 1];
+    }
+  }
+  // QCQP data: eigen-decomposition of the cone-scaled friction block (constant over the sweeps)
+  const float A11[3][3] = {{ar[4], ar[5], ar[6]}, {ar[5], ar[7], ar[8]}, {ar[6], ar[8], ar[9]}};
+  float As[3][3], Qe[3][3], lam[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b2 = 0; b2 < 3; b2++) As[a][b2] = A11[a][b2] * mus[a] * mus[b2];
+  eig3_sym(As, lam, Qe);
+  // solver block (layout: so100_device.h), f written after the warmstart decision
+  float P[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) P[i][j] = Qe[j][i] * mus[j];
+  cs[0] = make_float4(ar[0], ar[1], ar[2], ar[3]);
+  cs[1] = make_float4(ar[4], ar[5], ar[6], ar[7]);
+  cs[2] = make_float4(ar[8], ar[9], P[0][0], P[0][1]);
+  cs[3] = make_float4(P[0][2], P[1][0], P[1][1], P[1][2]);
+  cs[4] = make_float4(P[2][0], P[2][1], P[2][2], lam[0]);
+  cs[5] = make_float4(lam[1], lam[2], 1.f / lam[0], 1.f / lam[1]);
+  cs[6] = make_float4(1.f / lam[2], R[0], 1.f / ar[0], R[1]);
+  cs[kBlkFlags] = make_float4(R[3], m->pair_arm[p] ? 1.f : 0.f, 0.f, 0.f);
+  cs[kBlkAref] = make_float4(aref[0], aref[1], aref[2], aref[3]);
+#pragma unroll
+  for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
+}
+
 // ------------------------------------------------------------------ the step kernel
 struct StageArgs {
   const DevModel* m;
@@ -118,23 +214,36 @@ DEV void euler_update(EnvShared& sh, int lane, float h, float qacc, float& qpos_
   __syncthreads();
 }
 
-// write one box-box pair's contacts into slots base, base+1, ... (slots >= kMaxCon are dropped, as the
-// oracle's add_contact drops contacts beyond SO100_MAXCON)
-DEV void put_box_contacts(EnvShared& sh, const PairContacts& pc, int base, int p) {
+// Contact `slot` of the env's list: slots < kMaxCon on chip (the LDS contact area), the rest in the env's HBM
+// contact record (crec, kGeoOff: read back by contact_jac_ovf).  The list holds every contact (kConCap: every
+// pair at its collider's maximum), so nothing is dropped.
+DEV void store_contact(EnvShared& sh, float* crec, int slot, const float* fr, float p0, float p1, float p2, float dist,
+                       int pair) {
+  if (slot < kMaxCon) {
+#pragma unroll
+    for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
+    sh.con[slot].g.pos[0] = p0; sh.con[slot].g.pos[1] = p1;
+    sh.con[slot].g.pos[2] = p2; sh.con[slot].g.pos[3] = dist;
+    sh.con_dist[slot] = dist;
+    sh.con_pair[slot] = pair;
+  } else {
+    float4* g = reinterpret_cast<float4*>(crec + (size_t)slot * kConStride + kGeoOff);
+    g[0] = make_float4(p0, p1, p2, dist);
+    g[1] = make_float4(fr[0], fr[1], fr[2], fr[3]);
+    g[2] = make_float4(fr[4], fr[5], fr[6], fr[7]);
+    g[3] = make_float4(fr[8], 0.f, 0.f, 0.f);
+    g[4] = make_float4(__int_as_float(pair), dist, 0.f, 0.f);
+  }
+}
+
+// write one box-box pair's contacts into slots base, base+1, ...
+DEV void put_box_contacts(EnvShared& sh, float* crec, const PairContacts& pc, int base, int p) {
   // one frame per pair (every contact of a box pair shares its normal)
   float fr[9] = {pc.normal[0], pc.normal[1], pc.normal[2], 0, 0, 0, 0, 0, 0};
   if (pc.n > 0) make_frame(fr);
 #pragma unroll
   for (int c = 0; c < SO100_MAXCONPAIR; c++) {
-    const int slot = base + c;
-    if (c < pc.n && slot < kMaxCon) {
-#pragma unroll
-      for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
-      sh.con[slot].g.pos[0] = pc.pos[c][0]; sh.con[slot].g.pos[1] = pc.pos[c][1];
-      sh.con[slot].g.pos[2] = pc.pos[c][2]; sh.con[slot].g.pos[3] = pc.dist[c];
-      sh.con_dist[slot] = pc.dist[c];
-      sh.con_pair[slot] = p;
-    }
+    if (c < pc.n) store_contact(sh, crec, base + c, fr, pc.pos[c][0], pc.pos[c][1], pc.pos[c][2], pc.dist[c], p);
   }
 }
 
@@ -146,7 +255,7 @@ DEV void put_box_contacts(EnvShared& sh, const PairContacts& pc, int base, int p
 //     box, 3 pairs per lane), the candidates compacted in pair order and run through the box-box
 //     collider 16 at a time (a wave runs as many rounds as its busiest env needs; usually none).
 // Contacts are appended after `tot` in pair order; returns the new total.
-DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, int grp, bool valid, int tot) {
+DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec, int lane, int grp, bool valid, int tot) {
   // ---- pad-table (lanes 0..7)
   bool tfound = false, nearbin = false;
   float tx = 0.f, ty = 0.f, tz = 0.f;
@@ -205,17 +314,12 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
   const uint32_t trow = (uint32_t)((__ballot(tfound) >> (grp * 16)) & 0xFFull);
   {
     const int slot = tot + __popc(trow & ((1u << lane) - 1u));
-    if (tfound && slot < kMaxCon) {
+    if (tfound) {
       float fr[9] = {0.f, 0.f, -1.f, 0, 0, 0, 0, 0, 0};
       opaque(fr[2]);              // a constant frame: built here, not hoisted out of the fused substep loop
       make_frame(fr);
-#pragma unroll
-      for (int t = 0; t < 9; t++) sh.con[slot].g.frame[t] = fr[t];
       const float top = m->table_top;
-      sh.con[slot].g.pos[0] = tx; sh.con[slot].g.pos[1] = ty;
-      sh.con[slot].g.pos[2] = 0.5f * (tz + top); sh.con[slot].g.pos[3] = tz - top;
-      sh.con_dist[slot] = tz - top;
-      sh.con_pair[slot] = SO100_PAIR_PAD0 + lane;
+      store_contact(sh, crec, slot, fr, tx, ty, 0.5f * (tz + top), tz - top, SO100_PAIR_PAD0 + lane);
     }
   }
   tot += __popc(trow);
@@ -268,7 +372,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, int lane, in
     int off = 0, sum = 0;
 #pragma unroll
     for (int k = 0; k < kLanes; k++) { const int c = sh.cnt[k]; off += (k < lane) ? c : 0; sum += c; }
-    put_box_contacts(sh, pc, tot + off, p);
+    put_box_contacts(sh, crec, pc, tot + off, p);
     tot += sum;
     __syncthreads();
   }
@@ -349,7 +453,10 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
     SSTAMP(6);
-    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, lane, grp, valid);
+    // the env's contact record in HBM: the contacts beyond the kMaxCon held on chip (every kernel), and the
+    // split path's solver record
+    float* const crec = args.w.con + (size_t)e * kConEnv;
+    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, args.w.con + (size_t)(env - grp) * kConEnv, lane, grp, valid);
     SSTAMP(7);
     PairContacts pc;
     pc.n = 0;
@@ -363,44 +470,44 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       int off = 0, tot = 0;
 #pragma unroll
       for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
-      put_box_contacts(sh, pc, off, lane);
+      put_box_contacts(sh, crec, pc, off, lane);
       const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
-      if (hfound && hslot < kMaxCon) {
+      if (hfound) {
         float fr[9] = {0.f, 0.f, 1.f, 0, 0, 0, 0, 0, 0};
         opaque(fr[2]);            // a constant frame: built here, not hoisted out of the fused substep loop
         make_frame(fr);
-#pragma unroll
-        for (int t = 0; t < 9; t++) sh.con[hslot].g.frame[t] = fr[t];
         const float top = m->table_top;
-        sh.con[hslot].g.pos[0] = hx; sh.con[hslot].g.pos[1] = hy;
-        sh.con[hslot].g.pos[2] = 0.5f * (hz + top); sh.con[hslot].g.pos[3] = hz - top;
-        sh.con_dist[hslot] = hz - top;
-        sh.con_pair[hslot] = SO100_NPAIR_BOX + lane;
+        store_contact(sh, crec, hslot, fr, hx, hy, 0.5f * (hz + top), hz - top, SO100_NPAIR_BOX + lane);
       }
       tot += __popc(hrow);
-      const int mslot = tot + lane;
-      if (lane < nmpr && mslot < kMaxCon) {
+      // the convex collider's contacts, staged in order: staged contact j is contact tot + j (staged j >= kMaxCon
+      // in the record, mpr_contacts)
+      if (lane < nmpr) {
         const MprStage st = sh.mpr[lane];
         float fr[9] = {st.nrm[0], st.nrm[1], st.nrm[2], 0, 0, 0, 0, 0, 0};
         make_frame(fr);
-#pragma unroll
-        for (int t = 0; t < 9; t++) sh.con[mslot].g.frame[t] = fr[t];
-#pragma unroll
-        for (int t = 0; t < 4; t++) sh.con[mslot].g.pos[t] = st.pos[t];
-        sh.con_dist[mslot] = st.pos[3];
-        sh.con_pair[mslot] = __float_as_int(st.nrm[3]);
+        store_contact(sh, crec, tot + lane, fr, st.pos[0], st.pos[1], st.pos[2], st.pos[3], __float_as_int(st.nrm[3]));
+      }
+      for (int j0 = kMaxCon; j0 < wave_max_i(nmpr); j0 += kLanes) {   // rare: more than kMaxCon convex contacts
+        const int j = j0 + lane;
+        if (j < nmpr) {
+          const float4* stg = reinterpret_cast<const float4*>(crec + (size_t)j * kConStride + kMprStageOff);
+          const float4 sp = stg[0], sn = stg[1];
+          float fr[9] = {sn.x, sn.y, sn.z, 0, 0, 0, 0, 0, 0};
+          make_frame(fr);
+          store_contact(sh, crec, tot + j, fr, sp.x, sp.y, sp.z, sp.w, __float_as_int(sn.w));
+        }
       }
       tot += nmpr;
       __syncthreads();
-      tot = pad_contacts(m, sh, lane, grp, valid, tot);
-      const int drop = tot > kMaxCon ? tot - kMaxCon : 0;   // the oracle's ncon_dropped
+      tot = pad_contacts(m, sh, crec, lane, grp, valid, tot);
+      // every contact is kept (kConCap is the list's maximum), so none is dropped: 0 is written as the counter
       if (lane == 0) {
-        sh.ncon = tot < kMaxCon ? tot : kMaxCon;
-        if constexpr (kFused) sh.ndrop = (sub == 0 ? 0 : sh.ndrop) + drop;   // stored by the fused epilogue
+        sh.ncon = tot;
+        if constexpr (kFused) sh.ndrop = 0;              // stored by the fused epilogue
       }
       if constexpr (!kFused) {
-        if (valid && lane == 0 && B.ncon_dropped)
-          B.ncon_dropped[env] = (sub == 0 ? 0u : B.ncon_dropped[env]) + (uint32_t)drop;
+        if (valid && lane == 0 && B.ncon_dropped && sub == 0) B.ncon_dropped[env] = 0u;
       }
     }
     __syncthreads();
@@ -417,7 +524,6 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         else atomicOr(fl, 2u);
       }
     }
-    float* const crec = args.w.con + (size_t)e * kMaxCon * kConRec;
 
     // ---------------- S4/S5: M^-1 rows, frictionloss and joint-limit rows (lane = dof)
     float minv_row[6];
@@ -475,7 +581,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
           float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
           if (c < ncon && lane < SO100_NV) {
             J = contact_jac(m, sh, c, lane);
-            if constexpr (!kFused) reinterpret_cast<float4*>(crec + c * kConRec + kJOff)[lane] = J;
+            if constexpr (!kFused) reinterpret_cast<float4*>(crec + c * kConStride + kJOff)[lane] = J;
           }
           if constexpr (kFused) {
             if (c < kJReg) nr.J[c] = J;
@@ -506,22 +612,32 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       nr.c_aref = make_float4(0.f, 0.f, 0.f, 0.f);
       nr.c_R = make_float4(1.f, 1.f, 1.f, 1.f);
       nr.c_mu = make_float4(1.f, 1.f, 1.f, 0.f);
-      if (lane < ncon) {
-        const int p = sh.con_pair[lane];
-        const float dist = sh.con_dist[lane];
-        const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
-        const float K = m->pair_K[p], Bd = m->pair_B[p];
-        const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
-        const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
-        float R[4];
-        // (reciprocals by v_rcp, the square root by v_sqrt: 1 ulp, on the contact's setup chain)
-        R[0] = fmaxf(kMinVal, (1.f - imp) * __builtin_amdgcn_rcpf(imp) * m->pair_tran[p]);
-        R[1] = R[0] * mu0 * mu0 * __builtin_amdgcn_rcpf(mu0 * mu0 * m->impratio);
-        R[2] = R[1];
-        R[3] = R[0] * mu0 * mu0 * __builtin_amdgcn_rcpf(mu1 * mu1 * m->impratio);
-        nr.c_aref = make_float4(-Bd * cVn[0] - K * imp * (dist - m->pair_margin[p]), -Bd * cVn[1], -Bd * cVn[2], -Bd * cVn[3]);
-        nr.c_R = make_float4(R[0], R[1], R[2], R[3]);
-        nr.c_mu = make_float4(mu0 * __builtin_amdgcn_sqrtf(R[1] * __builtin_amdgcn_rcpf(R[0])), mu0, mu1, 0.f);
+      if (lane < ncon) newton_contact_rows(m, sh.con_pair[lane], sh.con_dist[lane], cVn, fscale, nr.c_aref, nr.c_R, nr.c_mu);
+      if (ncon_max > kMaxCon) {
+        // the contacts beyond kMaxCon (rare): J and their aref / R / cone coefficients to the env's HBM record,
+        // block by block of 16 (lane k: contact kMaxCon + 16 b + k), for both paths' newton_solve
+        for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
+          float cv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+          for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
+            const int c = b0 + k;
+            float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (c < ncon && lane < SO100_NV) {
+              J = contact_jac_ovf(m, sh, crec, c, lane);
+              reinterpret_cast<float4*>(crec + (size_t)c * kConStride + kJOff)[lane] = J;
+            }
+            const float v0 = rowsum16(J.x * qvel_r), v1 = rowsum16(J.y * qvel_r);
+            const float v2 = rowsum16(J.z * qvel_r), v3 = rowsum16(J.w * qvel_r);
+            if (lane == k) { cv[0] = v0; cv[1] = v1; cv[2] = v2; cv[3] = v3; }
+          }
+          const int c = b0 + lane;
+          if (c < ncon) {
+            float4* sl = reinterpret_cast<float4*>(crec + (size_t)c * kConStride);
+            const float* g = crec + (size_t)c * kConStride;
+            newton_contact_rows(m, __float_as_int(g[kGeoPair]), g[kGeoDist], cv, fscale, sl[0], sl[1], sl[2]);
+          }
+        }
+        __syncthreads();          // the record's J rows are read by the other lanes of the row in the solve
       }
       SSTAMP(4);
       nr.qs = lane < SO100_NV ? qs_r : 0.f;
@@ -576,7 +692,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c < ncon && lane < SO100_NV) {
           J = contact_jac(m, sh, c, lane);
-          reinterpret_cast<float4*>(crec + c * kConRec + kJOff)[lane] = J;
+          reinterpret_cast<float4*>(crec + c * kConStride + kJOff)[lane] = J;
         }
         Jr[c] = J;
         const float4 M = minv_times(J, minv_row, invmc, lane);   // M^-1 J' column of this dof
@@ -601,79 +717,9 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     // ---------------- S6b: scalar setup of contact `lane` (impedance, regularisers, warmstart dual map,
     // eigen-decomposition for the QCQP) -> solver block in the HBM record
     float cf[4] = {0.f, 0.f, 0.f, 0.f};
-    if (lane < ncon) {
-      const int p = sh.con_pair[lane];
-      const float dist = sh.con_dist[lane];
-      const float imp = getimpedance(m->pair_solimp[p], dist, m->pair_margin[p]);
-      const float K = m->pair_K[p], Bd = m->pair_B[p];
-      const float fs = m->pair_cube[p] ? fscale : 1.f;     // DR friction scale: cube pairs
-      const float mu0 = m->pair_mu0[p] * fs, mu1 = m->pair_mu1[p] * fs;
-      float R[4];
-      R[0] = fmaxf(kMinVal, (1.f - imp) / imp * m->pair_tran[p]);
-      R[1] = R[0] * mu0 * mu0 / (mu0 * mu0 * m->impratio);
-      R[2] = R[1];
-      R[3] = R[0] * mu0 * mu0 / (mu1 * mu1 * m->impratio);
-      float aref[4];
-      aref[0] = -Bd * cV[0] - K * imp * (dist - m->pair_margin[p]);
-      aref[1] = -Bd * cV[1]; aref[2] = -Bd * cV[2]; aref[3] = -Bd * cV[3];
-      // A + R, upper triangle row-major: 00 01 02 03 11 12 13 22 23 33
-      float ar[10];
-#pragma unroll
-      for (int k = 0; k < 10; k++) ar[k] = cA[k];
-      ar[0] += R[0]; ar[4] += R[1]; ar[7] += R[2]; ar[9] += R[3];
-      // warmstart force: dual map of jar = J qacc_warmstart - aref (elliptic zones)
-      float jar[4];
-#pragma unroll
-      for (int r = 0; r < 4; r++) jar[r] = cW[r] - aref[r];
-      const float mus[3] = {mu0, mu0, mu1};
-      {
-        const float mu = mu0 * sqrtf(R[1] / R[0]);
-        float U[4], T = 0.f;
-        U[0] = jar[0] * mu;
-#pragma unroll
-        for (int k = 1; k < 4; k++) { U[k] = jar[k] * mus[k - 1]; T += U[k] * U[k]; }
-        T = sqrtf(T);
-        const float N = U[0];
-        if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
-          cf[0] = cf[1] = cf[2] = cf[3] = 0.f;
-        } else if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
-#pragma unroll
-          for (int k = 0; k < 4; k++) cf[k] = -jar[k] / R[k];
-        } else {
-          const float Dm = (1.f / R[0]) / (mu * mu * (1.f + mu * mu));
-          const float NmT = N - mu * T;
-          cf[0] = -Dm * NmT * mu;
-#pragma unroll
-          for (int k = 1; k < 4; k++) cf[k] = -cf[0] / T * U[k] * mus[k - 1];
-        }
-      }
-      // QCQP data: eigen-decomposition of the cone-scaled friction block (constant over the sweeps)
-      const float A11[3][3] = {{ar[4], ar[5], ar[6]}, {ar[5], ar[7], ar[8]}, {ar[6], ar[8], ar[9]}};
-      float As[3][3], Qe[3][3], lam[3];
-#pragma unroll
-      for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b2 = 0; b2 < 3; b2++) As[a][b2] = A11[a][b2] * mus[a] * mus[b2];
-      eig3_sym(As, lam, Qe);
-      // solver block (layout: so100_device.h), f written after the warmstart decision
-      float P[3][3];
-#pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) P[i][j] = Qe[j][i] * mus[j];
-      float4* cs = reinterpret_cast<float4*>(crec + lane * kConRec);
-      cs[0] = make_float4(ar[0], ar[1], ar[2], ar[3]);
-      cs[1] = make_float4(ar[4], ar[5], ar[6], ar[7]);
-      cs[2] = make_float4(ar[8], ar[9], P[0][0], P[0][1]);
-      cs[3] = make_float4(P[0][2], P[1][0], P[1][1], P[1][2]);
-      cs[4] = make_float4(P[2][0], P[2][1], P[2][2], lam[0]);
-      cs[5] = make_float4(lam[1], lam[2], 1.f / lam[0], 1.f / lam[1]);
-      cs[6] = make_float4(1.f / lam[2], R[0], 1.f / ar[0], R[1]);
-      cs[kBlkFlags] = make_float4(R[3], m->pair_arm[p] ? 1.f : 0.f, 0.f, 0.f);
-      cs[kBlkAref] = make_float4(aref[0], aref[1], aref[2], aref[3]);
-#pragma unroll
-      for (int r = 0; r < 4; r++) cost_part += 0.5f * R[r] * cf[r] * cf[r] + cf[r] * (cAc[r] - aref[r]);
-    }
+    if (lane < ncon)
+      pgs_contact_block(m, sh.con_pair[lane], sh.con_dist[lane], fscale, cA, cV, cAc, cW,
+                        reinterpret_cast<float4*>(crec + lane * kConStride), cf, cost_part);
     SSTAMP(4);
     // J' f of the warmstart forces: contact c's forces broadcast from lane c
 #pragma unroll
@@ -681,6 +727,56 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       if (c < ncon_max) {
         const float4 fc = bcast_row4(make_float4(cf[0], cf[1], cf[2], cf[3]), c);
         phi += Jr[c].x * fc.x + Jr[c].y * fc.y + Jr[c].z * fc.z + Jr[c].w * fc.w;
+      }
+    }
+    if (ncon_max > kMaxCon) {
+      // the contacts beyond kMaxCon (rare), block by block of 16 (lane k: contact kMaxCon + 16 b + k): J (-> the
+      // record), the row reductions, the contact's block (-> the record) and warmstart force, J' f (J read back)
+      for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
+        float oA[10], oV[4], oAc[4], oW[4];
+#pragma unroll
+        for (int k = 0; k < 10; k++) oA[k] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; r++) oV[r] = oAc[r] = oW[r] = 0.f;
+#pragma unroll 1
+        for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
+          const int c = b0 + k;
+          float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (c < ncon && lane < SO100_NV) {
+            J = contact_jac_ovf(m, sh, crec, c, lane);
+            reinterpret_cast<float4*>(crec + (size_t)c * kConStride + kJOff)[lane] = J;
+          }
+          const float4 M = minv_times(J, minv_row, invmc, lane);
+          const float jv[4] = {J.x, J.y, J.z, J.w}, mv[4] = {M.x, M.y, M.z, M.w};
+          const bool mine = lane == k;
+          int q2 = 0;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+#pragma unroll
+            for (int q = r; q < 4; q++, q2++) {
+              const float a = rowsum16(jv[r] * mv[q]);
+              oA[q2] = mine ? a : oA[q2];
+            }
+            const float v = rowsum16(jv[r] * qvel_r), ac = rowsum16(jv[r] * qs_r), w = rowsum16(jv[r] * warm_r);
+            oV[r] = mine ? v : oV[r];
+            oAc[r] = mine ? ac : oAc[r];
+            oW[r] = mine ? w : oW[r];
+          }
+        }
+        float of[4] = {0.f, 0.f, 0.f, 0.f};
+        const int c = b0 + lane;
+        if (c < ncon) {
+          float4* cs = reinterpret_cast<float4*>(crec + (size_t)c * kConStride);
+          const float* g = crec + (size_t)c * kConStride;
+          pgs_contact_block(m, __float_as_int(g[kGeoPair]), g[kGeoDist], fscale, oA, oV, oAc, oW, cs, of, cost_part);
+          cs[kBlkF] = make_float4(of[0], of[1], of[2], of[3]);     // zeroed below if the warmstart is dropped
+        }
+#pragma unroll 1
+        for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
+          const float4 fk = shfl_row4(make_float4(of[0], of[1], of[2], of[3]), k);
+          const float4 J = ovf_j(crec, b0 + k, lane, ncon);
+          phi += J.x * fk.x + J.y * fk.y + J.z * fk.z + J.w * fk.w;
+        }
       }
     }
     // ---------------- S7: warmstart dual cost 0.5 f'ARf + f'b (keep the warmstart only if <= 0)
@@ -702,7 +798,11 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     } else {
       qacc_c += dq;
     }
-    if (lane < ncon) reinterpret_cast<float4*>(crec + lane * kConRec)[kBlkF] = make_float4(cf[0], cf[1], cf[2], cf[3]);
+    if (lane < ncon) reinterpret_cast<float4*>(crec + lane * kConStride)[kBlkF] = make_float4(cf[0], cf[1], cf[2], cf[3]);
+    if (ncon_max > kMaxCon && cost > 0.f) {
+      for (int c = kMaxCon + lane; c < ncon; c += kLanes)
+        reinterpret_cast<float4*>(crec + (size_t)c * kConStride)[kBlkF] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 
     // ---------------- solver record -> HBM (consumed by so100_pgs_kernel)
     if (valid) {
@@ -812,7 +912,10 @@ DEV void final_stage(const StageArgs& args, EnvShared& sh, int lane, int grp, in
       if (B.diverged) B.diverged[env] = diverged;
       if (B.contact_bits) B.contact_bits[env] = bits;
       if (goal && B.total_steps) B.total_steps[env] = B.total_steps[env] + 1;
-      if (B.ep_return) {
+      // (without auto-reset an env left truncated keeps reporting truncated: its episode is counted once, at
+      // the step that reached the limit; stepping a terminated env without a reset is outside the contract)
+      const bool ended_before = args.max_steps > 0 && elapsed0 >= args.max_steps;
+      if (B.ep_return && !ended_before) {
         // episode statistics (RecordEpisodeStatistics): the running float64 return, and at the episode's end
         // its return and length into ep_final and the env's running totals
         const double ret = B.ep_return[env] + reward;
@@ -1018,11 +1121,19 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     TL_MARK(0);
     NewtonDiag diag;
     const bool dbg = kDebug && args.b.debug && sub == nsub - 1;
-    const float qacc = newton_solve(sa.m, nr, lane, valid, dbg, diag);
+    // the env's HBM contact record, for its contacts beyond kMaxCon (rare): its address recomputed from fresh ids
+    // where needed, not held across the solve
+    auto rec = [&]() -> float* {
+      int l2, g2, en2, e2;
+      fresh_ids(group, args.n, l2, g2, en2, e2);
+      return args.w.con + (size_t)e2 * kConEnv;
+    };
+    const float qacc = newton_solve(sa.m, nr, lane, valid, dbg, diag, rec);
     if (dbg) {
       int row = env;
       asm volatile("" : "+v"(row));        // not the assembly's row address (GVN would hold that across the solve)
       newton_diag_write(args.b.debug + (size_t)row * SO100_DBG_STRIDE, lane, valid, qacc, diag);
+      if (valid) newton_diag_write_ovf(args.b.debug + (size_t)row * SO100_DBG_STRIDE, rec(), nr.ncon, lane);
     }
     warm_r = lane < SO100_NV ? qacc : 0.f;
     TL_MARK(1);
@@ -1303,6 +1414,14 @@ extern "C" int so100_dev_epa_cycles(unsigned long long* out, int reset) {
 }
 namespace so100 {
 #endif
+__global__ void so100_contact_counts_kernel(const float* __restrict__ hdr, int n, int32_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = __float_as_int(hdr[(size_t)i * kHdrEnv + H_NCON]);
+}
+hipError_t launch_contact_counts(const Workspace& w, int n, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(so100_contact_counts_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w.hdr, n, out);
+  return hipGetLastError();
+}
 hipError_t launch_contact_count(const Workspace& w, int n, uint64_t* accum, hipStream_t s) {
   int blocks = (n + 255) / 256;
   if (blocks > 256) blocks = 256;
@@ -1315,10 +1434,10 @@ hipError_t free_workspace(Workspace* w);
 hipError_t alloc_workspace(int n, Workspace* w) {
   *w = Workspace{};
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kMaxCon * kConRec * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kConEnv * sizeof(float));
   // zero once: record slots a solver lane reads but never uses are then finite, never garbage
   if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
-  if (e == hipSuccess) e = hipMemset(w->con, 0, (size_t)n * kMaxCon * kConRec * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(w->con, 0, (size_t)n * kConEnv * sizeof(float));
   const size_t ngroups = (size_t)(n + kPgsEnvs - 1) / kPgsEnvs;
   if (e == hipSuccess) e = hipMalloc(&w->gflag, 2 * ngroups * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->hcount, 2 * sizeof(int));
@@ -1341,13 +1460,17 @@ hipError_t free_workspace(Workspace* w) {
   w->hcount = w->hlist = w->order = nullptr;
   return r;
 }
-// The fused path's workspace: the record header (only its contact counts are written) and the wave-order
-// buffers.
+// The fused path's workspace: the record header (only its contact counts are written), the wave-order buffers,
+// and the per-env contact record of the contacts beyond the kMaxCon held on chip (kConEnv floats per env:
+// 252 KB, 16.5 GB at 65,536 envs, for a list that can hold every contact; touched only where an env has more
+// than kMaxCon contacts).
 hipError_t alloc_fused_workspace(int n, Workspace* w) {
   *w = Workspace{};
   const size_t ng = (size_t)(n + kEnvsPerBlock - 1) / kEnvsPerBlock;
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
   if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kConEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(w->con, 0, (size_t)n * kConEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->gcost, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->gcost, 0, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->order, ng * sizeof(int));

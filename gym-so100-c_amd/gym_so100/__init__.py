@@ -2,7 +2,8 @@
 
 * ``SO100VecEnv``: batched envs on one GPU (torch tensors), the hot path.
 * ``SO100Env`` / ``SO100GoalEnv``: single-env Gymnasium-style classes (reference env.py).
-* Registration of the reference's env ids when gymnasium is importable (reference __init__.py:4-32).
+* Registration of the reference's env ids when gymnasium is importable (reference __init__.py:4-32), and
+  ``gym_so100.make(id, **kwargs)``, the same construction (SO100Env + TimeLimit) where it is not.
 """
 from .vec_env import SO100VecEnv  # noqa: F401
 from .env import SO100Env, SO100GoalEnv  # noqa: F401
@@ -21,3 +22,5 @@ try:  # gymnasium is an optional dependency here (absent in this image)
                   nondeterministic=True, kwargs={"obs_type": "so100_pixels_agent_pos", "task": _kw["task"]})
 except ImportError:
     pass
+
+from .registration import make  # noqa: E402,F401  (gym.make for the ids above where gymnasium is absent)

@@ -11,7 +11,8 @@ LIB_PATH = os.environ.get("SO100_LIB") or os.path.join(HERE, "_lib", "libso100_h
 
 SO100_FLAG_AUTORESET = 1
 SO100_FLAG_DR = 2
-SO100_DBG_STRIDE = 160
+SO100_DBG_OVF = 160                   # include/so100.h: the debug entries of contacts >= 16
+SO100_DBG_STRIDE = 160 + 6 * (562 - 16)
 TASKS = {"so100_cube_to_bin": 0, "so100_touch_cube": 1, "so100_touch_cube_sparse": 2, "so100_goal": 3}
 
 _P = ctypes.c_void_p
@@ -45,7 +46,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 13         # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 14         # include/so100.h SO100_ABI_VERSION
 HULL_CELLG = 8           # SO100_HULL_CELLG
 HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 
@@ -76,6 +77,7 @@ def load():
     lib.so100_profile_enable.argtypes = [_P, ctypes.c_int]
     lib.so100_profile_read.argtypes = [_P, _P, _P, _P, _P]
     lib.so100_contact_count.argtypes = [_P, _P, _P]
+    lib.so100_contact_counts.argtypes = [_P, _P, _P]
     lib.so100_chunk_info.argtypes = [_P, _P, _P]
     lib.so100_set_step_mode.argtypes = [_P, ctypes.c_int]
     lib.so100_step_mode.argtypes = [_P]
@@ -86,8 +88,8 @@ def load():
     lib.so100_fused_build.argtypes = [_P, ctypes.c_int]
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
-               "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_chunk_info",
-               "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells",
+               "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_contact_counts",
+               "so100_chunk_info", "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells",
                "so100_set_fused_build", "so100_fused_build"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
@@ -107,7 +109,7 @@ def load():
 EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
-                    "so100_contact_count", "so100_chunk_info", "so100_render_mesh", "so100_render",
+                    "so100_contact_count", "so100_contact_counts", "so100_chunk_info", "so100_render_mesh", "so100_render",
                     "so100_set_step_mode", "so100_step_mode", "so100_hull_cells", "so100_set_fused_build",
                     "so100_fused_build")
 

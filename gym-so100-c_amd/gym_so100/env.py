@@ -27,6 +27,14 @@ except ImportError:          # gymnasium is optional here
             return None
 
 
+def _check_seed(seed):
+    """numpy.random.RandomState(seed) accepts integers in [0, 2**32) (utils.py:24); so does the cube spawn."""
+    s = int(seed)
+    if not 0 <= s < 2 ** 32:
+        raise ValueError(f"Seed must be between 0 and 2**32 - 1 (got {seed})")
+    return s
+
+
 class SO100Env(_Base):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 50}
 
@@ -65,8 +73,11 @@ class SO100Env(_Base):
         self.action_space = spaces.Box(low=-1, high=1, shape=(len(SO100_ACTIONS),), dtype=np.float32)
 
     def reset(self, seed=None, options=None):
+        """seed: an int in [0, 2**32) spawns the cube as numpy's RandomState(seed) (utils.py:18-29, which rejects
+        other values); None draws a fresh spawn (in-kernel seed from the env's base seed and episode counter,
+        where the reference's RandomState(None) draws from OS entropy)."""
         super().reset(seed=seed)
-        obs, _ = self._venv.reset(seed=None if seed is None else [int(seed)])
+        obs, _ = self._venv.reset(seed=None if seed is None else [_check_seed(seed)])
         return self._np_obs(obs), {"is_success": False}                 # env.py:169
 
     def _np_obs(self, obs):
@@ -134,7 +145,7 @@ class SO100GoalEnv(_Base):
     def reset(self, seed=None, options=None):
         super().reset(seed=seed)
         self.current_step = 0
-        obs, _ = self._venv.reset(seed=None if seed is None else [int(seed)])
+        obs, _ = self._venv.reset(seed=None if seed is None else [_check_seed(seed)])
         return self._goal_obs(obs), {"is_success": False}
 
     def compute_reward(self, achieved_goal, desired_goal, info):

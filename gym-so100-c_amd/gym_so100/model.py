@@ -29,8 +29,9 @@ PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 151: (pad i, bin box j) at 15
 NPAIR_PAD = 8 * (1 + NBINBOX)                    # 48
 NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 191
 NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
-MAXCON, CONDIM, NOBS = 16, 4, 15
-NEFC_MAX = NV + NHINGE + MAXCON * CONDIM
+MAXCON, CONDIM, NOBS = 16, 4, 15      # MAXCON: contacts an env holds on chip (include/so100_model.h)
+NCON_MAX = 53 * 8 + 191 - 53           # SO100_NCON_MAX: the whole contact list (every pair at its maximum)
+NEFC_MAX = NV + NHINGE + NCON_MAX * CONDIM
 
 _d = ctypes.c_double
 _i = ctypes.c_int

@@ -463,6 +463,15 @@ class SO100VecEnv:
         _native.check(self.lib.so100_contact_count(self._handle, _native.ptr(accum), self._stream()),
                       "so100_contact_count")
 
+    def contact_counts(self):
+        """int32 device tensor [N]: each env's contact count in the last solver launch (the last substep's list;
+        up to SO100_NCON_MAX, the first 16 held on chip)."""
+        torch = _torch()
+        out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        _native.check(self.lib.so100_contact_counts(self._handle, _native.ptr(out), self._stream()),
+                      "so100_contact_counts")
+        return out
+
     def close(self):
         if getattr(self, "_handle", None):
             self.lib.so100_destroy(self._handle)

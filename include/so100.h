@@ -13,7 +13,8 @@
  * Conventions: plain pointers and sizes only; every array is DEVICE memory allocated by the caller
  * (PyTorch-ROCm tensors in the Python layer); row-major [n_envs, dim].  Calls enqueue on `stream`
  * (a hipStream_t, NULL = default stream) and never synchronise the host.  Status: 0 = ok, < 0 = error
- * (message in so100_last_error()).  No C++ exceptions cross this boundary.
+ * (message in so100_last_error()): -1 bad arguments / model, -2 a HIP error, -3 a C++ exception caught at the
+ * boundary (e.g. host memory exhausted).  No C++ exceptions cross this boundary.
  */
 #ifndef SO100_H
 #define SO100_H
@@ -24,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 13  /* 13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 14  /* 14: no per-env contact cap (SO100_NCON_MAX: every pair at its collider's maximum), debug stride 3,436 (SO100_DBG_OVF), ncon_dropped always 0, status -3 for a caught C++ exception;  13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -71,14 +72,16 @@ typedef struct so100_buffers {
    * holds its float32 rounding, exact for the CubeToBin / sparse / GoalEnv ladders, rounded for the dense
    * TouchCube shaping); NULL = not written */
   double*   reward64;
-  /* [N] contacts the 16-per-env cap (SO100_MAXCON) left out, summed over the step's substeps: the counterpart
-   * of the oracle's ncon_dropped (MuJoCo has no such cap; 0 is the bar).  NULL = not written */
+  /* [N] contacts left out of the env's contact list, summed over the step's substeps (the oracle's ncon_dropped).
+   * Since ABI 14 the list holds every contact (SO100_NCON_MAX, as MuJoCo keeps every contact), so this is always
+   * written as 0: kept as a checked invariant.  NULL = not written */
   uint32_t* ncon_dropped;
   /* Device-side episode statistics (what gymnasium's RecordEpisodeStatistics / SB3's VecMonitor keep on the
    * host, reference scripts/train_sac.py:290; SURVEY §5 Metrics), written by the step epilogue; the host reads
    * them only on demand.  ep_final and ep_accum are written only when ep_return is given.  NULL = not kept.
    *   ep_return [N]   return of the running episode: the sum of its float64 rewards so far; set to 0 when the
    *                   episode ends (terminated or truncated, with or without auto-reset) and by so100_reset;
+   *                   without auto-reset, an env stepped on past its TimeLimit without a reset is counted once;
    *   ep_final  [N,2] return and length (steps) of the env's last finished episode, written at its end;
    *   ep_accum  [N,4] over the env's finished episodes: count, successes (ended with is_success), sum of
    *                   returns, sum of lengths; never cleared by the library (the caller zeroes it). */
@@ -89,12 +92,14 @@ typedef struct so100_buffers {
 
 /* Debug record per env (floats), written by the last substep of a step when `debug` is not NULL:
  *   [0] ncon  [1] solver iterations  [2] last improvement  [3] nefc  [4..15] qacc (the last solve)
- *   [16..31] contact dist  [32..47] contact normal force (efc_force row 0 of contact c)
+ *   [16..31] contact dist  [32..47] contact normal force (efc_force row 0 of contact c)   (contacts c < 16)
  *   [48..63] contact pair id (-1 unused)  [64..75] qacc_smooth  [76..87] dof frictionloss forces
  *   [88..95] profiling stamps (diagnostic builds)
- *   [96..143] contact c's friction forces (efc_force rows 1..3 of contact c) at 96 + 3 c
- *   [144..159] reserved */
-#define SO100_DBG_STRIDE 160
+ *   [96..143] contact c's friction forces (efc_force rows 1..3 of contact c) at 96 + 3 c   (contacts c < 16)
+ *   [144..159] reserved
+ *   [SO100_DBG_OVF + 6 (c - 16) ...] contacts c >= 16 of the list: dist, pair id, normal force, 3 friction forces */
+#define SO100_DBG_OVF 160
+#define SO100_DBG_STRIDE (SO100_DBG_OVF + 6 * (SO100_NCON_MAX - SO100_MAXCON))   /* 3,436 */
 
 typedef struct so100_env so100_env;   /* opaque: device model copy + launch config */
 
@@ -172,6 +177,9 @@ int so100_chunk_info(const so100_env* env, int* nchunks, int* profiled_envs);
 /* Adds the contact count of the last solver launch, summed over the N envs, to *accum (DEVICE
  * uint64).  Enqueued on `stream`, no synchronisation. */
 int so100_contact_count(so100_env* env, uint64_t* accum, void* stream);
+/* Writes each env's contact count of the last solver launch (the last substep's list) to out (DEVICE int32 [N]).
+ * Enqueued on `stream`, no synchronisation.  (ABI 14) */
+int so100_contact_counts(so100_env* env, int32_t* out, void* stream);
 
 /* ---- camera images: the reference's default observation, obs_type
  * "so100_pixels_agent_pos" (gym_so100/__init__.py:4-32) = the `top` camera rendered by dm_control

@@ -61,9 +61,17 @@
 #define SO100_PAIR_TABLE 8          /* ("red_box", "table") — single_arm.py:354 touch_table */
 #define SO100_NPAIR_GRIPPER 8       /* pairs 0..7 — single_arm.py:348-352 touch_gripper   */
 #define SO100_MAXCONPAIR 8          /* contacts per box-box pair: every clipped point, as mjc_BoxBox */
-#define SO100_MAXCON 16             /* contacts kept per env per position stage           */
+/* box-box pairs that keep every clipped point: the cube against the 8 pads and the 5 bin boxes (pairs 0..13
+ * but the cube-table pair 8, whose table is a mesh: one convex contact) and the 40 pad-bin pairs */
+#define SO100_NPAIR_MULTI (SO100_NPAIR_BOX - 1 + SO100_NPAIR_PADBIN)                        /* 53 */
+/* The contact list of an env holds up to SO100_NCON_MAX contacts: every pair at its collider's maximum (8 for
+ * a multi-point box-box pair, 1 for the convex collider and the table rules), so no contact MuJoCo would keep
+ * can be left out (MuJoCo has no per-env cap).  The kernels hold the first SO100_MAXCON of them on chip (the
+ * solver's lane c owns contact c); the rest live in the env's HBM record (include/so100.h). */
+#define SO100_NCON_MAX (SO100_NPAIR_MULTI * SO100_MAXCONPAIR + SO100_NPAIR - SO100_NPAIR_MULTI)  /* 562 */
+#define SO100_MAXCON 16             /* contacts an env holds on chip (LDS / registers) per position stage */
 #define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, table/bin-hull pairs are 3 */
-#define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_MAXCON * SO100_CONDIM)
+#define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_NCON_MAX * SO100_CONDIM)
 #define SO100_SOLVER_PGS 0          /* projected Gauss-Seidel on the dual (mj_solPGS)               */
 #define SO100_SOLVER_NEWTON 1       /* primal Newton with exact line search (mj_solNewton)          */
 #define SO100_CONVEX_MPR 0          /* mesh pairs through libccd's MPR (MuJoCo behind mjDSBL_NATIVECCD)  */

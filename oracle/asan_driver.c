@@ -5,7 +5,7 @@
  * instrumented executable instead (`make -C oracle asan`; tests/test_oracle_sanitizers.py runs it).  It
  * loads a model written by gym_so100.model (the so100_model struct's bytes) and drives every oracle stage
  * over contact-rich states: random arm poses within the joint ranges (self-collision, Base and pad/link
- * hull contacts through MPR), cubes pressed into a bin corner (up to 12 contacts, the 16-contact cap),
+ * hull contacts through MPR), cubes pressed into a bin corner (up to 12 contacts: beyond the 16 the kernels hold on chip),
  * cubes spawned by RandomState seeds, and random actions, with the model's solver and variant.
  *
  * usage: oracle_asan_{64,32} <model.bin> <envs> <steps>      exit 0 = clean (a sanitizer report aborts)

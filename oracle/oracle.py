@@ -10,8 +10,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-NBODY, NHINGE, NQ, NV, NU, NGEOM, NPAIR, MAXCON, CONDIM, NOBS = 9, 6, 13, 12, 6, 15, 14, 16, 4, 15
-NEFC = NV + NHINGE + MAXCON * CONDIM
+NBODY, NHINGE, NQ, NV, NU, NGEOM, CONDIM, NOBS = 9, 6, 13, 12, 6, 15, 4, 15
+NCON_MAX = 53 * 8 + 191 - 53         # include/so100_model.h SO100_NCON_MAX: every pair at its collider's maximum
+NEFC = NV + NHINGE + NCON_MAX * CONDIM
 
 
 def _arr(t, *dims):
@@ -37,7 +38,7 @@ def _make_types(real):
             ("site_cube", _arr(real, 3)), ("site_ee", _arr(real, 3)),
             ("cinert", _arr(real, NBODY, 13)), ("cdof", _arr(real, NV, 6)),
             ("qM", _arr(real, NV, NV)), ("qL", _arr(real, NV, NV)),
-            ("ncon", i), ("ncon_dropped", i), ("con", _arr(Contact, MAXCON)),
+            ("ncon", i), ("ncon_dropped", i), ("con", _arr(Contact, NCON_MAX)),
             ("nefc", i), ("efc_type", _arr(i, NEFC)), ("efc_id", _arr(i, NEFC)), ("efc_dim", _arr(i, NEFC)),
             ("efc_J", _arr(real, NEFC, NV)),
             ("efc_pos", _arr(real, NEFC)), ("efc_margin", _arr(real, NEFC)), ("efc_frictionloss", _arr(real, NEFC)),
@@ -47,14 +48,14 @@ def _make_types(real):
             ("cvel", _arr(real, NBODY, 6)), ("cdof_dot", _arr(real, NV, 6)), ("qfrc_bias", _arr(real, NV)),
             ("efc_vel", _arr(real, NEFC)),
             ("actuator_force", _arr(real, NU)), ("qfrc_actuator", _arr(real, NV)), ("qacc_smooth", _arr(real, NV)),
-            ("efc_aref", _arr(real, NEFC)), ("efc_b", _arr(real, NEFC)), ("efc_AR", _arr(real, NEFC, NEFC)),
+            ("efc_aref", _arr(real, NEFC)), ("efc_b", _arr(real, NEFC)),
             ("efc_force", _arr(real, NEFC)), ("qacc", _arr(real, NV)),
             ("solver_iter", i), ("solver_improvement", real), ("elapsed_steps", i),
             ("mocap_pos", _arr(real, 3)), ("mocap_quat", _arr(real, 4)),
             ("weld_pos", _arr(real, 6)), ("weld_J", _arr(real, 6, NV)), ("weld_D", _arr(real, 6)),
             ("weld_aref", _arr(real, 6)), ("weld_f", _arr(real, NV)),
-            ("snap_ncon", i), ("snap_ndrop", i), ("snap_pair", _arr(i, MAXCON)),
-            ("snap_force", _arr(real, MAXCON, 4)), ("snap_frf", _arr(real, NV)), ("snap_qacc", _arr(real, NV)),
+            ("snap_ncon", i), ("snap_ndrop", i), ("snap_pair", _arr(i, NCON_MAX)),
+            ("snap_force", _arr(real, NCON_MAX, 4)), ("snap_frf", _arr(real, NV)), ("snap_qacc", _arr(real, NV)),
         ]
     return Contact, Data
 

@@ -10,6 +10,7 @@
  */
 #include "so100_oracle.h"
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -571,7 +572,8 @@ static void make_frame(real f[9]) {
  *   pairs 106..145 (finger pad i, bin box j) box-box, like the cube's pairs.  The kernel appends the pad
  *     contacts after the MPR contacts in the same pair order. */
 static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
-  if (d->ncon >= SO100_MAXCON) { d->ncon_dropped++; return; }
+  /* the list has room for every pair at its collider's maximum (SO100_NCON_MAX): nothing is dropped */
+  if (d->ncon >= SO100_NCON_MAX) { d->ncon_dropped++; return; }
   so100o_contact* con = &d->con[d->ncon++];
   *con = *c;
   con->pair = p;
@@ -1671,7 +1673,7 @@ static void force_from_jar(const so100_model* m, const so100o_data* d, const rea
 
 /* [3P] mj_solPGS: projected Gauss-Seidel on the dual, elliptic contact blocks (normal first, then
  * friction by QCQP), improvement-based termination scaled by 1/(meaninertia*nv). */
-static void sol_pgs(const so100_model* m, so100o_data* d) {
+static void sol_pgs(const so100_model* m, so100o_data* d, const real* AR) {
   const int nefc = d->nefc;
   real* f = d->efc_force;
   const real scale = 1 / ((real)m->meaninertia * (real)NV);
@@ -1684,12 +1686,12 @@ static void sol_pgs(const so100_model* m, so100o_data* d) {
       real res[4], old[4];
       for (int k = 0; k < dim; k++) {
         real s = d->efc_b[i + k];
-        for (int j = 0; j < nefc; j++) s += d->efc_AR[i + k][j] * f[j];
+        for (int j = 0; j < nefc; j++) s += AR[(size_t)(i + k) * nefc + j] * f[j];
         res[k] = s;
         old[k] = f[i + k];
       }
       if (dim == 1) {
-        f[i] -= res[0] / d->efc_AR[i][i];
+        f[i] -= res[0] / AR[(size_t)i * nefc + i];
         if (d->efc_type[i] == SO100O_EFC_FRICTION) {
           real fl = d->efc_frictionloss[i];
           f[i] = f[i] < -fl ? -fl : (f[i] > fl ? fl : f[i]);
@@ -1697,7 +1699,7 @@ static void sol_pgs(const so100_model* m, so100o_data* d) {
           f[i] = 0;
         }
       } else {
-        f[i] -= res[0] / d->efc_AR[i][i];
+        f[i] -= res[0] / AR[(size_t)i * nefc + i];
         if (f[i] < MINVAL) {
           f[i] = 0;
           for (int k = 1; k < dim; k++) f[i + k] = 0;
@@ -1705,9 +1707,9 @@ static void sol_pgs(const so100_model* m, so100o_data* d) {
           real Af[3][3], bf[3], x[3];
           int nf = dim - 1;
           for (int a = 0; a < nf; a++) {
-            bf[a] = res[1 + a] + d->efc_AR[i + 1 + a][i] * (f[i] - old[0]);
+            bf[a] = res[1 + a] + AR[(size_t)(i + 1 + a) * nefc + i] * (f[i] - old[0]);
             for (int c = 0; c < nf; c++) {
-              Af[a][c] = d->efc_AR[i + 1 + a][i + 1 + c];
+              Af[a][c] = AR[(size_t)(i + 1 + a) * nefc + i + 1 + c];
               bf[a] -= Af[a][c] * old[1 + c];
             }
           }
@@ -1719,7 +1721,7 @@ static void sol_pgs(const so100_model* m, so100o_data* d) {
       for (int k = 0; k < dim; k++) delta[k] = f[i + k] - old[k];
       for (int k = 0; k < dim; k++) {
         real q = 0;
-        for (int c = 0; c < dim; c++) q += d->efc_AR[i + k][i + c] * delta[c];
+        for (int c = 0; c < dim; c++) q += AR[(size_t)(i + k) * nefc + i + c] * delta[c];
         improvement -= delta[k] * (res[k] + (real)0.5 * q);
       }
       i += dim;
@@ -1997,8 +1999,10 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   for (int i = 0; i < nefc; i++)
     d->efc_aref[i] = -d->efc_B[i] * d->efc_vel[i] - d->efc_K[i] * d->efc_imp[i] * (d->efc_pos[i] - d->efc_margin[i]);
   if (m->solver == SO100_SOLVER_NEWTON) { sol_newton(m, d); return; }
-  /* [3P] mj_projectConstraint: b, AR = J M^-1 J' + R */
+  /* [3P] mj_projectConstraint: b, AR = J M^-1 J' + R (nefc x nefc, on the heap: the list may be long) */
   static __thread real MJT[NEFC][NV];
+  real* AR = (real*)malloc(sizeof(real) * (size_t)nefc * (size_t)nefc);
+  if (!AR) abort();
   for (int i = 0; i < nefc; i++) {
     real s = 0;
     for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * d->qacc_smooth[k];
@@ -2009,7 +2013,7 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
     for (int j = 0; j < nefc; j++) {
       real s = 0;
       for (int k = 0; k < NV; k++) s += d->efc_J[i][k] * MJT[j][k];
-      d->efc_AR[i][j] = s + (i == j ? d->efc_R[i] : 0);
+      AR[(size_t)i * nefc + j] = s + (i == j ? d->efc_R[i] : 0);
     }
   /* [3P] warmstart (mj_fwdConstraint, dual solver): force from jar(qacc_warmstart); keep it only if
    * its dual cost 0.5 f'ARf + f'b is not positive */
@@ -2023,11 +2027,12 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   real cost = 0;
   for (int i = 0; i < nefc; i++) {
     real s = 0;
-    for (int j = 0; j < nefc; j++) s += d->efc_AR[i][j] * d->efc_force[j];
+    for (int j = 0; j < nefc; j++) s += AR[(size_t)i * nefc + j] * d->efc_force[j];
     cost += d->efc_force[i] * ((real)0.5 * s + d->efc_b[i]);
   }
   if (cost > 0) memset(d->efc_force, 0, sizeof(real) * nefc);
-  sol_pgs(m, d);
+  sol_pgs(m, d, AR);
+  free(AR);
   /* qacc = qacc_smooth + M^-1 J' f */
   for (int k = 0; k < NV; k++) {
     real s = 0;
@@ -2100,7 +2105,7 @@ double so100o_env_step(const so100_model* m, so100o_data* d, int task, const flo
   memset(d->snap_force, 0, sizeof(d->snap_force));
   memset(d->snap_frf, 0, sizeof(d->snap_frf));
   for (int c = 0; c < d->ncon; c++) d->snap_pair[c] = d->con[c].pair;
-  for (int c = d->ncon; c < SO100_MAXCON; c++) d->snap_pair[c] = -1;
+  for (int c = d->ncon; c < SO100_NCON_MAX; c++) d->snap_pair[c] = -1;
   for (int i = 0; i < d->nefc; i++) {
     if (d->efc_type[i] == SO100O_EFC_FRICTION) d->snap_frf[d->efc_id[i]] = d->efc_force[i];
     if (d->efc_type[i] != SO100O_EFC_CONTACT || d->efc_dim[i] == 0) continue;

@@ -68,6 +68,29 @@ def test_episode_statistics_match_host_restatement(fused):
     v.close()
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_episode_statistics_without_autoreset(fused):
+    """autoreset=False and no reset after the TimeLimit: the env keeps reporting truncated, but its episode is
+    counted once, with its length at the limit (the totals grew on every later step before)."""
+    from gym_so100 import SO100VecEnv
+    torch.cuda.set_device(0)
+    n = 32
+    v = SO100VecEnv(n, device="cuda:0", seed=5, max_episode_steps=5, reward64=True, episode_stats=True,
+                    autoreset=False)
+    v.fused = fused
+    v.reset(seed=40)
+    a = torch.zeros(n, 6, device=v.device)
+    for t in range(9):
+        _, _, term, trunc, _ = v.step(a)
+        torch.cuda.synchronize()
+        assert bool(trunc.all()) == (t >= 4)
+    acc = v.ep_accum.cpu().numpy()
+    assert not term.any()
+    assert np.all(acc[:, 0] == 1.0) and np.all(acc[:, 3] == 5.0)
+    assert np.all(v.ep_final.cpu().numpy()[:, 1] == 5.0)
+    v.close()
+
+
 def test_sb3_episode_info():
     """VecMonitor's info["episode"] for the envs that finished, from the kernel's statistics."""
     from gym_so100.sb3 import SO100SB3VecEnv

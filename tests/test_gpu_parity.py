@@ -128,12 +128,21 @@ def _step_all_builds(env, act):
 
 def _gpu_solve(dbg_row):
     """(pairs, forces [ncon, 4], dof frictionloss forces, qacc) of the last solve from a debug record row
-    (include/so100.h SO100_DBG_STRIDE layout)."""
+    (include/so100.h SO100_DBG_STRIDE layout: contacts 0..15 in the fixed fields, the rest of the list from
+    SO100_DBG_OVF, 6 floats each)."""
+    from gym_so100._native import SO100_DBG_OVF
     nc = int(dbg_row[0])
+    n0 = min(nc, 16)
     f = np.zeros((nc, 4))
-    f[:, 0] = dbg_row[32:32 + nc]
-    f[:, 1:] = dbg_row[96:96 + 3 * 16].reshape(16, 3)[:nc]
-    return dbg_row[48:48 + nc].astype(np.int64), f, dbg_row[76:88].astype(np.float64), dbg_row[4:16].astype(np.float64)
+    pairs = np.zeros(nc, np.int64)
+    f[:n0, 0] = dbg_row[32:32 + n0]
+    f[:n0, 1:] = dbg_row[96:96 + 3 * 16].reshape(16, 3)[:n0]
+    pairs[:n0] = dbg_row[48:48 + n0]
+    if nc > 16:
+        ov = dbg_row[SO100_DBG_OVF:SO100_DBG_OVF + 6 * (nc - 16)].reshape(nc - 16, 6)
+        pairs[16:] = ov[:, 1]
+        f[16:] = ov[:, 2:6]
+    return pairs, f, dbg_row[76:88].astype(np.float64), dbg_row[4:16].astype(np.float64)
 
 
 def _force_err(f, fo):
@@ -156,6 +165,9 @@ class TF:
 
     def __init__(self):
         self.qp, self.qv, self.fqp, self.fqv, self.qa, self.fqa = [], [], [], [], [], []
+        # the ensemble floor (_tf_run ens=K): per env step the fp64 oracle's error under K independent 1-ulp
+        # input perturbations, qvel and qacc [steps, K], contact forces (lists equal to the fp64 oracle's)
+        self.eqv, self.eqa, self.eforce = [], [], []
         self.pqv, self.pqa, self.pforce, self.psame = [], [], [], []
         self.force, self.fforce, self.same, self.fsame, self.pairs = [], [], [], [], []
         self.drop_gpu, self.drop_ora = [], []
@@ -166,14 +178,16 @@ class TF:
 
     def arrays(self):
         for k in ("qp", "qv", "fqp", "fqv", "qa", "fqa", "pqv", "pqa", "pforce", "psame", "force", "fforce", "same",
-                  "fsame", "drop_gpu", "drop_ora", "near0"):
+                  "fsame", "drop_gpu", "drop_ora", "near0", "eqv", "eqa", "eforce"):
             setattr(self, k, np.array(getattr(self, k)))
         return self
 
     def floor(self, name, q):
-        """the larger of the two floors' q-quantile (q = 1: maximum) for qv / qa / force"""
-        f = {"qv": (self.fqv, self.pqv), "qa": (self.fqa, self.pqa), "force": (self.fforce, self.pforce)}[name]
-        return max(np.quantile(x, q) if len(x) else 0.0 for x in f)
+        """the largest of the floors' q-quantile (q = 1: maximum) for qv / qa / force: the fp32 restatement, the
+        single 1-ulp perturbation and, where it ran, the ensemble of K perturbations"""
+        f = {"qv": (self.fqv, self.pqv, self.eqv), "qa": (self.fqa, self.pqa, self.eqa),
+             "force": (self.fforce, self.pforce, self.eforce)}[name]
+        return max(np.quantile(np.ravel(x), q) if np.size(x) else 0.0 for x in f)
 
     def summary(self, label):
         q = lambda x, p: np.quantile(x, p) if len(x) else float("nan")
@@ -189,13 +203,15 @@ class TF:
                 f"{int(self.drop_gpu.sum())} oracle {int(self.drop_ora.sum())}")
 
 
-def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None):
+def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, ens=0):
     """Teacher-forced steps: each starts the product kernels, the debug build and both oracles from the
-    GPU's fp32 state (act_fn(step) -> [n, 6] float32 actions)."""
+    GPU's fp32 state (act_fn(step) -> [n, 6] float32 actions).  ens = K > 0: also the ensemble floor, the fp64
+    oracle from K independent 1-ulp perturbations of each state (TF.eqv / eqa / eforce)."""
     res = res or TF()
     n = env.num_envs
     d64, d32, dp, dq = o64.new_data(), o32.new_data(), o64.new_data(), o64.new_data()
     prng = np.random.default_rng(12345)
+    erng = np.random.default_rng(777)
     for step in range(steps):
         q0 = env.qpos.cpu().numpy().astype(np.float64)
         v0 = env.qvel.cpu().numpy().astype(np.float64)
@@ -249,6 +265,21 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None):
                 res.force += list(_force_err(gf, f64))
                 res.fforce += list(_force_err(f32, f64))
             res.states.append((q0[i], v0[i], w0[i], act[i]) + ((mocap[i],) if mocap is not None else ()))
+            if ens:
+                eq, ea = [], []
+                for _ in range(ens):
+                    o64.set_state(dp, q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)),
+                                  v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12)), w0[i])
+                    if mocap is not None:
+                        _set_mocap(dp, mocap[i])
+                    o64.env_step(model, dp, task, act[i])
+                    pe, fe, _, qae, _ = o64.last_solve(dp)
+                    eq.append(_rel(o64.get_state(dp)[1], ov))
+                    ea.append(_rel(qae, qa64))
+                    if np.array_equal(pe, p64) and len(pe):
+                        res.eforce += list(_force_err(fe, f64))
+                res.eqv.append(eq)
+                res.eqa.append(ea)
     return res
 
 
@@ -399,12 +430,14 @@ def test_chunking_invariance(monkeypatch, variant):
     from gym_so100 import SO100VecEnv
     n = 4160
     kw = dict(device="cuda:0", seed=4, max_episode_steps=5, debug=True, variant=variant)
+    # chunks belong to the split path (a fused step is one launch), whose workspaces are made when it is first
+    # selected: while SO100_CHUNKS applies
     monkeypatch.setenv("SO100_CHUNKS", "1")
     one = SO100VecEnv(n, **kw)
+    one.fused = False
     monkeypatch.setenv("SO100_CHUNKS", "4")
     four = SO100VecEnv(n, **kw)
-    for e in (one, four):
-        e.fused = False                  # chunks belong to the split path (a fused step is one launch)
+    four.fused = False
     assert one.chunk_info() == (1, n)
     k, n0 = four.chunk_info()
     assert k == 4 and n0 < n
@@ -670,7 +703,7 @@ def test_hull_table_parity(solver, oracle64, oracle32):
     assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
     assert r.bit_bad <= max(2, 0.05 * len(r.qv))
     _force_bars(r)
-    assert r.drop_gpu.sum() == 0
+    assert r.drop_gpu.sum() == 0 and r.drop_ora.sum() == 0
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -711,7 +744,7 @@ def test_pad_contact_parity(solver, oracle64, oracle32):
     assert np.quantile(r.qv, 0.9) <= 2 * r.floor("qv", 0.9) + 1e-4
     assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
     _force_bars(r)
-    assert r.drop_gpu.sum() == 0
+    assert r.drop_gpu.sum() == 0 and r.drop_ora.sum() == 0
 
 
 @pytest.mark.parametrize("solver,convex", [("newton", "epa"), ("pgs", "epa"), ("newton", "mpr"), ("pgs", "mpr")])
@@ -763,7 +796,7 @@ def test_mpr_contact_parity(solver, convex, oracle64, oracle32):
         assert np.median(r.force) <= 2 * r.floor("force", 0.5) + 1e-6
         assert np.mean(r.force > 1e-4) <= 1.5 * max(np.mean(r.fforce > 1e-4), np.mean(r.pforce > 1e-4)) + 0.05
         assert np.median(r.qa) <= 2 * r.floor("qa", 0.5) + 1e-6
-    assert r.drop_gpu.sum() == 0
+    assert r.drop_gpu.sum() == 0 and r.drop_ora.sum() == 0
 
 
 def test_newton_solver_parity(oracle64, oracle32):
@@ -803,7 +836,7 @@ def test_newton_solver_parity(oracle64, oracle32):
     assert np.quantile(r.qv, 0.9) <= 2 * r.floor("qv", 0.9) + 1e-4
     assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
     _force_bars(r, median_abs=1e-4)
-    assert r.drop_gpu.sum() == 0
+    assert r.drop_gpu.sum() == 0 and r.drop_ora.sum() == 0
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -854,12 +887,34 @@ def test_domain_randomization_config4_shard(solver):
     shard.close()
 
 
-def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed, strict=True, nsubstep=None):
-    """random arm configurations with a contact in pairs [p0, p1), the actuators holding them;
-    teacher-forced GPU steps at the fp32 floor.  strict: the GPU's median within 2x the fp32 restatement's
-    median and its max within 2x its max (+1e-3); otherwise (pad-link: the pads sit inside the jaw hulls, deep
-    overlaps on both sides of a pad) the median within the floor's upper quartile, the p95 within 2x its p95
-    and the max within 5x its max."""
+ENS = 8     # the ensemble floor's size: independent 1-ulp perturbations of each state
+
+
+def _ensemble_bars(r, name="qv"):
+    """The deep-fold gate (round 4): these states (links pushed centimetres into each other) are chaotic, so a
+    single perturbation's maximum is a noisy bar that legal fp reorderings can cross.  The GPU's error
+    distribution is graded against the ensemble of ENS independent 1-ulp input perturbations of the fp64 oracle
+    (and the fp32 restatement) on the same states: median, p90 and p99 within 2x the floor's (+1e-5 / 1e-4),
+    the tail mass (share off by more than 1e-4) within 1.5x the floor's (+0.03), and per state the GPU beyond
+    every ensemble member of its own state (2x + 1e-5) at most as often as one member would be (1 / (ENS + 1))."""
+    g = getattr(r, name)
+    f = {"qv": r.fqv, "qa": r.fqa}[name]
+    E = np.asarray({"qv": r.eqv, "qa": r.eqa}[name])
+    ens = E.ravel()
+    fl = lambda q: max(np.quantile(f, q), np.quantile(ens, q))
+    assert np.median(g) <= 2 * fl(0.5) + 1e-5, (name, np.median(g), fl(0.5))
+    assert np.quantile(g, 0.9) <= 2 * fl(0.9) + 1e-4, (name, np.quantile(g, 0.9), fl(0.9))
+    assert np.quantile(g, 0.99) <= 2 * fl(0.99) + 1e-4, (name, np.quantile(g, 0.99), fl(0.99))
+    tail = lambda x: np.mean(np.asarray(x) > 1e-4)
+    assert tail(g) <= 1.5 * max(tail(f), tail(ens)) + 0.03, (name, tail(g), tail(f), tail(ens))
+    beyond = g > 2 * np.maximum(E.max(axis=1), f) + 1e-5
+    assert beyond.mean() <= 1.0 / (E.shape[1] + 1), (name, beyond.mean())
+    return beyond
+
+
+def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed, nsubstep=None, select=None):
+    """random arm configurations with a contact in pairs [p0, p1) (or select(d)), the actuators holding them;
+    teacher-forced GPU steps graded against the ensemble floor (_ensemble_bars) on qvel and qacc."""
     from gym_so100.model import build_model
     model = build_model(solver=solver, nsubstep=nsubstep)
     rng = np.random.default_rng(seed)
@@ -873,7 +928,7 @@ def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed, strict=
         for k in range(6):
             d.qpos[k] = arm[k]
         oracle64.call("so100o_fwd_position", model, d)
-        if any(p0 <= d.con[i].pair < p1 for i in range(d.ncon)) and not d.ncon_dropped:
+        if (select(d) if select else any(p0 <= d.con[i].pair < p1 for i in range(d.ncon))) and not d.ncon_dropped:
             q, v, w, _ = oracle64.get_state(d)
             states.append((q, v * 0, w * 0))
             targets.append(np.clip((arm - lo) / (hi - lo) * 2 - 1, -1, 1))
@@ -882,25 +937,24 @@ def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed, strict=
     env = _new_env(n, solver, nsubstep=nsubstep)
     env.reset(seed=3)
     _set_states(env, states)
-    r = _tf_run(env, model, oracle64, oracle32, 3, lambda step: targets + rng.normal(0, 0.02, (n, 6))).arrays()
+    r = _tf_run(env, model, oracle64, oracle32, 3, lambda step: targets + rng.normal(0, 0.02, (n, 6)), ens=ENS).arrays()
     env.close()
     cls = np.array([int(((p >= p0) & (p < p1)).sum()) for p in r.pairs])
+    E = r.eqv
     print(f"\nGPU {label} contacts per env mean {cls.mean():.2f} (envs with any: {(cls > 0).mean():.2f}); "
           + r.summary(f"{solver} {label}" + (f", {nsubstep} substep per env step" if nsubstep else "")))
+    q = lambda x, p: np.quantile(np.ravel(x), p)
+    print(f"ensemble floor ({E.shape[1]} perturbations x {E.shape[0]} steps): qvel median / p90 / p99 / max "
+          f"{q(E, .5):.2e} / {q(E, .9):.2e} / {q(E, .99):.2e} / {E.max():.2e}; GPU p99 {q(r.qv, .99):.2e}; "
+          f"contact-list flips (GPU vs fp64 oracle, last substep): {int((~r.same).sum())} of {len(r.same)}")
     assert (cls > 0).mean() > 0.5
-    if strict:
-        assert np.median(r.qv) <= 2 * r.floor("qv", 0.5) + 1e-5
-        # the max over the env-steps whose GPU and oracle contact lists agree: a contact that one side sees
-        # and the other does not (a deep fold's vertex on the boundary of another hull) is a discrete flip that
-        # fp32 cannot resolve as fp64 does; the flips are counted and kept rare
-        print(f"contact-list flips (GPU vs fp64 oracle, last substep): {int((~r.same).sum())} of {len(r.same)}")
-        assert r.same.mean() >= 0.95
-        assert r.qv[r.same].max() <= 2 * r.floor("qv", 1.0) + 1e-3
-    else:
-        assert np.median(r.qv) <= 2 * r.floor("qv", 0.75) + 1e-5
-        assert np.quantile(r.qv, 0.95) <= 2 * r.floor("qv", 0.95) + 1e-3
-        assert r.qv.max() <= 5 * r.floor("qv", 1.0) + 1e-3
-    assert np.mean(r.qv > 1e-4) <= 1.5 * max(np.mean(r.fqv > 1e-4), np.mean(r.pqv > 1e-4)) + 0.05    # tail mass (MPR portals)
+    # a contact one side sees and the other does not (a deep fold's vertex on another hull's boundary) is a
+    # discrete flip fp32 cannot resolve as fp64 does: counted and kept rare
+    assert r.same.mean() >= 0.9
+    beyond = _ensemble_bars(r, "qv")
+    _ensemble_bars(r, "qa")
+    print(f"GPU steps beyond their state's whole ensemble (2x + 1e-5): {int(beyond.sum())} of {len(beyond)}")
+    assert r.drop_gpu.sum() == 0 and r.drop_ora.sum() == 0     # every contact kept (no per-env cap, as MuJoCo)
     return r
 
 
@@ -926,7 +980,7 @@ def test_pad_link_contact_parity(solver, oracle64, oracle32):
     the pair table is every pair MuJoCo's filters leave): random arm configurations folding a jaw onto a
     link, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
     from gym_so100.model import PAIR_PADLINK0, PAIR_PAD0
-    _arm_contact_parity(solver, oracle64, oracle32, PAIR_PADLINK0, PAIR_PAD0, "pad-link", 23, strict=False)
+    _arm_contact_parity(solver, oracle64, oracle32, PAIR_PADLINK0, PAIR_PAD0, "pad-link", 23)
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -941,10 +995,31 @@ def test_arm_contact_substep_parity(solver, cls, oracle64, oracle32):
     from gym_so100.model import PAIR_SELF0, PAIR_BASE0, PAIR_PADLINK0, PAIR_PAD0
     p0, p1, seed = {"self": (PAIR_SELF0, PAIR_BASE0, 17), "base": (PAIR_BASE0, PAIR_PADLINK0, 19),
                     "padlink": (PAIR_PADLINK0, PAIR_PAD0, 23)}[cls]
-    r = _arm_contact_parity(solver, oracle64, oracle32, p0, p1, cls, seed, strict=True, nsubstep=1)
+    r = _arm_contact_parity(solver, oracle64, oracle32, p0, p1, cls, seed, nsubstep=1)
     _force_bars(r, median_abs=1e-4 if solver == "newton" else None)
     if solver == "newton":
         assert np.median(r.qv) <= 1e-4 and np.median(r.qa) <= 1e-4
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+@pytest.mark.parametrize("nsubstep", [1, None])
+def test_overflow_contact_parity(solver, nsubstep, oracle64, oracle32):
+    """Contact lists longer than the 16 an env holds on chip (round 4: no per-env cap, as MuJoCo): random arm
+    poses whose first position stage holds more than 16 contacts (jaws and pads jammed into the bin walls, folds
+    into the Base and the links; 17-73 contacts), the actuators holding them.  The contacts beyond 16 live in the
+    env's HBM contact record (J, the rows, the solve's per-contact state); teacher-forced GPU steps against the
+    fp64 oracle, which keeps every contact too, per substep (nsubstep = 1) and per env step.  No contact may be
+    dropped by either side, and the per-contact forces of the whole list (debug record, SO100_DBG_OVF) are graded."""
+    from gym_so100.model import NPAIR
+    r = _arm_contact_parity(solver, oracle64, oracle32, 0, NPAIR, "overflow", 29, nsubstep=nsubstep,
+                            select=lambda d: d.ncon > 16)
+    ncon = np.array([len(p) for p in r.pairs])
+    print(f"GPU contact-list length: mean {ncon.mean():.1f}, max {ncon.max()}, share > 16: {(ncon > 16).mean():.2f}")
+    assert (ncon > 16).mean() > 0.5 and ncon.max() > 32       # the record's contacts really take part
+    if nsubstep == 1:
+        _force_bars(r, median_abs=1e-4 if solver == "newton" else None)
+        if solver == "newton":
+            assert np.median(r.qv) <= 1e-4 and np.median(r.qa) <= 1e-4
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -1100,12 +1175,10 @@ def test_product_builds_bitwise(n):
 def test_config2_benched_full_size(fused):
     """configs[2] as bench.py times it on one GPU: 65,536 envs in one process, the fused step (auto mode, the
     benched path) and the split step (4 env chunks on concurrent streams), with auto-reset; 40 steps of random
-    actions keep the state
-    finite and the contract: unit quaternions, obs layout, reward ladder, no divergence, TimeLimit counters,
-    and the 16-per-env contact cap binding as rarely as in the oracle: MuJoCo keeps every box-box point (up to 8
-    per pair), and a jaw jammed into the bin walls collects 20-46 pad-bin contacts, so the cap drops some; the
-    fp64 oracle on this workload drops 3.4e-4 per env step (tools/dev/contact_drops.py, 65,536 x 40), the
-    bar is 1e-3 (DESIGN.md §4 deviation 2)."""
+    actions keep the state finite and the contract: unit quaternions, obs layout, reward ladder, no divergence,
+    TimeLimit counters, and every contact kept: MuJoCo keeps every box-box point (up to 8 per pair), and a jaw
+    jammed into the bin walls collects 20-46 pad-bin contacts; the list holds them all (no per-env cap since
+    round 4), so none is dropped, and the envs with more than the 16 held on chip are counted."""
     from gym_so100 import SO100VecEnv
     n = 65536
     env = SO100VecEnv(n, device="cuda:0", seed=0)
@@ -1114,10 +1187,11 @@ def test_config2_benched_full_size(fused):
     assert env.chunk_info()[0] == (1 if fused else 4)
     env.reset(seed=1000)
     g = torch.Generator(device="cuda").manual_seed(0)
-    drops, rewards = 0, set()
+    drops, rewards, over16 = 0, set(), 0
     for k in range(40):
         obs, rew, term, trunc, info = env.step(torch.rand(n, 6, generator=g, device="cuda") * 2 - 1)
         drops += int(info["ncon_dropped"].sum())
+        over16 += int((env.contact_counts() > 16).sum())
         if k % 10 == 9:
             rewards |= set(torch.unique(rew).tolist())
     torch.cuda.synchronize()
@@ -1137,8 +1211,9 @@ def test_config2_benched_full_size(fused):
     assert not info["diverged"].any()
     assert ((env.elapsed == 40) | (env.episode > 1)).all()         # TimeLimit 700 not reached (only successes reset)
     assert rewards <= {0.0, 1.0, 2.0, 2.5, 3.0, 4.0}
-    print(f"\n65,536 envs x 40 steps: contacts dropped by the 16-per-env cap: {drops} ({drops / (40 * n):.2e} per env step)")
-    assert drops / (40 * n) <= 1e-3
+    print(f"\n65,536 envs x 40 steps: env steps ending with more than the 16 contacts held on chip: {over16} "
+          f"({over16 / (40 * n):.2e} per env step); contacts dropped: {drops}")
+    assert drops == 0
     env.close()
 
 

@@ -237,7 +237,7 @@ def test_separated_boxes_no_contact(model, oracle64):
 
 def test_pgs_frictionloss_kkt(oracle64):
     """Arm moving, no contacts: every frictionloss row satisfies the box-constrained optimality (PGS, the
-    dual solver: efc_AR / efc_b are its data)."""
+    dual solver: AR = J M^-1 J' + R and efc_b are its data)."""
     from gym_so100.model import build_model
     model = build_model(solver="pgs")
     d = fresh(oracle64, model, box=(-0.2, 0.45, 0.5, 1, 0, 0, 0))
@@ -251,7 +251,9 @@ def test_pgs_frictionloss_kkt(oracle64):
     oracle64.call("so100o_fwd_acceleration", model, d)
     n = d.nefc
     assert n == 12 and d.ncon == 0
-    A = np.array([[d.efc_AR[i][j] for j in range(n)] for i in range(n)])
+    J = np.array([d.efc_J[i][:] for i in range(n)])
+    M = np.array([d.qM[i][:] for i in range(12)])
+    A = J @ np.linalg.solve(M, J.T) + np.diag(np.array(d.efc_R[:n]))
     b = np.array(d.efc_b[:n])
     f = np.array(d.efc_force[:n])
     fl = np.array(d.efc_frictionloss[:n])
