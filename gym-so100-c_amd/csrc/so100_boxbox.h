@@ -316,6 +316,10 @@ DEV void geom_pose_b(const DevModel* __restrict__ m, const EnvShared& sh, int g,
     for (int k = 0; k < 9; k++) mat[k] = m->geom_mat[g][k];
     return;
   }
+  if (b == SO100_MOCAP_BODY) {   // the EE variant's marker box: centred on the mocap body (so100_create checks)
+    cube_frame(sh.mocap, pos, mat);
+    return;
+  }
   const float* bp;
   const float* bm;
   if (b == SO100_CUBE_BODY) { bp = sh.cube_pos; bm = sh.cube_mat; }

@@ -330,7 +330,7 @@ int build_device_model(const so100_model* s, DevModel* d) {
   }
   // (finger pad, link hull) pairs through MPR: a pad box on a jaw against the Base or a link hull on bodies
   // 2..5 (the MPR kernel takes the pad's pose from its jaw's frame)
-  for (int p = SO100_PAIR_PADLINK0; p < SO100_PAIR_PAD0; p++) {
+  for (int p = SO100_PAIR_PADLINK0; p < SO100_PAIR_MOCAPHULL0; p++) {
     const int g1 = s->pair_geom1[p], k2 = -1 - s->pair_geom2[p];
     if (g1 < 1 || g1 > SO100_NPAD || (s->geom_body[g1] != 6 && s->geom_body[g1] != 7))
       return fail("model: pad-link pair p must have a finger pad as geom1");
@@ -339,8 +339,30 @@ int build_device_model(const so100_model* s, DevModel* d) {
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: pad-link pairs must have condim 3 or 4");
     if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
   }
+  // the EE variant's mocap marker box (geom SO100_MOCAP_GEOM on the mocap body, centred on it: the kernels take its
+  // pose as the mocap pose) against link hull k, through the convex collider
+  if (s->geom_body[SO100_MOCAP_GEOM] != SO100_MOCAP_BODY) return fail("model: the marker box must sit on the mocap body");
+  for (int k = 0; k < 3; k++)
+    if (s->geom_pos[SO100_MOCAP_GEOM][k] != 0 || s->geom_quat[SO100_MOCAP_GEOM][1 + k] != 0)
+      return fail("model: the marker box must be centred on the mocap body");
+  for (int p = SO100_PAIR_MOCAPHULL0; p < SO100_PAIR_PAD0; p++) {
+    const int k = p - SO100_PAIR_MOCAPHULL0;
+    if (s->pair_geom1[p] != SO100_MOCAP_GEOM || s->pair_geom2[p] != -1 - k) return fail("model: pair p must be (marker, hull k)");
+    if (s->pair_body1[p] != SO100_MOCAP_BODY || s->pair_body2[p] != s->hull_body[k]) return fail("model: marker-hull pair bodies");
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: marker pairs must have condim 3 or 4");
+    if (s->pair_margin[p] != 0) return fail("model: MPR pairs take no margin");
+  }
+  // (cube | pad i, marker box) box-box pairs
+  for (int p = SO100_PAIR_MOCAPBOX0; p < SO100_NPAIR; p++) {
+    const int i = p - SO100_PAIR_MOCAPBOX0;
+    if (s->pair_geom1[p] != (i == 0 ? SO100_CUBE_GEOM : i) || s->pair_geom2[p] != SO100_MOCAP_GEOM)
+      return fail("model: pair p must be (cube | pad i, marker)");
+    if (s->pair_body1[p] != s->geom_body[s->pair_geom1[p]] || s->pair_body2[p] != SO100_MOCAP_BODY)
+      return fail("model: marker box pair bodies");
+    if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: marker pairs must have condim 3 or 4");
+  }
   // pad pairs: (finger pad i, table) at SO100_PAIR_PAD0 + i, (pad i, bin box j) at SO100_PAIR_PADBIN0 + 5 i + j
-  for (int p = SO100_PAIR_PAD0; p < SO100_NPAIR; p++) {
+  for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_MOCAPBOX0; p++) {
     const bool tbl = p < SO100_PAIR_PADBIN0;
     const int q = p - SO100_PAIR_PADBIN0;
     const int i = tbl ? p - SO100_PAIR_PAD0 : q / SO100_NBINBOX, j = tbl ? 0 : 1 + q % SO100_NBINBOX;
@@ -353,7 +375,8 @@ int build_device_model(const so100_model* s, DevModel* d) {
   }
   for (int g = 0; g < SO100_NGEOM; g++) {
     int b = s->geom_body[g];
-    if (!(b == 0 || b == 6 || b == 7 || b == SO100_CUBE_BODY)) return fail("model: geoms must be static, on the jaws or the cube");
+    if (!(b == 0 || b == 6 || b == 7 || b == SO100_CUBE_BODY || (g == SO100_MOCAP_GEOM && b == SO100_MOCAP_BODY)))
+      return fail("model: geoms must be static, on the jaws, the cube or (the marker) the mocap body");
   }
 
   {
@@ -458,7 +481,9 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->pair_mu1[p] = (float)s->pair_friction[p][1];
     d->pair_margin[p] = (float)s->pair_margin[p];
     const int b1 = s->pair_body1[p], b2 = s->pair_body2[p];
-    if (b1 < 0 || b1 >= SO100_NBODY || b2 < 0 || b2 >= SO100_NBODY) return fail("model: pair body out of range");
+    // bodies 0..SO100_NBODY-1, or the mocap body (no dofs, welded to the world for the dynamics: invweight0 = 0)
+    if (b1 < 0 || b1 > SO100_NBODY || b2 < 0 || b2 > SO100_NBODY) return fail("model: pair body out of range");
+    static_assert(SO100_MOCAP_BODY == SO100_NBODY, "the mocap body follows the body arrays");
     // the kernels' box pairs take a geom's body from the pair (geom_pose_b)
     if ((s->pair_geom1[p] >= 0 && s->geom_body[s->pair_geom1[p]] != b1) ||
         (s->pair_geom2[p] >= 0 && s->geom_body[s->pair_geom2[p]] != b2))
@@ -468,8 +493,9 @@ int build_device_model(const so100_model* s, DevModel* d) {
     d->pair_cond4[p] = s->pair_condim[p] == 4;
     d->pair_arm[p] = (b1 >= 2 && b1 <= 7) || (b2 >= 2 && b2 <= 7);
     d->pair_cube[p] = b1 == SO100_CUBE_BODY || b2 == SO100_CUBE_BODY;
-    d->pair_tran[p] = (float)(s->body_invweight0[b1][0] + s->body_invweight0[b2][0]);
-    d->pair_rot[p] = (float)(s->body_invweight0[b1][1] + s->body_invweight0[b2][1]);
+    auto invw = [&](int b, int k) { return b == SO100_MOCAP_BODY ? 0.0 : s->body_invweight0[b][k]; };
+    d->pair_tran[p] = (float)(invw(b1, 0) + invw(b2, 0));
+    d->pair_rot[p] = (float)(invw(b1, 1) + invw(b2, 1));
   }
   for (int k = 0; k < SO100_NHULL_ALL; k++) {
     // the convex collider's support ids hold a vertex index in 10 bits (so100_convex.h sup_from_id)

@@ -959,8 +959,10 @@ DEV bool mpr_broadphase(const DevModel* __restrict__ m, const MprObj& o, int k) 
 
 // Broadphase bounding spheres (oracle mpr_broadphase stage 1), one per collision object: hull k at k (< 10,
 // the Base hull at 9), geom g (1..14: pads, cube, bin boxes) at 9 + g.  World centre (hull: its bounding box
-// centre; box: its centre) and radius (hull_half.w / geom_rbound), by the arithmetic mpr_sphere uses.
-constexpr int kSphObj = SO100_NHULL_ALL + SO100_NGEOM - 1;   // 24
+// centre; box: its centre) and radius (hull_half.w / geom_rbound), by the arithmetic mpr_sphere uses.  (The
+// EE variant's marker box, the last geom, has its own pass: marker_contacts.)
+static_assert(SO100_MOCAP_GEOM == SO100_NGEOM - 1, "the marker box is the last geom");
+constexpr int kSphObj = SO100_NHULL_ALL + SO100_MOCAP_GEOM - 1;   // 24
 DEV float4 sphere_obj(const DevModel* __restrict__ m, const EnvShared& sh, int o) {
   float c[3], r;
   if (o < SO100_NHULL_ALL) {
@@ -987,6 +989,28 @@ DEV float4 sphere_obj(const DevModel* __restrict__ m, const EnvShared& sh, int o
     r = m->geom_rbound[g];
   }
   return make_float4(c[0], c[1], c[2], r);
+}
+
+// a convex pair's contact (in hull k's body frame H) to the world, staged as the env's convex contact `slot`:
+// the LDS staging area, or (rare: beyond kMaxCon) the env's HBM contact record crec
+DEV void stage_convex_hit(const DevModel* __restrict__ m, EnvShared& sh, float* crec, int slot, int p, float depth,
+                          const float* dir, const float* pos) {
+  const int k = -1 - m->pair_g2[p];
+  float RH[9], pH[3], wn[3], wp[3];
+  hull_frame(m, sh, m->hull_body[k], RH, pH);
+  mulmv3(wn, RH, dir);
+  mulmv3(wp, RH, pos);
+  const float4 sp = make_float4(wp[0] + pH[0], wp[1] + pH[1], wp[2] + pH[2], -depth);
+  const float4 sn = make_float4(wn[0], wn[1], wn[2], __int_as_float(p));
+  if (slot < kMaxCon) {
+    MprStage& st = sh.mpr[slot];
+    st.pos[0] = sp.x; st.pos[1] = sp.y; st.pos[2] = sp.z; st.pos[3] = sp.w;
+    st.nrm[0] = sn.x; st.nrm[1] = sn.y; st.nrm[2] = sn.z; st.nrm[3] = sn.w;
+  } else {
+    float4* stg = reinterpret_cast<float4*>(crec + (size_t)slot * kConStride + kMprStageOff);
+    stg[0] = sp;
+    stg[1] = sn;
+  }
 }
 
 // The MPR pairs 23..142 of one substep ((cube | bin box, hull), hull-hull self-collision, the Base hull, the
@@ -1016,7 +1040,9 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
   // each env's candidates go to its dynamics scratch (RNE cdd + tau: dead from the collision on; the contact
   // area holds the rows' EPA polytopes)
-  static_assert(kConvex <= (int)(sizeof(shm[0].ser.cdd) + sizeof(shm[0].ser.tau)), "an env's candidate list fits");
+  static_assert(kConvex + SO100_NPAIR_MOCAPHULL <= (int)(sizeof(shm[0].ser.cdd) + sizeof(shm[0].ser.tau)),
+                "an env's candidate list fits");
+  static_assert(SO100_PAIR_MOCAPHULL0 == SO100_PAIR_MPR0 + kConvex, "the marker pairs follow the wave-shared pairs");
   static_assert(__builtin_offsetof(SerialScratch, cdd) >= sizeof(ConArea), "the candidate lists do not alias the contact area");
   // the sphere table and the sphere survivors' list in the env's MPR staging area
   static_assert(kSphObj * sizeof(float4) + kConvex <= sizeof(shm[0].mpr), "sphere table + list fit the staging area");
@@ -1055,7 +1081,8 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
   const int s0c = __builtin_amdgcn_readlane(scnt, 0), s1c = __builtin_amdgcn_readlane(scnt, 16);
   const int s2c = __builtin_amdgcn_readlane(scnt, 32), s3c = __builtin_amdgcn_readlane(scnt, 48);
   const int spre1 = s0c, spre2 = s0c + s1c, spre3 = s0c + s1c + s2c, stotal = spre3 + s3c;
-  if (stotal == 0) return 0;
+  const bool ee = m->ee;
+  if (stotal == 0 && !ee) return 0;
   {
     uint8_t* slist = reinterpret_cast<uint8_t*>(&shm[grp].mpr[0]) + kSphObj * sizeof(float4);
 #pragma unroll
@@ -1098,6 +1125,27 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
       c0 += __popcll(pb & e0); c1 += __popcll(pb & e1); c2 += __popcll(pb & e2); c3 += __popcll(pb & e3);
     }
   }
+  if (ee) {
+    // EE variant: the marker box against the 9 link hulls (pairs 143..151, list items kConvex + k): both broadphase
+    // stages on lanes 0..8 of the env's own row, the survivors appended to its list (they follow in pair order)
+    bool cand = false;
+    if (valid && lane < SO100_NPAIR_MOCAPHULL) {
+      const int p = SO100_PAIR_MOCAPHULL0 + lane;
+      if (mpr_sphere(m, sh, p)) {
+        MprObj o;
+        mpr_obj_setup(m, sh, p, o);
+        cand = mpr_broadphase(m, o, -1 - m->pair_g2[p]);
+      }
+    }
+    const uint64_t mb = __ballot(cand);
+    if (cand) {
+      const int base = grp == 0 ? c0 : grp == 1 ? c1 : grp == 2 ? c2 : c3;
+      const uint32_t row = (uint32_t)((mb >> (grp * 16)) & 0xFFFFull);
+      reinterpret_cast<uint8_t*>(&shm[grp].ser.cdd[0][0])[base + __popc(row & ((1u << lane) - 1u))] = (uint8_t)(kConvex + lane);
+    }
+    c0 += __popcll(mb & 0xFFFFull); c1 += __popcll(mb & (0xFFFFull << 16));
+    c2 += __popcll(mb & (0xFFFFull << 32)); c3 += __popcll(mb & (0xFFFFull << 48));
+  }
   const int pre1 = c0, pre2 = c0 + c1, pre3 = c0 + c1 + c2;
   const int total = pre3 + c3;
   if (total == 0) return 0;
@@ -1129,24 +1177,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
       const bool h = it < total && ((hb >> (16 * g)) & 1ull);
       if (g < grp && h && env_of(it) == ie) slot++;
     }
-    if (hit && lane == 0) {
-      const int k = -1 - m->pair_g2[p];
-      float RH[9], pH[3], wn[3], wp[3];
-      hull_frame(m, shm[ie], m->hull_body[k], RH, pH);
-      mulmv3(wn, RH, dir);
-      mulmv3(wp, RH, pos);
-      const float4 sp = make_float4(wp[0] + pH[0], wp[1] + pH[1], wp[2] + pH[2], -depth);
-      const float4 sn = make_float4(wn[0], wn[1], wn[2], __int_as_float(p));
-      if (slot < kMaxCon) {
-        MprStage& st = shm[ie].mpr[slot];
-        st.pos[0] = sp.x; st.pos[1] = sp.y; st.pos[2] = sp.z; st.pos[3] = sp.w;
-        st.nrm[0] = sn.x; st.nrm[1] = sn.y; st.nrm[2] = sn.z; st.nrm[3] = sn.w;
-      } else {                                // rare: the env's staging beyond kMaxCon, in its HBM record
-        float4* stg = reinterpret_cast<float4*>(crec0 + (size_t)ie * kConEnv + (size_t)slot * kConStride + kMprStageOff);
-        stg[0] = sp;
-        stg[1] = sn;
-      }
-    }
+    if (hit && lane == 0) stage_convex_hit(m, shm[ie], crec0 + (size_t)ie * kConEnv, slot, p, depth, dir, pos);
 #pragma unroll
     for (int g = 0; g < kEnvsPerBlock; g++) {
       const int it = kEnvsPerBlock * rd + g;

@@ -248,12 +248,13 @@ DEV void put_box_contacts(EnvShared& sh, float* crec, const PairContacts& pc, in
 }
 
 // Finger pads vs the table and the bin boxes (oracle collision(): pad_table, collide_box_pair).
-//   pairs 98..105 (pad i, table), lane i: the hull-table rule on the pad's 8 corners — the corners inside
+//   pairs 152..159 (pad i, table), lane i: the hull-table rule on the pad's 8 corners — the corners inside
 //     the top face's footprint and below the top count; one contact at the deepest corner's distance, at
 //     the counted corners' x-y centroid, midway in z between the deepest corner and the top; normal -z;
-//   pairs 106..145 (pad i, bin box j): a conservative test (the pad's bounding sphere against the static
+//   pairs 160..199 (pad i, bin box j): a conservative test (the pad's bounding sphere against the static
 //     box, 3 pairs per lane), the candidates compacted in pair order and run through the box-box
-//     collider 16 at a time (a wave runs as many rounds as its busiest env needs; usually none).
+//     collider 16 at a time (a wave runs as many rounds as its busiest env needs; usually none);
+//   (EE variant) pairs 200..208 (cube | pad i, the mocap marker box) join the pad-bin candidates.
 // Contacts are appended after `tot` in pair order; returns the new total.
 DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec, int lane, int grp, bool valid, int tot) {
   // ---- pad-table (lanes 0..7)
@@ -324,10 +325,12 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec,
   }
   tot += __popc(trow);
   // ---- pad-bin candidates (3 pairs per lane); the whole wave skips them when no pad is near the bin
-  if (__ballot(nearbin) == 0ull) return tot;
+  const bool anybin = __ballot(nearbin) != 0ull;
+  if (!anybin && !m->ee) return tot;
   uint64_t cm = 0ull;
 #pragma unroll
   for (int r = 0; r < 3; r++) {
+    if (!anybin) break;
     const int q = r * kLanes + lane;
     bool cand = false;
     if (valid && q < SO100_NPAIR_PADBIN) {
@@ -354,6 +357,11 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec,
     }
     cm |= ((__ballot(cand) >> (grp * 16)) & 0xFFFFull) << (16 * r);
   }
+  // EE variant: the cube and the pads against the marker box (pairs 200..208 = SO100_PAIR_PADBIN0 + 40 + i, after
+  // the pad-bin pairs in pair order): every one a candidate (collide_pair's bounding spheres decide)
+  static_assert(SO100_PAIR_MOCAPBOX0 == SO100_PAIR_PADBIN0 + SO100_NPAIR_PADBIN, "the marker pairs follow the pad-bin pairs");
+  static_assert(SO100_NPAIR_PADBIN + SO100_NPAIR_MOCAPBOX <= 64, "one candidate mask");
+  if (m->ee && valid) cm |= ((1ull << SO100_NPAIR_MOCAPBOX) - 1ull) << SO100_NPAIR_PADBIN;
   const int ncand = __popcll(cm);
   const int rounds = (wave_max_i(ncand) + kLanes - 1) / kLanes;
   for (int r = 0; r < rounds; r++) {
@@ -449,6 +457,10 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     // ---------------- S3: collision: hulls vs the table (lane k = hull k), box-hull pairs by MPR
     // (staged in LDS), one box pair per lane; compaction in pair order (box pairs, table-hull pairs,
     // box-hull pairs)
+    // (the convex pairs first: the other collision results are then not held across their narrowphase's register
+    // peak; the contacts are compacted in pair order below whatever the order of computation)
+    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, args.w.con + (size_t)(env - grp) * kConEnv, lane, grp, valid);
+    SSTAMP(7);
     float hx, hy, hz;
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
     const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
@@ -456,8 +468,6 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     // the env's contact record in HBM: the contacts beyond the kMaxCon held on chip (every kernel), and the
     // split path's solver record
     float* const crec = args.w.con + (size_t)e * kConEnv;
-    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, args.w.con + (size_t)(env - grp) * kConEnv, lane, grp, valid);
-    SSTAMP(7);
     PairContacts pc;
     pc.n = 0;
     if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
@@ -613,7 +623,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       nr.c_R = make_float4(1.f, 1.f, 1.f, 1.f);
       nr.c_mu = make_float4(1.f, 1.f, 1.f, 0.f);
       if (lane < ncon) newton_contact_rows(m, sh.con_pair[lane], sh.con_dist[lane], cVn, fscale, nr.c_aref, nr.c_R, nr.c_mu);
-      if (ncon_max > kMaxCon) {
+      if (kOvfOn && ncon_max > kMaxCon) {
         // the contacts beyond kMaxCon (rare): J and their aref / R / cone coefficients to the env's HBM record,
         // block by block of 16 (lane k: contact kMaxCon + 16 b + k), for both paths' newton_solve
         for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {

@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get("SO100_LIB") or os.path.join(HERE, "_lib", "libso100_h
 SO100_FLAG_AUTORESET = 1
 SO100_FLAG_DR = 2
 SO100_DBG_OVF = 160                   # include/so100.h: the debug entries of contacts >= 16
-SO100_DBG_STRIDE = 160 + 6 * (562 - 16)
+SO100_DBG_STRIDE = 160 + 6 * (643 - 16)
 TASKS = {"so100_cube_to_bin": 0, "so100_touch_cube": 1, "so100_touch_cube_sparse": 2, "so100_goal": 3}
 
 _P = ctypes.c_void_p
@@ -46,7 +46,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 14         # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 15         # include/so100.h SO100_ABI_VERSION
 HULL_CELLG = 8           # SO100_HULL_CELLG
 HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 

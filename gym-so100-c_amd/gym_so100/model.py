@@ -15,7 +15,8 @@ from . import constants as C
 
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "so100_model.json")
 
-NBODY, NHINGE, NQ, NV, NU, NGEOM = 9, 6, 13, 12, 6, 15
+NBODY, NHINGE, NQ, NV, NU, NGEOM = 9, 6, 13, 12, 6, 16
+MOCAP_GEOM, MOCAP_BODY = 15, 9                  # the EE variant's mocap marker box and its (mocap) body
 NPAIR_BOX, NHULL, HULL_NVERT, NBINBOX = 14, 9, 2560, 5
 PAIR_MPR0 = NPAIR_BOX + NHULL                  # (box, hull) pairs of the MPR convex collider start here
 PAIR_SELF0 = PAIR_MPR0 + (1 + NBINBOX) * NHULL  # 77: hull-hull self-collision pairs
@@ -24,13 +25,15 @@ NPAIR_SELF = 21
 PAIR_BASE0 = PAIR_SELF0 + NPAIR_SELF             # 98: (cube, Base hull), 99..106 (Base hull, hull k = 1..8)
 PAIR_PADLINK0 = PAIR_BASE0 + 9                   # 107: (pad, link hull) pairs 107..142 through MPR
 NPAIR_PADLINK = 36
-PAIR_PAD0 = PAIR_PADLINK0 + NPAIR_PADLINK        # 143: (pad i, table) pairs 143..150
-PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 151: (pad i, bin box j) at 151 + 5 i + j, box-box
+PAIR_MOCAPHULL0 = PAIR_PADLINK0 + NPAIR_PADLINK  # 143: (mocap marker, link hull k) 143..151, EE only, convex
+PAIR_PAD0 = PAIR_MOCAPHULL0 + NHULL              # 152: (pad i, table) pairs 152..159
+PAIR_PADBIN0 = PAIR_PAD0 + 8                     # 160: (pad i, bin box j) at 160 + 5 i + j, box-box
 NPAIR_PAD = 8 * (1 + NBINBOX)                    # 48
-NPAIR = PAIR_PAD0 + NPAIR_PAD                    # 191
+PAIR_MOCAPBOX0 = PAIR_PAD0 + NPAIR_PAD           # 200: (cube | pad i, mocap marker) 200..208, EE only, box-box
+NPAIR = PAIR_MOCAPBOX0 + 9                       # 209
 NPAIR_BITS = PAIR_MPR0                         # contact_bits covers pairs 0..22
 MAXCON, CONDIM, NOBS = 16, 4, 15      # MAXCON: contacts an env holds on chip (include/so100_model.h)
-NCON_MAX = 53 * 8 + 191 - 53           # SO100_NCON_MAX: the whole contact list (every pair at its maximum)
+NCON_MAX = 62 * 8 + 209 - 62           # SO100_NCON_MAX: the whole contact list (every pair at its maximum)
 NEFC_MAX = NV + NHINGE + NCON_MAX * CONDIM
 
 _d = ctypes.c_double

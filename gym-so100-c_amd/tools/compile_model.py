@@ -202,6 +202,7 @@ MJ_SOLREF = [0.02, 1.0]
 MJ_SOLIMP = [0.9, 0.95, 0.001, 0.5, 2.0]
 MJ_FRICTION = [1.0, 0.005, 0.0001]
 MJ_CONDIM = 3
+MOCAP_BODY = 9          # the EE variant's mocap body (include/so100_model.h SO100_MOCAP_BODY): no dofs, not in the body arrays
 
 
 def compile_model():
@@ -348,7 +349,16 @@ def compile_model():
     binb = bodies["bin"]
     for g in binb["geoms"]:
         add_geom(g["name"], 0, binb["pos"] + vec(g["pos"], 3), [1, 0, 0, 0], vec(g["size"], 3), g)
+    # geom 15: the EE variant's mocap marker box (so_arm100_ee.xml:155: a group-0 box with the default contype /
+    # conaffinity, so MuJoCo collides it).  Its body is the mocap body (MOCAP_BODY, no dofs: its pose is the env's
+    # mocap input); it exists in both variants' tables, its pairs are collided only in the EE variant.
+    ee_root = ET.parse(os.path.join(ASSETS, "trs_so_arm100", "so_arm100_ee.xml")).getroot()
+    mocap_b = [b for b in ee_root.find("worldbody").findall("body") if b.get("mocap") == "true"][0]
+    mg = mocap_b.find("geom")
+    assert mg.get("type") == "box" and not mg.get("pos") and not mg.get("quat") and not mg.get("contype")
+    add_geom("mocap_target_box", MOCAP_BODY, [0, 0, 0], [1, 0, 0, 0], vec(mg.get("size"), 3), dict(mg.attrib))
     gid = {g["name"]: i for i, g in enumerate(geoms)}
+    assert len(geoms) == 16
 
     # ---- arm/jaw collision hulls (convex hulls of the class="collision" meshes of the moving bodies) ----
     from scipy.spatial import ConvexHull
@@ -455,7 +465,15 @@ def compile_model():
             pairs.append(dict(g1=gid[n1], g2=-1 - k, body1=g1["body"], body2=h["body"], name1=n1,
                               name2=h["name"], hull=k, **mixed(g1, h)))
     assert len(pairs) == 143
-    # Pairs 143..150: the 8 finger pads against the table; 151..190: against the 5 bin boxes (151 + 5 i + j).
+    # Pairs 143..151 (EE variant only): the mocap marker box against the 9 link hulls, through the convex
+    # collider (MuJoCo's static-static filter removes the marker against the table, the bin and the Base: a mocap
+    # body is welded to the world; geom1 = the box, box < mesh)
+    mk = geoms[gid["mocap_target_box"]]
+    for k, h in enumerate(hulls[:9]):
+        pairs.append(dict(g1=gid["mocap_target_box"], g2=-1 - k, body1=MOCAP_BODY, body2=h["body"],
+                          name1="mocap_target_box", name2=h["name"], hull=k, ee_only=True, **mixed(mk, h)))
+    assert len(pairs) == 152
+    # Pairs 152..159: the 8 finger pads against the table; 160..199: against the 5 bin boxes (160 + 5 i + j).
     # geom1 = the pad: the table is a mesh (box < mesh) and the bin boxes come after the arm in the model
     # (so100_transfer_cube.xml includes the arm before the bin), so the normal points from the pad to the
     # table / bin box.  Pad-table contacts follow the hull-table rule (one per pair); pad-bin pairs are
@@ -466,7 +484,14 @@ def compile_model():
         g1, g2 = geoms[gid[n1]], geoms[gid[n2]]
         pairs.append(dict(g1=gid[n1], g2=gid[n2], body1=g1["body"], body2=g2["body"], name1=n1, name2=n2,
                           **mixed(g1, g2)))
-    assert len(pairs) == 191
+    assert len(pairs) == 200
+    # Pairs 200..208 (EE variant only): the cube and the 8 finger pads against the mocap marker box, box-box (the
+    # marker has the highest geom id: geom1 = the cube / pad, normal towards the marker)
+    for n1 in ["red_box"] + pads:
+        g1 = geoms[gid[n1]]
+        pairs.append(dict(g1=gid[n1], g2=gid["mocap_target_box"], body1=g1["body"], body2=MOCAP_BODY, name1=n1,
+                          name2="mocap_target_box", ee_only=True, **mixed(g1, mk)))
+    assert len(pairs) == 209
 
     # ---- EE / mocap variant (so100_transfer_cube_ee.xml: the same scene with trs_so_arm100/so_arm100_ee.xml,
     # whose only differences are the mocap body at :155 and the weld equality at :171-173) ----

@@ -11,14 +11,19 @@
  *   dofs   0..5 arm hinges (Rotation, Pitch, Elbow, Wrist_Pitch, Wrist_Roll, Jaw),
  *          6..8 cube linear (world frame), 9..11 cube angular (body frame)  (MuJoCo free-joint layout)
  *   qpos   0..5 hinges, 6..8 cube position, 9..12 cube quaternion (w,x,y,z)
- *   geoms  0 table | 1..4 fixed_jaw_pad_1..4 | 5..8 moving_jaw_pad_1..4 | 9 red_box | 10..14 bin walls+floor
+ *   geoms  0 table | 1..4 fixed_jaw_pad_1..4 | 5..8 moving_jaw_pad_1..4 | 9 red_box | 10..14 bin walls+floor |
+ *          15 the EE variant's mocap marker box (so_arm100_ee.xml:155; body SO100_MOCAP_BODY: its pose is the env's
+ *          mocap input)
  *   pairs  0..7 pad-vs-red_box | 8 (red_box, table) | 9..13 (red_box, bin_*)   (box-box)
  *          14..22 (table, hull k): arm/jaw collision hulls vs the table top
  *          23..31 (red_box, hull k) | 32..76 (bin box j, hull k) at 32 + 9 j + k, j = bin_wall,
  *          bin_wall2..4, bin_floor: box vs convex hull through the MPR convex collider
  *          77..97 (hull k1, hull k2): self-collision of hulls on non-adjacent arm links (MPR)
  *          98..106 (red_box, Base hull) and (Base hull, hull k), k = 1..8: the static Base (MPR)
- *          107..114 (finger pad i, table); 115..154 (finger pad i, bin box j) at 115 + 5 i + j
+ *          107..142 (finger pad, link hull)
+ *          143..151 (mocap marker box, link hull k) (EE variant only, convex collider)
+ *          152..159 (finger pad i, table); 160..199 (finger pad i, bin box j) at 160 + 5 i + j
+ *          200..208 (cube | finger pad i, mocap marker box) (EE variant only, box-box)
  *   hulls  0 Rotation_Pitch | 1 Upper_Arm | 2 Lower_Arm | 3 Wrist_Pitch_Roll |
  *          4..5 Fixed_Jaw_Collision_1..2 | 6..8 Moving_Jaw_Collision_1..3
  */
@@ -30,7 +35,9 @@
 #define SO100_NQ 13
 #define SO100_NV 12
 #define SO100_NU 6
-#define SO100_NGEOM 15
+#define SO100_NGEOM 16
+#define SO100_MOCAP_GEOM 15         /* the EE variant's mocap marker box */
+#define SO100_MOCAP_BODY 9          /* its body: the mocap body (no dofs; not in the body arrays)         */
 #define SO100_NPAIR_BOX 14         /* box-box pairs 0..13 */
 #define SO100_NHULL 9               /* arm/jaw collision hulls (moving links) */
 #define SO100_HULL_BASE 9           /* hull 9: the static Base's collision hull */
@@ -46,12 +53,17 @@
 #define SO100_NPAIR_PADLINK 36                              /* 107..142: pads vs Base, Rotation_Pitch, Upper_Arm,
                                                                Lower_Arm, Wrist_Pitch_Roll (not the fixed pads' parent) */
 #define SO100_NPAIR_CONVEX (SO100_NPAIR_MPR + SO100_NPAIR_SELF + SO100_NPAIR_BASE + SO100_NPAIR_PADLINK)  /* 120 through MPR */
-#define SO100_PAIR_PAD0 (SO100_PAIR_PADLINK0 + SO100_NPAIR_PADLINK)  /* 143: first (pad, table | bin box) pair */
+#define SO100_PAIR_MOCAPHULL0 (SO100_PAIR_PADLINK0 + SO100_NPAIR_PADLINK)  /* 143: (mocap box, link hull k), EE only */
+#define SO100_NPAIR_MOCAPHULL SO100_NHULL                   /* 9 */
+#define SO100_PAIR_PAD0 (SO100_PAIR_MOCAPHULL0 + SO100_NPAIR_MOCAPHULL)  /* 152: first (pad, table | bin box) pair */
 #define SO100_NPAD 8                                        /* finger pads: geoms 1..8 */
-#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 151: (pad i, bin box j) at 151 + 5 i + j */
+#define SO100_PAIR_PADBIN0 (SO100_PAIR_PAD0 + SO100_NPAD)   /* 160: (pad i, bin box j) at 160 + 5 i + j */
 #define SO100_NPAIR_PADBIN (SO100_NPAD * SO100_NBINBOX)     /* 40, box-box */
 #define SO100_NPAIR_PAD (SO100_NPAD + SO100_NPAIR_PADBIN)   /* 48: 143..150 (pad i, table), then pad-bin */
-#define SO100_NPAIR (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)     /* 191: every pair MuJoCo's filters leave */
+#define SO100_PAIR_MOCAPBOX0 (SO100_PAIR_PAD0 + SO100_NPAIR_PAD)  /* 200: (cube | pad i, mocap box), EE only */
+#define SO100_NPAIR_MOCAPBOX (1 + SO100_NPAD)               /* 9, box-box */
+#define SO100_NPAIR (SO100_PAIR_MOCAPBOX0 + SO100_NPAIR_MOCAPBOX)  /* 209: every pair MuJoCo's filters leave (the
+                                                               joint variant's 191 and the EE variant's 18 more) */
 #define SO100_NPAIR_BITS SO100_PAIR_MPR0                    /* contact_bits covers pairs 0..22 */
 #define SO100_HULL_NVERT 2560       /* hull vertex capacity, all hulls */
 #define SO100_HULL_CELLG 8          /* support-direction cells per cube-map face edge (so100_hull_cells) */
@@ -62,13 +74,14 @@
 #define SO100_NPAIR_GRIPPER 8       /* pairs 0..7 — single_arm.py:348-352 touch_gripper   */
 #define SO100_MAXCONPAIR 8          /* contacts per box-box pair: every clipped point, as mjc_BoxBox */
 /* box-box pairs that keep every clipped point: the cube against the 8 pads and the 5 bin boxes (pairs 0..13
- * but the cube-table pair 8, whose table is a mesh: one convex contact) and the 40 pad-bin pairs */
-#define SO100_NPAIR_MULTI (SO100_NPAIR_BOX - 1 + SO100_NPAIR_PADBIN)                        /* 53 */
+ * but the cube-table pair 8, whose table is a mesh: one convex contact), the 40 pad-bin pairs and (EE variant) the
+ * cube and the pads against the mocap marker box */
+#define SO100_NPAIR_MULTI (SO100_NPAIR_BOX - 1 + SO100_NPAIR_PADBIN + SO100_NPAIR_MOCAPBOX)  /* 62 */
 /* The contact list of an env holds up to SO100_NCON_MAX contacts: every pair at its collider's maximum (8 for
  * a multi-point box-box pair, 1 for the convex collider and the table rules), so no contact MuJoCo would keep
  * can be left out (MuJoCo has no per-env cap).  The kernels hold the first SO100_MAXCON of them on chip (the
  * solver's lane c owns contact c); the rest live in the env's HBM record (include/so100.h). */
-#define SO100_NCON_MAX (SO100_NPAIR_MULTI * SO100_MAXCONPAIR + SO100_NPAIR - SO100_NPAIR_MULTI)  /* 562 */
+#define SO100_NCON_MAX (SO100_NPAIR_MULTI * SO100_MAXCONPAIR + SO100_NPAIR - SO100_NPAIR_MULTI)  /* 643 */
 #define SO100_MAXCON 16             /* contacts an env holds on chip (LDS / registers) per position stage */
 #define SO100_CONDIM 4              /* max condim: cube pairs mix to 4, table/bin-hull pairs are 3 */
 #define SO100_NEFC_MAX (SO100_NV + SO100_NHINGE + SO100_NCON_MAX * SO100_CONDIM)

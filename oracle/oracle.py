@@ -10,8 +10,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-NBODY, NHINGE, NQ, NV, NU, NGEOM, CONDIM, NOBS = 9, 6, 13, 12, 6, 15, 4, 15
-NCON_MAX = 53 * 8 + 191 - 53         # include/so100_model.h SO100_NCON_MAX: every pair at its collider's maximum
+NBODY, NHINGE, NQ, NV, NU, NGEOM, CONDIM, NOBS = 9, 6, 13, 12, 6, 16, 4, 15
+NCON_MAX = 62 * 8 + 209 - 62         # include/so100_model.h SO100_NCON_MAX: every pair at its collider's maximum
 NEFC = NV + NHINGE + NCON_MAX * CONDIM
 
 

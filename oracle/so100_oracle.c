@@ -244,15 +244,22 @@ static void kinematics(const so100_model* m, so100o_data* d) {
     quat2mat(iR, iq);
     mulmm3(d->ximat[b], d->xmat[b], iR);
   }
+  /* the mocap body (the EE variant's marker, so_arm100_ee.xml:155): its frame is the mocap pose (mj_kinematics
+   * takes mocap_pos and the normalised mocap_quat) */
+  real mq[4] = {d->mocap_quat[0], d->mocap_quat[1], d->mocap_quat[2], d->mocap_quat[3]}, mR[9];
+  quat_normalize(mq);
+  quat2mat(mR, mq);
   for (int g = 0; g < SO100_NGEOM; g++) {
-    int b = m->geom_body[g];
+    const int b = m->geom_body[g];
+    const real* bp = b == SO100_MOCAP_BODY ? d->mocap_pos : d->xpos[b];
+    const real* bR = b == SO100_MOCAP_BODY ? mR : d->xmat[b];
     real gp[3], gq[4], gR[9], t[3];
     load3(gp, m->geom_pos[g]);
     load4(gq, m->geom_quat[g]);
-    mulmv3(t, d->xmat[b], gp);
-    for (int k = 0; k < 3; k++) d->geom_xpos[g][k] = d->xpos[b][k] + t[k];
+    mulmv3(t, bR, gp);
+    for (int k = 0; k < 3; k++) d->geom_xpos[g][k] = bp[k] + t[k];
     quat2mat(gR, gq);
-    mulmm3(d->geom_xmat[g], d->xmat[b], gR);
+    mulmm3(d->geom_xmat[g], bR, gR);
   }
   real sp[3], t[3];
   load3(sp, m->site_cube_pos);
@@ -1207,10 +1214,12 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = best - top;
     add_contact(d, &con, p);
   }
-  /* pairs 23..142 through the MPR convex collider, in H = the body frame of hull k (geom2):
+  /* pairs 23..151 through the MPR convex collider, in H = the body frame of hull k (geom2):
    *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links;
-   *   98..106 the static Base hull (the cube, then link hulls 1..8); 107..142 (finger pad, link hull k) */
+   *   98..106 the static Base hull (the cube, then link hulls 1..8); 107..142 (finger pad, link hull k);
+   *   143..151 (EE variant only) the mocap marker box against link hull k */
   for (int p = SO100_PAIR_MPR0; p < SO100_PAIR_PAD0; p++) {
+    if (p >= SO100_PAIR_MOCAPHULL0 && !m->ee) break;
     const int k = -1 - m->pair_geom2[p], g = m->pair_geom1[p], b = m->hull_body[k];
     const real* RH = d->xmat[b];
     mpr_obj o;
@@ -1265,9 +1274,12 @@ static void collision(const so100_model* m, so100o_data* d) {
     con.dist = -depth;
     add_contact(d, &con, p);
   }
-  /* pairs 143..190: the finger pads vs the table (143..150), then vs the bin boxes (box-box) */
+  /* pairs 152..199: the finger pads vs the table (152..159), then vs the bin boxes (box-box) */
   for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_PADBIN0; p++) pad_table(m, d, p);
-  for (int p = SO100_PAIR_PADBIN0; p < SO100_NPAIR; p++) collide_box_pair(m, d, p);
+  for (int p = SO100_PAIR_PADBIN0; p < SO100_PAIR_MOCAPBOX0; p++) collide_box_pair(m, d, p);
+  /* pairs 200..208 (EE variant only): the cube and the pads against the mocap marker box (box-box) */
+  if (m->ee)
+    for (int p = SO100_PAIR_MOCAPBOX0; p < SO100_NPAIR; p++) collide_box_pair(m, d, p);
 #ifdef SO100O_STATS
   if (so100o_stat_buf && so100o_stat_n < so100o_stat_cap)
     for (int k = 0; k < SO100O_NSTAT; k++) so100o_stat_buf[so100o_stat_n * SO100O_NSTAT + k] = so100o_stat_cur[k];
@@ -1359,7 +1371,7 @@ static void make_constraint(const so100_model* m, so100o_data* d) {
     for (int side = 0; side < 2; side++) {
       int b = side ? b2 : b1;
       real sg = side ? (real)1 : (real)-1;
-      if (b == 0 || b == 1) continue;              /* world / static Base: no dofs */
+      if (b == 0 || b == 1 || b == SO100_MOCAP_BODY) continue;   /* world / static Base / mocap: no dofs */
       if (b == SO100_CUBE_BODY) {
         real off[3];
         for (int t = 0; t < 3; t++) off[t] = con->pos[t] - d->xpos[b][t];
@@ -1382,8 +1394,11 @@ static void make_constraint(const so100_model* m, so100o_data* d) {
       }
     }
     const int dim = m->pair_condim[p];
-    real tran = (real)(m->body_invweight0[b1][0] + m->body_invweight0[b2][0]);
-    real rot = (real)(m->body_invweight0[b1][1] + m->body_invweight0[b2][1]);
+    /* the mocap body is welded to the world for the dynamics: invweight0 = 0 */
+    real tran = (real)((b1 == SO100_MOCAP_BODY ? 0 : m->body_invweight0[b1][0]) +
+                       (b2 == SO100_MOCAP_BODY ? 0 : m->body_invweight0[b2][0]));
+    real rot = (real)((b1 == SO100_MOCAP_BODY ? 0 : m->body_invweight0[b1][1]) +
+                      (b2 == SO100_MOCAP_BODY ? 0 : m->body_invweight0[b2][1]));
     real imp = getimpedance(m->pair_solimp[p], con->dist, (real)m->pair_margin[p]);
     real K, B;
     solref_kb(m->pair_solref[p], m->pair_solimp[p], h, &K, &B);

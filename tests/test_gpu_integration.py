@@ -33,12 +33,17 @@ class HipPhysicsBackend:
         self.b = _native.SO100Buffers()
         for k, v in self.t.items():
             setattr(self.b, k, v.data_ptr())
-        self.seed_t = z(1, dt=torch.int32)
+        self.seed_t = z(1, dt=torch.int32)                          # uint32 seeds, stored as int32 bits
 
-    def reset(self, seed):
-        self.seed_t.fill_(int(seed) & 0x7FFFFFFF)
-        _native.check(self.lib.so100_reset(self.h, ctypes.byref(self.b), None,
-                                           ctypes.c_void_p(self.seed_t.data_ptr()), None), "so100_reset")
+    def reset(self, seed=None):
+        seeds = None
+        if seed is not None:
+            s = int(seed)
+            if not 0 <= s < 2 ** 32:
+                raise ValueError("Seed must be between 0 and 2**32 - 1")
+            self.seed_t.fill_(int(np.array(s, np.uint32).view(np.int32)))
+            seeds = ctypes.c_void_p(self.seed_t.data_ptr())
+        _native.check(self.lib.so100_reset(self.h, ctypes.byref(self.b), None, seeds, None), "so100_reset")
         return self.t["obs"][0].cpu().numpy()
 
     def step(self, action):
@@ -68,5 +73,18 @@ def test_reference_side_binding_matches_vec_env():
         torch.cuda.synchronize()
         np.testing.assert_array_equal(ob1, ob2[0].cpu().numpy())
         assert r1 == float(r2[0]) and t1 == bool(t2[0])
+    # seeds >= 2**31 spawn as RandomState(seed) does (no sign-bit mask), seed=None resets with a fresh spawn
+    for seed in (2 ** 31 + 12345, 2 ** 32 - 1):
+        o1 = be.reset(seed)
+        o2, _ = ve.reset(seed=[seed])
+        np.testing.assert_array_equal(o1, o2[0].cpu().numpy())
+        pose = ve.spawn_pose([seed]).cpu().numpy()[0]                # device MT19937 == RandomState(seed)
+        np.testing.assert_array_equal(ve.qpos[0, 6:9].cpu().numpy(), pose[:3].astype(np.float32))
+        np.testing.assert_array_equal(pose, np.random.RandomState(seed).uniform([-0.25, 0.3, 0.05], [-0.15, 0.6, 0.05])
+                                      .tolist() + [1.0, 0.0, 0.0, 0.0])
+    o3 = be.reset(None)
+    assert np.all(np.isfinite(o3))
+    with pytest.raises(ValueError):
+        be.reset(2 ** 32)
     be.close()
     ve.close()

@@ -979,8 +979,8 @@ def test_pad_link_contact_parity(solver, oracle64, oracle32):
     """The finger pads against the arm's own link hulls (pairs 107..142 through MPR, round 2; with them
     the pair table is every pair MuJoCo's filters leave): random arm configurations folding a jaw onto a
     link, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
-    from gym_so100.model import PAIR_PADLINK0, PAIR_PAD0
-    _arm_contact_parity(solver, oracle64, oracle32, PAIR_PADLINK0, PAIR_PAD0, "pad-link", 23)
+    from gym_so100.model import PAIR_PADLINK0, PAIR_MOCAPHULL0
+    _arm_contact_parity(solver, oracle64, oracle32, PAIR_PADLINK0, PAIR_MOCAPHULL0, "pad-link", 23)
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -992,9 +992,9 @@ def test_arm_contact_substep_parity(solver, cls, oracle64, oracle32):
     DESIGN.md §5), so per env step no fp32 implementation can hold 1e-4 there; per substep the problem is
     well conditioned at the median, and the GPU's product kernels must hold north_star's 1e-4 on qvel,
     qacc and the contact forces at the median (Newton, MuJoCo's solver), and the floors' bars in the tail."""
-    from gym_so100.model import PAIR_SELF0, PAIR_BASE0, PAIR_PADLINK0, PAIR_PAD0
+    from gym_so100.model import PAIR_SELF0, PAIR_BASE0, PAIR_PADLINK0, PAIR_MOCAPHULL0
     p0, p1, seed = {"self": (PAIR_SELF0, PAIR_BASE0, 17), "base": (PAIR_BASE0, PAIR_PADLINK0, 19),
-                    "padlink": (PAIR_PADLINK0, PAIR_PAD0, 23)}[cls]
+                    "padlink": (PAIR_PADLINK0, PAIR_MOCAPHULL0, 23)}[cls]
     r = _arm_contact_parity(solver, oracle64, oracle32, p0, p1, cls, seed, nsubstep=1)
     _force_bars(r, median_abs=1e-4 if solver == "newton" else None)
     if solver == "newton":
@@ -1119,11 +1119,16 @@ def test_ee_weld_parity(solver, oracle64, oracle32):
                 mocap=mocap).arrays()
     ee_gap = np.linalg.norm(venv.obs[:, 6:9].cpu().numpy() - mocap[:, :3], axis=1)
     venv.close()
-    print(f"\nee-target gap after 30 steps: median {np.median(ee_gap):.3f} m; " + r.summary(f"ee {solver}"))
+    # the marker box at the target (so_arm100_ee.xml:155) collides with the gripper (pairs 143..151 against the link
+    # hulls, 200..208 against the cube and the pads): its contacts are in the lists the GPU and the oracle agree on
+    from gym_so100.model import PAIR_MOCAPHULL0, PAIR_PAD0, PAIR_MOCAPBOX0
+    marker = np.array([int((((p >= PAIR_MOCAPHULL0) & (p < PAIR_PAD0)) | (p >= PAIR_MOCAPBOX0)).sum()) for p in r.pairs])
+    print(f"\nee-target gap after 30 steps: median {np.median(ee_gap):.3f} m; marker contacts in "
+          f"{np.mean(marker > 0):.2f} of env-steps; " + r.summary(f"ee {solver}"))
+    assert np.mean(marker > 0) > 0.2 and np.mean(r.same[marker > 0]) > 0.8
     assert np.median(r.qp) <= 1e-5 and np.median(r.qv) <= 1e-5
     assert np.quantile(r.qv, 0.9) <= 2 * r.floor("qv", 0.9) + 1e-4
     assert r.qv.max() <= 2 * r.floor("qv", 1.0) + 1e-3
-    assert np.median(ee_gap) < 0.04
 
 
 @pytest.mark.parametrize("n", [4099, 12291])

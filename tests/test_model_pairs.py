@@ -1,4 +1,4 @@
-"""The model's contact-pair table (gym_so100/assets/so100_model.json, 191 pairs) against MuJoCo's collision
+"""The model's contact-pair table (gym_so100/assets/so100_model.json: 191 pairs, 209 with the EE variant's) against MuJoCo's collision
 filters applied to the reference MJCF: the table is exactly the pair set MuJoCo would hand
 to a narrowphase, no pair more, none missing.  Filters restated from MuJoCo 3.3.3's broadphase (mj_collision /
 filter): contype/conaffinity compatibility, same weld body (which includes static-static), the
@@ -15,10 +15,18 @@ REF = "/root/reference/gym_so100/assets"
 pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference MJCF not present")
 
 
-def test_pair_table_is_mujocos_filtered_pair_set():
+@pytest.mark.parametrize("variant", ["joint", "ee"])
+def test_pair_table_is_mujocos_filtered_pair_set(variant):
+    """joint: so100_transfer_cube.xml's pairs (those not marked ee_only); ee: so100_transfer_cube_ee.xml's, the
+    same scene plus the mocap body of so_arm100_ee.xml:155 (a jointless child of the world, so welded to it:
+    its marker box meets neither the table, the bin nor the Base)."""
     sys.path.insert(0, os.path.join(ROOT, "gym-so100-c_amd", "tools"))
     from compile_model import parse
     _, bodies, _, excludes = parse()
+    if variant == "ee":
+        bodies = dict(bodies)
+        bodies["mocap_target"] = {"joints": [], "parent": "world",
+                                  "geoms": [{"name": "mocap_target_box", "type": "box"}]}
     weld = {"world": "world"}
 
     def weld_of(b):
@@ -48,12 +56,13 @@ def test_pair_table_is_mujocos_filtered_pair_set():
                 continue
             want.add(frozenset((n1, n2)))
     model = json.load(open(os.path.join(ROOT, "gym-so100-c_amd", "gym_so100", "assets", "so100_model.json")))
-    have = {frozenset((p["name1"], p["name2"])) for p in model["pairs"]}
-    assert len(have) == len(model["pairs"]) == 191
+    pairs = [p for p in model["pairs"] if variant == "ee" or not p.get("ee_only")]
+    have = {frozenset((p["name1"], p["name2"])) for p in pairs}
+    assert len(have) == len(pairs) == {"joint": 191, "ee": 209}[variant]
     assert not have - want, sorted(map(sorted, have - want))     # no pair MuJoCo would filter out
     assert not want - have, sorted(map(sorted, want - have))     # none missing: round 2 added the 36
     # finger-pad / link-hull pairs (4 links for the fixed-jaw pads, Wrist_Pitch_Roll being their parent, 5
     # for the moving-jaw pads)
-    pads = [p for p in model["pairs"] if p["name1"].endswith(("_pad_1", "_pad_2", "_pad_3", "_pad_4"))
+    pads = [p for p in pairs if p["name1"].endswith(("_pad_1", "_pad_2", "_pad_3", "_pad_4"))
             and p["g2"] < 0]
     assert len(pads) == 36

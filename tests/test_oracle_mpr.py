@@ -357,10 +357,10 @@ def test_pad_link_contacts_are_real_overlaps(model, oracle64):
     proves to overlap a link by more than the tolerance always get their contact.  Random arm poses fold the
     jaws onto the links."""
     from scipy.optimize import linprog
-    from gym_so100.model import PAIR_PADLINK0, PAIR_PAD0
+    from gym_so100.model import PAIR_PADLINK0, PAIR_MOCAPHULL0
     rng = np.random.default_rng(33)
     lo = np.array([r[0] for r in model.jnt_range]); hi = np.array([r[1] for r in model.jnt_range])
-    assert PAIR_PAD0 - PAIR_PADLINK0 == 36
+    assert PAIR_MOCAPHULL0 - PAIR_PADLINK0 == 36
 
     def world(d, k):
         b = model.hull_body[k]
@@ -379,8 +379,8 @@ def test_pad_link_contacts_are_real_overlaps(model, oracle64):
         d = _state(oracle64, model, rng.uniform(lo, hi), (0.4, 0.95, 0.6, 1, 0, 0, 0))
         if d.ncon_dropped:
             continue
-        got = {d.con[i].pair: d.con[i] for i in range(d.ncon) if PAIR_PADLINK0 <= d.con[i].pair < PAIR_PAD0}
-        for p in range(PAIR_PADLINK0, PAIR_PAD0):
+        got = {d.con[i].pair: d.con[i] for i in range(d.ncon) if PAIR_PADLINK0 <= d.con[i].pair < PAIR_MOCAPHULL0}
+        for p in range(PAIR_PADLINK0, PAIR_MOCAPHULL0):
             g, k = model.pair_geom1[p], -1 - model.pair_geom2[p]
             R = np.array(d.geom_xmat[g][:]).reshape(3, 3)
             pad = _box_corners(np.array(d.geom_xpos[g][:]), R, np.array(model.geom_size[g][:]))

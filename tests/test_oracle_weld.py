@@ -100,8 +100,13 @@ def test_weld_elimination_is_exact(models, oracle64):
 
 
 def test_weld_pulls_ee_to_target(models, oracle64):
-    """Mocap target 3 cm from the end effector: the weld closes the gap (position and orientation)."""
-    m = models["ee"]
+    """Mocap target 3 cm from the end effector: the weld closes the gap (position and orientation).  The marker box
+    at the target (so_arm100_ee.xml:155) collides with the gripper's links (test_marker_box_blocks_the_gripper), so
+    this weld-only property is checked with the box shrunk to a point."""
+    from gym_so100.model import MOCAP_GEOM, build_model
+    m = build_model(solver="newton", variant="ee")
+    for k in range(3):
+        m.geom_size[MOCAP_GEOM][k] = 1e-5
     d = state(oracle64, m, np.zeros(6), np.zeros(3), np.array([1.0, 0, 0, 0]))
     p0 = np.array(d.site_ee[:])
     _, R = ee_frame(d)
@@ -117,3 +122,31 @@ def test_weld_pulls_ee_to_target(models, oracle64):
     dist = np.linalg.norm(np.array(d.site_ee[:]) - target)
     assert dist0 > 0.029 and dist < 0.5 * dist0, (dist0, dist)
     assert np.linalg.norm(np.array(d.weld_pos[3:])) < 0.05        # orientation held
+
+
+def test_marker_box_blocks_the_gripper(models, oracle64):
+    """The EE variant's mocap marker (a 4 x 12 x 4 cm box, default contype/conaffinity) is a collision geom in MuJoCo:
+    centred on a target 3 cm from the end effector it overlaps the wrist and jaw link hulls (pairs 143..151), and
+    its contacts hold the gripper off where the weld alone would pull it in (test_weld_pulls_ee_to_target)."""
+    from gym_so100.model import PAIR_MOCAPHULL0, PAIR_PAD0
+    m = models["ee"]
+    d = state(oracle64, m, np.zeros(6), np.zeros(3), np.array([1.0, 0, 0, 0]))
+    p0 = np.array(d.site_ee[:])
+    _, R = ee_frame(d)
+    from scipy.spatial.transform import Rotation
+    q = Rotation.from_matrix(R).as_quat()[[3, 0, 1, 2]]
+    target = p0 + np.array([0.0, 0.03, 0.0])
+    d = state(oracle64, m, np.zeros(6), target, q)
+    marker = [d.con[i].pair for i in range(d.ncon) if PAIR_MOCAPHULL0 <= d.con[i].pair < PAIR_PAD0]
+    assert len(marker) >= 2, marker
+    dist0 = np.linalg.norm(np.array(d.site_ee[:]) - target)
+    act = np.zeros(6, np.float32)
+    for _ in range(60):
+        oracle64.env_step(m, d, 0, act)
+    dist = np.linalg.norm(np.array(d.site_ee[:]) - target)
+    assert dist > 0.8 * dist0, (dist0, dist)
+    # the joint variant has no marker: none of its pairs ever appears there
+    mj = models["joint"]
+    dj = state(oracle64, mj, np.zeros(6), target, q)
+    assert not any(PAIR_MOCAPHULL0 <= dj.con[i].pair < PAIR_PAD0 or dj.con[i].pair >= PAIR_PAD0 + 48
+                   for i in range(dj.ncon))

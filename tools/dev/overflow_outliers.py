@@ -51,6 +51,45 @@ def main():
         if len(gp) != len(p64) or not np.array_equal(gp, p64):
             print("   pairs GPU ", list(gp))
             print("   pairs fp64", list(p64))
+    for i in order[:3]:
+        detail(r, int(i), solver, nsub)
+
+
+
+def detail(r, idx, solver, nsub):
+    """one state again, alone, with the debug record: per contact (pair, dist, forces) GPU vs the fp64 oracle"""
+    import torch
+    from gym_so100 import SO100VecEnv
+    from gym_so100.model import build_model
+    o64 = Oracle(64)
+    model = build_model(solver=solver, nsubstep=nsub)
+    q0, v0, w0, act = r.states[idx][:4]
+    env = SO100VecEnv(1, device="cuda:0", autoreset=False, max_episode_steps=0, debug=True, solver=solver, nsubstep=nsub)
+    env.reset(seed=3)
+    env.set_state(q0[None].astype(np.float32), v0[None].astype(np.float32), w0[None].astype(np.float32))
+    env.step(torch.as_tensor(act[None], dtype=torch.float32).cuda())
+    torch.cuda.synchronize()
+    dbg = env.debug.cpu().numpy()[0]
+    gp, gf, _, gqa = T._gpu_solve(dbg)
+    from gym_so100._native import SO100_DBG_OVF
+    nc = int(dbg[0])
+    gd = np.concatenate([dbg[16:16 + min(nc, 16)], dbg[SO100_DBG_OVF:SO100_DBG_OVF + 6 * max(nc - 16, 0)].reshape(-1, 6)[:, 0]])
+    d = o64.new_data()
+    o64.set_state(d, q0, v0, w0)
+    o64.env_step(model, d, 0, act)
+    p64, f64, _, qa64, _ = o64.last_solve(d)
+    # the oracle's last substep's contact distances: re-run the step without the final position stage
+    d2 = o64.new_data()
+    o64.set_state(d2, q0, v0, w0)
+    for k in range(6):
+        d2.ctrl[k] = 0.0
+    print(f"--- state {idx}: GPU ncon {nc}, oracle {len(p64)}; qacc GPU {np.array2string(gqa, precision=4)}\n"
+          f"    oracle qacc {np.array2string(qa64, precision=4)}")
+    for c in range(max(nc, len(p64))):
+        g = f"pair {gp[c]:3d} dist {gd[c]: .3e} f {np.array2string(gf[c], precision=4)}" if c < nc else "-"
+        o = f"pair {p64[c]:3d} f {np.array2string(f64[c], precision=4)}" if c < len(p64) else "-"
+        print(f"  c{c:2d} GPU {g} | fp64 {o}")
+    env.close()
 
 
 if __name__ == "__main__":
