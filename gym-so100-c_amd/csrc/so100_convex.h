@@ -1146,13 +1146,17 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     c0 += __popcll(mb & 0xFFFFull); c1 += __popcll(mb & (0xFFFFull << 16));
     c2 += __popcll(mb & (0xFFFFull << 32)); c3 += __popcll(mb & (0xFFFFull << 48));
   }
-  const int pre1 = c0, pre2 = c0 + c1, pre3 = c0 + c1 + c2;
-  const int total = pre3 + c3;
+  const int total = c0 + c1 + c2 + c3;
   if (total == 0) return 0;
+  // the list's env offsets (pre_1..3 <= 3 x 129) and the envs' staged counts (<= 129 each) packed into one word each:
+  // wave-uniform values held across the narrowphase's register peak (4 + 3 separate ones were spilled)
+  static_assert(3 * (kConvex + SO100_NPAIR_MOCAPHULL) < 1024 && kConvex + SO100_NPAIR_MOCAPHULL < 256, "packed counts");
+  const uint32_t prepk = (uint32_t)c0 | (uint32_t)(c0 + c1) << 10 | (uint32_t)(c0 + c1 + c2) << 20;
   __syncthreads();
-  int f0 = 0, f1 = 0, f2 = 0, f3 = 0;           // staged contacts per env (wave-uniform)
+  uint32_t fpk = 0u;                            // staged contacts of env e in byte e (wave-uniform)
   const int rounds = (total + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  auto env_of = [&](int item) { return item >= pre3 ? 3 : item >= pre2 ? 2 : item >= pre1 ? 1 : 0; };
+  auto pre_of = [&](int e) { return e == 0 ? 0 : (int)((prepk >> (10 * (e - 1))) & 1023u); };
+  auto env_of = [&](int item) { return item >= pre_of(3) ? 3 : item >= pre_of(2) ? 2 : item >= pre_of(1) ? 1 : 0; };
   for (int rd = 0; rd < rounds; rd++) {
     const int item = kEnvsPerBlock * rd + grp;
     const bool act = item < total;
@@ -1161,8 +1165,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     bool hit = false;
     int p = SO100_PAIR_MPR0;
     if (act) {
-      const int pre_ie = ie == 0 ? 0 : ie == 1 ? pre1 : ie == 2 ? pre2 : pre3;
-      p = SO100_PAIR_MPR0 + reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_ie];
+      p = SO100_PAIR_MPR0 + reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_of(ie)];
       MprObj o;
       mpr_obj_setup(m, shm[ie], p, o);
       o.cells = kCells;
@@ -1170,7 +1173,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
     const uint64_t hb = __ballot(hit);
-    int slot = ie == 0 ? f0 : ie == 1 ? f1 : ie == 2 ? f2 : f3;
+    int slot = (int)((fpk >> (8 * ie)) & 0xFFu);
 #pragma unroll
     for (int g = 0; g < kEnvsPerBlock; g++) {
       const int it = kEnvsPerBlock * rd + g;
@@ -1181,13 +1184,10 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
 #pragma unroll
     for (int g = 0; g < kEnvsPerBlock; g++) {
       const int it = kEnvsPerBlock * rd + g;
-      if (it < total && ((hb >> (16 * g)) & 1ull)) {
-        const int e = env_of(it);
-        f0 += e == 0; f1 += e == 1; f2 += e == 2; f3 += e == 3;
-      }
+      if (it < total && ((hb >> (16 * g)) & 1ull)) fpk += 1u << (8 * env_of(it));
     }
   }
-  return grp == 0 ? f0 : grp == 1 ? f1 : grp == 2 ? f2 : f3;
+  return (int)((fpk >> (8 * grp)) & 0xFFu);
 }
 
 }  // namespace so100

@@ -446,10 +446,7 @@ DEV void dynamics_par_bcast(const DevModel* __restrict__ m, EnvShared& sh, int l
     cross3(lin, ax, off);
 #pragma unroll
     for (int k = 0; k < 3; k++) { cdof_r[k] = ax[k]; cdof_r[3 + k] = lin[k]; }
-#pragma unroll
-    for (int k = 0; k < 13; k++) S.cin[a][k] = cin_r[k];
-#pragma unroll
-    for (int k = 0; k < 6; k++) S.cdof[a][k] = cdof_r[k];
+    // (no LDS copies of cin / cdof: this schedule reads the register copies by row broadcasts only)
   }
   DSTAMP(2);
   // ---- CRBA: composite inertia crb_i = cin_5 + ... + cin_i (that order) from the bodies' lanes by row broadcasts

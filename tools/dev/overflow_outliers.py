@@ -78,16 +78,26 @@ def detail(r, idx, solver, nsub):
     o64.set_state(d, q0, v0, w0)
     o64.env_step(model, d, 0, act)
     p64, f64, _, qa64, _ = o64.last_solve(d)
-    # the oracle's last substep's contact distances: re-run the step without the final position stage
-    d2 = o64.new_data()
-    o64.set_state(d2, q0, v0, w0)
-    for k in range(6):
-        d2.ctrl[k] = 0.0
+    # the solve's contact list in the oracle (nsub = 1: the position stage of the step's one substep), fp64 and fp32
+    o32 = Oracle(32)
+    cons = []
+    for o in (o64, o32):
+        d2 = o.new_data()
+        o.set_state(d2, q0, v0, w0)
+        o.call("so100o_fwd_position", model, d2)
+        cons.append([(d2.con[i].pair, d2.con[i].dist, np.array(d2.con[i].pos[:]), np.array(d2.con[i].frame[:3]))
+                     for i in range(d2.ncon)])
+    d32 = o32.new_data()
+    o32.set_state(d32, q0, v0, w0)
+    o32.env_step(model, d32, 0, act)
+    p32, f32, _, qa32, _ = o32.last_solve(d32)
     print(f"--- state {idx}: GPU ncon {nc}, oracle {len(p64)}; qacc GPU {np.array2string(gqa, precision=4)}\n"
-          f"    oracle qacc {np.array2string(qa64, precision=4)}")
+          f"    fp64 qacc {np.array2string(qa64, precision=4)}\n    fp32 qacc {np.array2string(qa32, precision=4)}")
     for c in range(max(nc, len(p64))):
-        g = f"pair {gp[c]:3d} dist {gd[c]: .3e} f {np.array2string(gf[c], precision=4)}" if c < nc else "-"
-        o = f"pair {p64[c]:3d} f {np.array2string(f64[c], precision=4)}" if c < len(p64) else "-"
+        g = f"pair {gp[c]:3d} dist {gd[c]: .4e} f {np.array2string(gf[c], precision=4)}" if c < nc else "-"
+        o = (f"pair {p64[c]:3d} dist {cons[0][c][1]: .4e} (fp32 {cons[1][c][1]: .4e}) f {np.array2string(f64[c], precision=4)}"
+             f" (fp32 {np.array2string(f32[c], precision=4)}) n {np.array2string(cons[0][c][3], precision=4)}"
+             if c < len(p64) and c < len(cons[1]) else "-")
         print(f"  c{c:2d} GPU {g} | fp64 {o}")
     env.close()
 
