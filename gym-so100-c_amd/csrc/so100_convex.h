@@ -34,6 +34,7 @@ struct MprObj {
 };
 constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
 constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
+constexpr float kSepTol = 1e-6f;            // a cached separating direction must clear the pair by 1 um (mpr_contacts)
 constexpr int kMprIters = 50;               // MuJoCo ccd_iterations
 
 DEV bool ccd_zero(float x) { return fabsf(x) < kCcdEps; }
@@ -495,7 +496,10 @@ DEV bool gjk_simplex(GjkPt* S, int& n, float* d) {
 }
 
 // GJK (oracle gjk): true when A - B encloses the origin, S then holds the enclosing tetrahedron
-DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, int lane) {
+// dsep: (the unit direction, 1) when the support test proved the pair separated, else w = 0 (so100_convex.h
+// mpr_contacts' separating-direction cache)
+DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, int lane, float4& dsep) {
+  dsep = make_float4(0.f, 0.f, 0.f, 0.f);
   float d[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) d[k] = o.hc[k] - o.c1[k];
@@ -512,7 +516,10 @@ DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, 
 #pragma unroll
     for (int k = 0; k < 3; k++) a.v[k] = as.v[k];
     a.id = as.id;
-    if (dot3(a.v, du) <= 0.f) return false;
+    if (dot3(a.v, du) <= 0.f) {
+      dsep = make_float4(du[0], du[1], du[2], 1.f);
+      return false;
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) pt_sel(S[k], a, n == k);
     n++;
@@ -789,7 +796,8 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
 
 // the mesh pairs' collider of the model (so100_model.convex): GJK + EPA (MuJoCo 3.3.3's default) or MPR
 DEV bool convex_penetration(const DevModel* __restrict__ m, const MprObj& o, float& depth, float* dir, float* pos,
-                            EpaPoly& P, int lane, int grp) {
+                            EpaPoly& P, int lane, int grp, float4& dsep) {
+  dsep = make_float4(0.f, 0.f, 0.f, 0.f);
   if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(m, o, depth, dir, pos, lane);
   GjkPt S[4];
 #pragma unroll
@@ -800,7 +808,7 @@ DEV bool convex_penetration(const DevModel* __restrict__ m, const MprObj& o, flo
   }
   const unsigned long long gt0 = ESTAMP_T();
   ESTAMP_ADD(2, 1);
-  const bool enc = gjk_enclose(m, o, S, lane);
+  const bool enc = gjk_enclose(m, o, S, lane, dsep);
   const unsigned long long gt1 = ESTAMP_T();
   ESTAMP_ADD(0, gt1 - gt0);
   if (!enc) return false;
@@ -1034,7 +1042,8 @@ DEV void stage_convex_hit(const DevModel* __restrict__ m, EnvShared& sh, float* 
 // Returns the env's number of convex contacts (uniform across its row).  Staged contacts j >= kMaxCon go to the
 // env's HBM contact record (slot j, kMprStageOff; crec0: the record of the wave's first env).
 template <bool kCells>
-DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec0, int lane, int grp, bool valid) {
+DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec0, float4* sep0, int lane, int grp,
+                     bool valid) {
   constexpr int kConvex = SO100_NPAIR_CONVEX;
   constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 8
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
@@ -1165,11 +1174,30 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     bool hit = false;
     int p = SO100_PAIR_MPR0;
     if (act) {
-      p = SO100_PAIR_MPR0 + reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_of(ie)];
+      const int q = reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_of(ie)];
+      p = SO100_PAIR_MPR0 + q;
       MprObj o;
       mpr_obj_setup(m, shm[ie], p, o);
       o.cells = kCells;
-      hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp);
+      // Temporal coherence: the direction that proved this pair separated in an earlier substep, re-checked on the
+      // current geometry with one support evaluation: max over the Minkowski difference along it below -kSepTol
+      // proves the pair separated now, which is GJK's own verdict (it returns no contact for a separated pair and
+      // for a touching one), so the contact list is the same; otherwise GJK (+ EPA) runs as before, from its usual
+      // start.  The cache never decides a contact: a stale entry (a reset, a far move) only fails the check.
+      float4* const sc = sep0 + (size_t)ie * kSepPairs + q;
+      const float4 c = *sc;
+      bool proved = false;
+      if (c.w != 0.f) {
+        const float du[3] = {c.x, c.y, c.z};
+        MprSup as;
+        mpr_support(m, o, du, as, lane);
+        proved = dot3(as.v, du) < -kSepTol;
+      }
+      if (!proved) {
+        float4 dsep;
+        hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp, dsep);
+        if (lane == 0) *sc = dsep;
+      }
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
     const uint64_t hb = __ballot(hit);

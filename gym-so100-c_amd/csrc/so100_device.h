@@ -150,6 +150,8 @@ constexpr int kConStride = kGeoOff + 24;    // 112 floats = 448 B per contact sl
 constexpr int kOvfJc = 12, kOvfJs = 16, kOvfF = 20;   // Newton overflow state (floats of the block)
 constexpr int kMprStageOff = 24;            // convex-collider staging (MprStage) of staged contacts >= kMaxCon
 constexpr size_t kConEnv = (size_t)kConCap * kConStride;   // floats per env
+// the convex pairs' separating-direction cache (so100_convex.h mpr_contacts): one float4 per (env, convex pair)
+constexpr int kSepPairs = 132;   // >= the 129 convex pairs (120 wave-shared + the EE marker's 9)
 enum HdrField : int {
   H_QACC = 0,       // qacc at the solver start (qacc_smooth, plus M^-1 J' f of the kept warmstart)
   H_FRAREF = 3,     // frictionloss rows: aref = -B vel
@@ -193,6 +195,9 @@ struct Workspace {
   // fused path (so100_fused_kernel): heavy-first wave order from the previous step's per-wave cost
   uint32_t* gcost;  // [ngroups] shader cycles of each 4-env wave in the last fused step
   int* order;       // [ngroups] launch order of the groups (so100_order_kernel), nullptr = natural
+  // [n][kSepPairs] the direction that last proved a convex pair separated (w = 1) or w = 0: a certificate the next
+  // substep re-checks with one support evaluation before it runs GJK (results unchanged: mpr_contacts)
+  float4* sep;
 };
 
 }  // namespace so100

@@ -459,7 +459,8 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     // box-hull pairs)
     // (the convex pairs first: the other collision results are then not held across their narrowphase's register
     // peak; the contacts are compacted in pair order below whatever the order of computation)
-    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, args.w.con + (size_t)(env - grp) * kConEnv, lane, grp, valid);
+    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, args.w.con + (size_t)(env - grp) * kConEnv,
+                                          args.w.sep + (size_t)(env - grp) * kSepPairs, lane, grp, valid);
     SSTAMP(7);
     float hx, hy, hz;
     const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
@@ -1454,13 +1455,15 @@ hipError_t alloc_workspace(int n, Workspace* w) {
   if (e == hipSuccess) e = hipMalloc(&w->hlist, 2 * kHeavyCap * sizeof(int));
   if (e == hipSuccess) e = hipMemset(w->gflag, 0, 2 * ngroups * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->hcount, 0, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&w->sep, (size_t)n * kSepPairs * sizeof(float4));
+  if (e == hipSuccess) e = hipMemset(w->sep, 0, (size_t)n * kSepPairs * sizeof(float4));
   if (e != hipSuccess) (void)free_workspace(w);
   return e;
 }
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
   for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist, (void*)w->gcost,
-                  (void*)w->order}) {
+                  (void*)w->order, (void*)w->sep}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
@@ -1468,6 +1471,7 @@ hipError_t free_workspace(Workspace* w) {
   w->hdr = w->con = nullptr;
   w->gflag = w->gcost = nullptr;
   w->hcount = w->hlist = w->order = nullptr;
+  w->sep = nullptr;
   return r;
 }
 // The fused path's workspace: the record header (only its contact counts are written), the wave-order buffers,
@@ -1484,6 +1488,8 @@ hipError_t alloc_fused_workspace(int n, Workspace* w) {
   if (e == hipSuccess) e = hipMalloc(&w->gcost, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->gcost, 0, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->order, ng * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&w->sep, (size_t)n * kSepPairs * sizeof(float4));
+  if (e == hipSuccess) e = hipMemset(w->sep, 0, (size_t)n * kSepPairs * sizeof(float4));
   if (e != hipSuccess) (void)free_workspace(w);
   return e;
 }

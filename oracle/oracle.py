@@ -11,6 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 NBODY, NHINGE, NQ, NV, NU, NGEOM, CONDIM, NOBS = 9, 6, 13, 12, 6, 16, 4, 15
+NPAIR = 209                           # include/so100_model.h SO100_NPAIR
 NCON_MAX = 62 * 8 + 209 - 62         # include/so100_model.h SO100_NCON_MAX: every pair at its collider's maximum
 NEFC = NV + NHINGE + NCON_MAX * CONDIM
 
@@ -56,6 +57,7 @@ def _make_types(real):
             ("weld_aref", _arr(real, 6)), ("weld_f", _arr(real, NV)),
             ("snap_ncon", i), ("snap_ndrop", i), ("snap_pair", _arr(i, NCON_MAX)),
             ("snap_force", _arr(real, NCON_MAX, 4)), ("snap_frf", _arr(real, NV)), ("snap_qacc", _arr(real, NV)),
+            ("sep_on", i), ("sep_hits", i), ("sep_sep", i), ("sep", _arr(real, NPAIR, 4)),
         ]
     return Contact, Data
 

@@ -930,8 +930,10 @@ static void so100o_item_push(int hit, int sep) {
 #define STAT(k, v) ((void)0)
 #endif
 
-/* GJK: 1 when A - B encloses the origin (S holds the enclosing tetrahedron), 0 otherwise */
-static int gjk(const mpr_obj* o, mpr_sup S[4]) {
+/* GJK: 1 when A - B encloses the origin (S holds the enclosing tetrahedron), 0 otherwise; dsep: (the direction, 1)
+ * when the support test proved the pair separated, else w = 0 (the kernels' separating-direction cache) */
+static int gjk(const mpr_obj* o, mpr_sup S[4], real dsep[4]) {
+  dsep[0] = dsep[1] = dsep[2] = dsep[3] = 0;
   real d[3];
   for (int k = 0; k < 3; k++) d[k] = o->hc[k] - o->c1[k];   /* from the interior point c1 - hc towards the origin */
   if (ccd_zero(dot3(d, d))) d[0] = 1;
@@ -944,7 +946,10 @@ static int gjk(const mpr_obj* o, mpr_sup S[4]) {
     real du[3] = {d[0] * ind, d[1] * ind, d[2] * ind};
     mpr_sup a;
     mpr_support(o, du, &a);
-    if (dot3(a.v, du) <= 0) return 0;              /* the support does not pass the origin: separated or touching */
+    if (dot3(a.v, du) <= 0) {                      /* the support does not pass the origin: separated or touching */
+      dsep[0] = du[0]; dsep[1] = du[1]; dsep[2] = du[2]; dsep[3] = 1;
+      return 0;
+    }
     S[n++] = a;
     if (n > 1 && gjk_simplex(S, &n, d)) return 1;
     if (n == 1) for (int k = 0; k < 3; k++) d[k] = -a.v[k];
@@ -1075,10 +1080,12 @@ static int box_axes_separate(const mpr_obj* o) {
 }
 #endif
 
-static int convex_penetration(const so100_model* m, const mpr_obj* o, real* depth, real dir[3], real pos[3]) {
+static int convex_penetration(const so100_model* m, const mpr_obj* o, real* depth, real dir[3], real pos[3],
+                              real dsep[4]) {
+  dsep[0] = dsep[1] = dsep[2] = dsep[3] = 0;
   if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(o, depth, dir, pos);
   mpr_sup S[4];
-  if (!gjk(o, S)) return 0;
+  if (!gjk(o, S, dsep)) return 0;
   STAT(1, 1);
   return epa_penetration(o, S, depth, dir, pos);
 }
@@ -1260,7 +1267,19 @@ static void collision(const so100_model* m, so100o_data* d) {
     so100o_item_mark[0] = so100o_stat_cur[3]; so100o_item_mark[1] = so100o_stat_cur[4];
 #endif
     real depth, dir[3], pos[3];
-    const int hit_ = convex_penetration(m, &o, &depth, dir, pos);
+    /* the kernels' separating-direction cache (so100_convex.h mpr_contacts), when d->sep_on: a direction that proved
+     * the pair separated in an earlier substep, re-checked with one support, skips GJK when it still clears the pair
+     * by 1e-6; results are unchanged (tests/test_oracle_epa.py::test_separation_cache_changes_nothing) */
+    if (d->sep_on && d->sep[p][3] != 0) {
+      real du[3] = {d->sep[p][0], d->sep[p][1], d->sep[p][2]};
+      mpr_sup a;
+      mpr_support(&o, du, &a);
+      if (dot3(a.v, du) < (real)-1e-6) { d->sep_hits++; continue; }
+    }
+    real dsep[4];
+    const int hit_ = convex_penetration(m, &o, &depth, dir, pos, dsep);
+    for (int k = 0; k < 4; k++) d->sep[p][k] = dsep[k];
+    d->sep_sep += dsep[3] != 0;
 #ifdef SO100O_STATS
     so100o_item_push(hit_, box_axes_separate(&o));
 #endif

@@ -97,3 +97,36 @@ def test_epa_position_is_between_the_surfaces(epa_contacts):
         lo_b, hi_a = (B @ n).min(), (A @ n).max()
         assert lo_b - 1e-9 <= pos @ n <= hi_a + 1e-9
         assert abs(pos @ n - 0.5 * (lo_b + hi_a)) < 1e-6 + 1e-3 * depth
+
+
+@pytest.mark.parametrize("bits", [64, 32])
+def test_separation_cache_changes_nothing(bits):
+    """The kernels' separating-direction cache (so100_convex.h mpr_contacts: a convex pair's last separating direction,
+    re-checked with one support before GJK) restated in the oracle (so100o_data.sep_on): random-action rollouts with
+    and without it are bitwise the same, state and contact lists, in both precisions, while the cache skips most of
+    the GJK runs of separated pairs."""
+    from oracle.oracle import Oracle
+    o = Oracle(bits)
+    m = build_model()
+    rng = np.random.default_rng(11)
+    hits = seps = 0
+    for env in range(10):
+        pose = o.spawn_pose(100 + env)
+        da, db = o.new_data(), o.new_data()
+        for d in (da, db):
+            o.reset(m, d, pose)
+        db.sep_on = 1
+        act = rng.uniform(-1, 1, 6).astype(np.float32)
+        for step in range(80):
+            if step % 8 == 0:
+                act = rng.uniform(-1, 1, 6).astype(np.float32)
+            for d in (da, db):
+                o.env_step(m, d, 0, act)
+            for xa, xb in zip(o.get_state(da), o.get_state(db)):
+                assert np.array_equal(xa, xb), (env, step)
+            pa, pb = o.last_solve(da)[0], o.last_solve(db)[0]
+            assert np.array_equal(pa, pb), (env, step)
+        hits += db.sep_hits
+        seps += db.sep_sep
+    print(f"\nGJK runs on separated pairs: {seps} with the cache, {hits} skipped by it")
+    assert hits > 2 * seps, (hits, seps)
