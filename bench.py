@@ -122,15 +122,16 @@ def cpu_baseline(seconds, solver="newton"):
 
 def load_step_traffic(n_envs, mode, solver):
     """The committed rocprofv3 PMC measurement of one env step's HBM traffic at this size and step mode
-    (profiles/r03_pmc_step_*.json, tools/gpurun/pmc_step_traffic.py: FETCH_SIZE and WRITE_SIZE passes, summed
-    over every kernel of a step), or None."""
-    path = os.path.join(ROOT, "profiles", f"r03_pmc_step_{mode}_{solver}_{n_envs}.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        return json.load(open(path))
-    except ValueError:
-        return None
+    (profiles/r<NN>_pmc_step_*.json, the newest round's, tools/gpurun/pmc_step_traffic.py: FETCH_SIZE and WRITE_SIZE
+    passes, summed over every kernel of a step), or None."""
+    for rnd in ("r04", "r03"):
+        path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_step_{mode}_{solver}_{n_envs}.json")
+        if os.path.exists(path):
+            try:
+                return json.load(open(path))
+            except ValueError:
+                return None
+    return None
 
 
 def main(argv=None):

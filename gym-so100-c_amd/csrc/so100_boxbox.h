@@ -317,7 +317,9 @@ DEV void geom_pose_b(const DevModel* __restrict__ m, const EnvShared& sh, int g,
     return;
   }
   if (b == SO100_MOCAP_BODY) {   // the EE variant's marker box: centred on the mocap body (so100_create checks)
-    cube_frame(sh.mocap, pos, mat);
+#pragma unroll
+    for (int k = 0; k < 3; k++) pos[k] = sh.mocap[k];
+    quat2mat(mat, sh.mocap + 3);      // normalised by set_controls
     return;
   }
   const float* bp;

@@ -435,6 +435,12 @@ int build_device_model(const so100_model* s, DevModel* d) {
   d->lim_K = (float)K;
   d->lim_B = (float)B;
   for (int k = 0; k < 5; k++) d->lim_solimp[k] = (float)s->jnt_solimp[k];
+  // the kernels' impedance (so100_dynamics.h getimpedance) takes solimp power 1 or 2 (MuJoCo's power, clamped at 1)
+  auto power_ok = [](const double* si) { const double pw = si[4] < 1 ? 1 : si[4]; return pw == 1 || pw == 2; };
+  if (!power_ok(s->jnt_solimp) || !power_ok(s->dof_solimp) || !power_ok(s->weld_solimp))
+    return fail("model: solimp power must be 1 or 2");
+  for (int p = 0; p < SO100_NPAIR; p++)
+    if (!power_ok(s->pair_solimp[p])) return fail("model: solimp power must be 1 or 2");
   for (int j = 0; j < 6; j++) d->lim_invw[j] = (float)s->dof_invweight0[j];
   for (int i = 0; i < SO100_NU; i++) {
     d->act_kp[i] = (float)s->act_kp[i];

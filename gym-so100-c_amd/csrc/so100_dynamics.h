@@ -41,12 +41,12 @@ DEV float getimpedance(const float* solimp, float pos, float margin) {
   float x = fabsf((pos - margin) * __builtin_amdgcn_rcpf(width));
   if (x >= 1.0f) return dmax;
   if (x <= 0.0f) return dmin;
+  // solimp power 1 or 2 (so100_create admits no other: MuJoCo's default 2 is the model's everywhere; a general
+  // power would inline four powf at every call site of this function, about 2,600 instructions of the fused kernel)
   float y;
   if (power == 1.0f) y = x;
-  else if (power == 2.0f) y = x <= mid ? x * x * __builtin_amdgcn_rcpf(mid)          // the model's solimp power
-                                       : 1.0f - (1.0f - x) * (1.0f - x) * __builtin_amdgcn_rcpf(1.0f - mid);
-  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.0f);
-  else y = 1.0f - powf(1.0f - x, power) / powf(1.0f - mid, power - 1.0f);
+  else y = x <= mid ? x * x * __builtin_amdgcn_rcpf(mid)
+                    : 1.0f - (1.0f - x) * (1.0f - x) * __builtin_amdgcn_rcpf(1.0f - mid);
   return dmin + y * (dmax - dmin);
 }
 
@@ -117,8 +117,7 @@ DEV void weld_fold(const DevModel* __restrict__ m, EnvShared& sh, int lane) {
 #pragma unroll
     for (int k = 0; k < 3; k++) p2[k] = S.xp[4][k] + t[k];
 #pragma unroll
-    for (int k = 0; k < 4; k++) q1[k] = sh.mocap[3 + k];
-    quat_normalize(q1);
+    for (int k = 0; k < 4; k++) q1[k] = sh.mocap[3 + k];      // normalised by set_controls
     quat2mat(R1, q1);
 #pragma unroll
     for (int i = 0; i < 3; i++)

@@ -158,17 +158,17 @@ DEV float4 ovf_j(const float* crec, int c, int lane, int ncon) {
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 // contact c's Newton data from its record slot (as the resident contacts' NewtonRows fields: aref, D = 1 / R, the
-// cone's mu, friction coefficients and middle-zone Dm)
+// cone's mu, friction coefficients and middle-zone Dm; the assembly stores D and Dm, so100_step.hip)
 struct OvfCon {
   float aref[4], D[4], mu, fr0, fr1, Dm;
 };
 DEV void ovf_load(const float* slot, OvfCon& o) {
-  const float4 a = reinterpret_cast<const float4*>(slot)[0], R = reinterpret_cast<const float4*>(slot)[1];
+  const float4 a = reinterpret_cast<const float4*>(slot)[0], D = reinterpret_cast<const float4*>(slot)[1];
   const float4 u = reinterpret_cast<const float4*>(slot)[2];
   o.aref[0] = a.x; o.aref[1] = a.y; o.aref[2] = a.z; o.aref[3] = a.w;
-  o.D[0] = 1.f / R.x; o.D[1] = 1.f / R.y; o.D[2] = 1.f / R.z; o.D[3] = 1.f / R.w;
+  o.D[0] = D.x; o.D[1] = D.y; o.D[2] = D.z; o.D[3] = D.w;
   o.mu = u.x; o.fr0 = u.y; o.fr1 = u.z;
-  o.Dm = o.D[0] / (o.mu * o.mu * (1.f + o.mu * o.mu));
+  o.Dm = u.w;
 }
 DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 DEV void st4(float* p, const float* v) { *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]); }

@@ -418,7 +418,14 @@ DEV void set_controls(const StageArgs& args, EnvShared& sh, int lane, int e, flo
                                           ((uint64_t)episode0 << 20) ^ (uint64_t)(elapsed0 * 8 + lane)));
     sh.ctrl[lane] = unnormalize_f32(a, m->action_lo[lane], m->action_hi[lane], m->action_span[lane]);
   }
-  if (m->ee && lane < 7) sh.mocap[lane] = B.mocap ? B.mocap[(size_t)e * 7 + lane] : m->mocap0[lane];
+  if (m->ee && lane < 7) {
+    // the mocap pose with its quaternion normalised once per env step (mj_kinematics normalises mocap_quat; the weld
+    // and the marker box read it every substep)
+    const float* src = B.mocap ? B.mocap + (size_t)e * 7 : m->mocap0;
+    float q[4] = {src[3], src[4], src[5], src[6]};
+    quat_normalize(q);
+    sh.mocap[lane] = lane < 3 ? src[lane] : lane == 3 ? q[0] : lane == 4 ? q[1] : lane == 5 ? q[2] : q[3];
+  }
 }
 
 // One substep's position/velocity stages and constraint assembly on the state in registers (after the
@@ -645,7 +652,15 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
           if (c < ncon) {
             float4* sl = reinterpret_cast<float4*>(crec + (size_t)c * kConStride);
             const float* g = crec + (size_t)c * kConStride;
-            newton_contact_rows(m, __float_as_int(g[kGeoPair]), g[kGeoDist], cv, fscale, sl[0], sl[1], sl[2]);
+            float4 aref4, R4, mu4;
+            newton_contact_rows(m, __float_as_int(g[kGeoPair]), g[kGeoDist], cv, fscale, aref4, R4, mu4);
+            // the solve's per-contact constants, as newton_solve derives them for the resident contacts (D = 1 / R,
+            // the middle zone's Dm), once here instead of at each of its reads (so100_newton.h ovf_load)
+            const float4 D4 = make_float4(1.f / R4.x, 1.f / R4.y, 1.f / R4.z, 1.f / R4.w);
+            mu4.w = D4.x / (mu4.x * mu4.x * (1.f + mu4.x * mu4.x));
+            sl[0] = aref4;
+            sl[1] = D4;
+            sl[2] = mu4;
           }
         }
         __syncthreads();          // the record's J rows are read by the other lanes of the row in the solve
