@@ -688,12 +688,13 @@ static int so100_struct_sizes_impl(int* model_bytes, int* buffers_bytes) {
 static so100_env* so100_create_impl(const so100_model* model, int n_envs, int device) {
   if (!model) { fail("so100_create: model is NULL"); return nullptr; }
   if (n_envs <= 0) { fail("so100_create: n_envs must be > 0"); return nullptr; }
+  // the model check first: host-only, so a malformed model fails the same way with or without a device
+  DevModel h;
+  if (build_device_model(model, &h) != 0) return nullptr;
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0) { fail_hip("so100_create: no HIP device", e == hipSuccess ? hipErrorNoDevice : e); return nullptr; }
   if (device < 0 || device >= ndev) { fail("so100_create: device index out of range"); return nullptr; }
-  DevModel h;
-  if (build_device_model(model, &h) != 0) return nullptr;
   DeviceGuard g(device);
   // the hulls' support cells: the table in the model, the candidates in their own buffer
   std::vector<uint32_t> hc;

@@ -88,3 +88,26 @@ def test_sb3_adapter_interface():
     for name in ("reset", "step_async", "step_wait", "step", "close", "seed", "get_attr", "set_attr",
                  "env_method", "env_is_wrapped", "get_images"):
         assert callable(getattr(SO100SB3VecEnv, name)), name
+
+
+@pytest.mark.parametrize("case", ["solimp_power", "marker_pair", "marker_off_centre"])
+def test_model_check_rejects_what_the_kernels_do_not_handle(model, case):
+    """so100_create's model check (before any device call) rejects a solimp power other than 1 or 2 (the kernels'
+    impedance has no general powf path), a marker pair that is not (marker, hull k), and a marker box off its
+    body's origin (the kernels take its pose as the mocap pose)."""
+    import copy
+    from gym_so100 import _native
+    from gym_so100.model import MOCAP_GEOM, PAIR_MOCAPHULL0
+    lib = _native.load()
+    bad = copy.deepcopy(model)
+    if case == "solimp_power":
+        bad.pair_solimp[5][4] = 3.0
+        want = b"solimp power"
+    elif case == "marker_pair":
+        bad.pair_geom2[PAIR_MOCAPHULL0 + 2] = -1
+        want = b"marker, hull k"
+    else:
+        bad.geom_pos[MOCAP_GEOM][0] = 0.01
+        want = b"centred"
+    assert lib.so100_create(ctypes.byref(bad), 4, 0) is None
+    assert want in lib.so100_last_error()
