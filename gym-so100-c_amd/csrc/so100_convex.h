@@ -34,7 +34,12 @@ struct MprObj {
 };
 constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
 constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
-constexpr float kSepTol = 1e-6f;            // a cached separating direction must clear the pair by 1 um (mpr_contacts)
+constexpr float kSepTol = 1e-6f;
+// EPA: a facet is visible from the new support point only when the point clears its plane by more than this (the
+// ccd_tolerance; oracle EPA_VISTOL): a point on a facet's plane within fp32 rounding is not "visible", so no facet is
+// built folding back over a coplanar one (an inverted facet, negative distance, that derailed fp32 EPA on face-face
+// hull contacts: DESIGN.md §4 deviation 7)
+constexpr float kEpaVisTol = 1e-6f;            // a cached separating direction must clear the pair by 1 um (mpr_contacts)
 constexpr int kMprIters = 50;               // MuJoCo ccd_iterations
 
 DEV bool ccd_zero(float x) { return fabsf(x) < kCcdEps; }
@@ -640,7 +645,7 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
       mfv[s3] = 0u;
       if (f < kEpaMaxF && ((alive >> f) & 1ull)) {
         const float4 pl = P.plane[f];
-        mv[s3] = (pl.x * w.v[0] + pl.y * w.v[1] + pl.z * w.v[2]) - pl.w > 0.f;
+        mv[s3] = (pl.x * w.v[0] + pl.y * w.v[1] + pl.z * w.v[2]) - pl.w > kEpaVisTol;
         mfv[s3] = P.fv[f];
       }
       vis |= ((__ballot(mv[s3]) >> (grp * kLanes)) & 0xFFFFull) << (kLanes * s3);

@@ -63,7 +63,7 @@ def _make_types(real):
 
 
 def ensure_built():
-    libs = [os.path.join(HERE, "build", f"liboracle{b}.so") for b in (64, 32)]
+    libs = [os.path.join(HERE, "build", f"liboracle{b}.so") for b in ("64", "32", "32fma")]
     if not all(os.path.exists(p) for p in libs):
         subprocess.check_call(["make", "-s", "-C", HERE])
     return libs
@@ -72,12 +72,13 @@ def ensure_built():
 class Oracle:
     """One precision flavour of the oracle library (bits=64 default, 32 = same code in float)."""
 
-    def __init__(self, bits=64):
+    def __init__(self, bits=64, fma=False):
+        """fma (bits=32 only): the build with multiply-adds contracted to FMAs, as the GPU compiler does"""
         ensure_built()
         self.bits = bits
         self.real = ctypes.c_double if bits == 64 else ctypes.c_float
         self.np_real = np.float64 if bits == 64 else np.float32
-        self.lib = ctypes.CDLL(os.path.join(HERE, "build", f"liboracle{bits}.so"))
+        self.lib = ctypes.CDLL(os.path.join(HERE, "build", f"liboracle{bits}{'fma' if fma else ''}.so"))
         self.Contact, self.Data = _make_types(self.real)
         L = self.lib
         P = ctypes.c_void_p

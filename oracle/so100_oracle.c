@@ -600,6 +600,7 @@ static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
  * the world at the end.  ccd_tolerance 1e-6, ccd_iterations 50 (MuJoCo defaults).  The loops libccd
  * leaves unbounded (discoverPortal's, refinePortal's) stop after the same 50 iterations: no contact. */
 #define MPR_TOL ((real)1e-6)
+#define EPA_VISTOL ((real)1e-6)
 #define MPR_ITERS 50
 /* libccd's zero/equality tests use MuJoCo's double-precision CCD_EPS (DBL_EPSILON) in both builds: the
  * tests are absolute, and FLT_EPSILON would misclassify mm-scale geometry (e.g. |v0 x v1|^2 ~ 1e-10 read
@@ -1008,7 +1009,9 @@ static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir
     /* the horizon: the edges (a, b) of the visible faces whose twin (b, a) is on no visible face, in (slot, edge)
      * order (the kernel finds them lane-parallel: each lane its slots' edges, the twin test by row ballots) */
     int vis[EPA_MAXF], edges[EPA_MAXE][2], ne = 0, over = 0;
-    for (int i = 0; i < EPA_MAXF; i++) vis[i] = F[i].alive && dot3(F[i].n, w.v) - F[i].dist > 0;
+    /* visible only when w clears the facet's plane by more than the ccd_tolerance (a point on the plane within
+     * rounding is not visible: no facet folds back over a coplanar one; the kernel's kEpaVisTol) */
+    for (int i = 0; i < EPA_MAXF; i++) vis[i] = F[i].alive && dot3(F[i].n, w.v) - F[i].dist > EPA_VISTOL;
     for (int i = 0; i < EPA_MAXF && !over; i++) {
       if (!vis[i]) continue;
       for (int k = 0; k < 3; k++) {

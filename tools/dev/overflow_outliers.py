@@ -1,7 +1,7 @@
 """The largest GPU errors of test_overflow_contact_parity's states (contact lists longer than 16), with the fp32
 restatement's error, the ensemble of 1-ulp perturbations and the contact lists of each (GPU box; test-side tool).
 
-    python tools/dev/overflow_outliers.py [newton|pgs] [nsubstep]
+    python tools/dev/overflow_outliers.py [newton|pgs] [nsubstep] [states.npz]
 """
 import os
 import sys
@@ -53,6 +53,9 @@ def main():
             print("   pairs fp64", list(p64))
     for i in order[:3]:
         detail(r, int(i), solver, nsub)
+    # the outlier states, for a CPU replay of their collision (tools/dev/epa_replay.py)
+    if len(sys.argv) > 3:
+        np.savez(sys.argv[3], **{f"s{int(i)}": np.concatenate([np.ravel(x) for x in r.states[int(i)][:4]]) for i in order})
 
 
 
