@@ -168,6 +168,9 @@ class TF:
         # the ensemble floor (_tf_run ens=K): per env step the fp64 oracle's error under K independent 1-ulp
         # input perturbations, qvel and qacc [steps, K], contact forces (lists equal to the fp64 oracle's)
         self.eqv, self.eqa, self.eforce = [], [], []
+        # (ens > 0) the fp32 restatement compiled with FMA contraction, as the GPU compiler contracts: a second fp32
+        # rounding of the same algorithm, qvel and qacc per env step
+        self.mqv, self.mqa = [], []
         self.pqv, self.pqa, self.pforce, self.psame = [], [], [], []
         self.force, self.fforce, self.same, self.fsame, self.pairs = [], [], [], [], []
         self.drop_gpu, self.drop_ora = [], []
@@ -178,7 +181,7 @@ class TF:
 
     def arrays(self):
         for k in ("qp", "qv", "fqp", "fqv", "qa", "fqa", "pqv", "pqa", "pforce", "psame", "force", "fforce", "same",
-                  "fsame", "drop_gpu", "drop_ora", "near0", "eqv", "eqa", "eforce"):
+                  "fsame", "drop_gpu", "drop_ora", "near0", "eqv", "eqa", "eforce", "mqv", "mqa"):
             setattr(self, k, np.array(getattr(self, k)))
         return self
 
@@ -280,7 +283,25 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
                         res.eforce += list(_force_err(fe, f64))
                 res.eqv.append(eq)
                 res.eqa.append(ea)
+                om = _oracle32fma()
+                dm = om.new_data()
+                om.set_state(dm, q0[i], v0[i], w0[i])
+                if mocap is not None:
+                    _set_mocap(dm, mocap[i])
+                om.env_step(model, dm, task, act[i])
+                res.mqv.append(_rel(om.get_state(dm)[1], ov))
+                res.mqa.append(_rel(om.last_solve(dm)[3], qa64))
     return res
+
+
+_O32FMA = []
+
+
+def _oracle32fma():
+    if not _O32FMA:
+        from oracle.oracle import Oracle
+        _O32FMA.append(Oracle(32, fma=True))
+    return _O32FMA[0]
 
 
 def _new_env(n, solver, **kw):
@@ -894,11 +915,13 @@ def _ensemble_bars(r, name="qv"):
     """The deep-fold gate (round 4): these states (links pushed centimetres into each other) are chaotic, so a
     single perturbation's maximum is a noisy bar that legal fp reorderings can cross.  The GPU's error
     distribution is graded against the ensemble of ENS independent 1-ulp input perturbations of the fp64 oracle
-    (and the fp32 restatement) on the same states: median, p90 and p99 within 2x the floor's (+1e-5 / 1e-4),
+    (and the fp32 restatement, host-compiled and FMA-contracted: round 4 found the contraction alone moves the
+    fp32 p99 up to 7x on these states, tools/dev/fp32_floor.py) on the same states: median, p90 and p99 within 2x the floor's (+1e-5 / 1e-4),
     the tail mass (share off by more than 1e-4) within 1.5x the floor's (+0.03), and per state the GPU beyond
     every ensemble member of its own state (2x + 1e-5) at most as often as one member would be (1 / (ENS + 1))."""
     g = getattr(r, name)
-    f = {"qv": r.fqv, "qa": r.fqa}[name]
+    # the fp32 floor: the restatement in fp32, as compiled for the host and with FMA contraction (the GPU's arithmetic)
+    f = np.maximum({"qv": r.fqv, "qa": r.fqa}[name], {"qv": r.mqv, "qa": r.mqa}[name])
     E = np.asarray({"qv": r.eqv, "qa": r.eqa}[name])
     ens = E.ravel()
     fl = lambda q: max(np.quantile(f, q), np.quantile(ens, q))
