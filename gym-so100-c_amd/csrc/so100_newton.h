@@ -34,11 +34,6 @@ namespace so100 {
 
 // One lane's share of a substep's Newton problem (its rows of the record).
 constexpr int kJReg = 8;               // contacts whose J rows stay in VGPRs
-#ifdef SO100_AB_NOOVF
-constexpr bool kOvfOn = false;         // TEMPORARY A/B (round 4): the overflow paths compiled out
-#else
-constexpr bool kOvfOn = true;
-#endif
 constexpr int kJLds = kMaxCon - kJReg;  // the others' J rows: LDS [kJLds][SO100_NV] float4 per env
 struct NewtonRows {
   float qs, warm, fr_aref;              // dof lanes: qacc_smooth, warmstart, frictionloss aref
@@ -365,7 +360,10 @@ DEV void newton_diag_write_ovf(float* dbg, const float* crec, int ncon, int lane
 // Solve one env's substep problem (its 16 lanes); returns qacc on the dof lanes.  want_diag: fill diag, the
 // diagnostics for the debug row, written by the caller (the row's address is then not held live across
 // the solve).  rec(): the env's HBM contact record (contacts >= kMaxCon), computed only where such contacts exist.
-template <class RecFn>
+// kOvf: the contacts beyond kMaxCon are handled (the wave holds an env with more than kMaxCon); the callers
+// instantiate both and choose per wave (newton_solve_any), so the common solve carries none of that code (a
+// same-box A/B measured the overflow paths inside the one solve at -3.0 % env steps/s at 65,536 envs)
+template <bool kOvf, class RecFn>
 DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, bool want_diag,
                        NewtonDiag& diag, RecFn rec) {
   const bool dof = lane < SO100_NV;
@@ -420,7 +418,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     const float gw = 0.5f * rowsum16(dof ? ew * mew : 0.f);
     float cwl = rows_cost(warm - fr_aref, lim_s * warm - lim_aref, xw);
     float csl = rows_cost(qs - fr_aref, lim_s * qs - lim_aref, xs);
-    if (kOvfOn && ncon_max > kMaxCon) {
+    if (kOvf && ncon_max > kMaxCon) {
       // contacts beyond kMaxCon: their jar at both candidates, the block's costs on the owning lanes; the
       // candidates go to the record (the chosen one becomes the iterate's jar below)
       float* crec = rec();
@@ -447,7 +445,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     const float cw = gw + rowsum16(cwl);
     const float cs = rowsum16(csl);
     const bool use_w = cw < cs;
-    if (kOvfOn && ncon_max > kMaxCon && !use_w) {
+    if (kOvf && ncon_max > kMaxCon && !use_w) {
       float* crec = rec();
       for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
         float* sl = ovf_slot(crec, c);
@@ -491,7 +489,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
       }
       for (int c = kJReg; c < ncon_max && c < kMaxCon; c++)
         grad -= dot4(jx_own(r, c, lane), shfl_row4(make_float4(fc[0], fc[1], fc[2], fc[3]), c));
-      if (kOvfOn && ncon_max > kMaxCon) {
+      if (kOvf && ncon_max > kMaxCon) {
         // contacts beyond kMaxCon: forces at the iterate's jar (kept in the record for c'(0) below), J' f
         float* crec = rec();
         for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
@@ -547,7 +545,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 #pragma unroll
           for (int j = 0; j < SO100_NV; j++) H[j] += dot4(w, jc_l[j]);
         }
-        if (kOvfOn && ncon_max > kMaxCon) {
+        if (kOvf && ncon_max > kMaxCon) {
           // contacts beyond kMaxCon: J' H_c J with J from the record (the Hessian re-evaluated at the iterate)
           float* crec = rec();
           for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
@@ -618,7 +616,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
         const float jsc[4] = {js4.x, js4.y, js4.z, js4.w};
         const float sfr = sv, slim = lim_s * sv;
         float ovf_l10 = 0.f;                   // contacts beyond kMaxCon: -f . J s at alpha = 0
-        if (kOvfOn && ncon_max > kMaxCon) {
+        if (kOvf && ncon_max > kMaxCon) {
           float* crec = rec();
           for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
             const float4 s4 = ovf_rows(crec, b0, sv, lane, ncon, ncon_max);
@@ -644,7 +642,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             l1 -= fv;
             l2 += vhv;
           }
-          if (kOvfOn && ncon_max > kMaxCon) {
+          if (kOvf && ncon_max > kMaxCon) {
             float* crec = rec();
             for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
               float* sl = ovf_slot(crec, c);
@@ -669,7 +667,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           l1 -= f_fr * sfr;
           l1 -= f_lim * slim;
           l1 -= fc[0] * jsc[0] + fc[1] * jsc[1] + fc[2] * jsc[2] + fc[3] * jsc[3];
-          if (kOvfOn && ncon_max > kMaxCon) l1 += ovf_l10;
+          if (kOvf && ncon_max > kMaxCon) l1 += ovf_l10;
           d10 = rowsum16(l1) + A1;
         }
         float alpha = 0.f;
@@ -706,7 +704,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           for (int k = 0; k < 4; k++) jc[k] += alpha * jsc[k];
           gauss += alpha * A1 + 0.5f * alpha * alpha * A2;
           float ncl = rows_cost(jfr, jlim, jc);
-          if (kOvfOn && ncon_max > kMaxCon) {
+          if (kOvf && ncon_max > kMaxCon) {
             // contacts beyond kMaxCon: jar += alpha J s in the record, their cost at the new iterate
             float* crec = rec();
             for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
@@ -750,6 +748,18 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     diag.impr = last_impr;
   }
   return qacc;
+}
+
+// the solve with or without the overflow paths, chosen per wave (uniform)
+template <class RecFn>
+DEV float newton_solve_any(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, bool want_diag,
+                           NewtonDiag& diag, RecFn rec) {
+  int ncon_max = r.ncon;
+  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
+  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
+  ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
+  if (ncon_max > kMaxCon) return newton_solve<true>(m, r, lane, valid, want_diag, diag, rec);
+  return newton_solve<false>(m, r, lane, valid, want_diag, diag, rec);
 }
 
 }  // namespace so100

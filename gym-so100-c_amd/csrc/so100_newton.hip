@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(kThreads, kNewtonWaves) so100_newton_kernel(Ne
   NewtonDiag diag;
   const bool dbg = a.last && a.debug;
   float* const crec = a.w.con + (size_t)e * kConEnv;      // contacts beyond kMaxCon (rare)
-  const float qacc = newton_solve(a.m, r, lane, valid, dbg, diag, [&]() { return crec; });
+  const float qacc = newton_solve_any(a.m, r, lane, valid, dbg, diag, [&]() { return crec; });
   if (dbg) {
     newton_diag_write(a.debug + (size_t)env * SO100_DBG_STRIDE, lane, valid, qacc, diag);
     if (valid) newton_diag_write_ovf(a.debug + (size_t)env * SO100_DBG_STRIDE, crec, r.ncon, lane);

@@ -631,7 +631,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
       nr.c_R = make_float4(1.f, 1.f, 1.f, 1.f);
       nr.c_mu = make_float4(1.f, 1.f, 1.f, 0.f);
       if (lane < ncon) newton_contact_rows(m, sh.con_pair[lane], sh.con_dist[lane], cVn, fscale, nr.c_aref, nr.c_R, nr.c_mu);
-      if (kOvfOn && ncon_max > kMaxCon) {
+      if (ncon_max > kMaxCon) {
         // the contacts beyond kMaxCon (rare): J and their aref / R / cone coefficients to the env's HBM record,
         // block by block of 16 (lane k: contact kMaxCon + 16 b + k), for both paths' newton_solve
         for (int b0 = kMaxCon; b0 < ncon_max; b0 += kLanes) {
@@ -1154,7 +1154,7 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       fresh_ids(group, args.n, l2, g2, en2, e2);
       return args.w.con + (size_t)e2 * kConEnv;
     };
-    const float qacc = newton_solve(sa.m, nr, lane, valid, dbg, diag, rec);
+    const float qacc = newton_solve_any(sa.m, nr, lane, valid, dbg, diag, rec);
     if (dbg) {
       int row = env;
       asm volatile("" : "+v"(row));        // not the assembly's row address (GVN would hold that across the solve)

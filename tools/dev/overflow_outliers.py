@@ -1,7 +1,7 @@
 """The largest GPU errors of test_overflow_contact_parity's states (contact lists longer than 16), with the fp32
 restatement's error, the ensemble of 1-ulp perturbations and the contact lists of each (GPU box; test-side tool).
 
-    python tools/dev/overflow_outliers.py [newton|pgs] [nsubstep] [states.npz]
+    python tools/dev/overflow_outliers.py [newton|pgs] [nsubstep, 0 = the model's 10] [states.npz] [overflow|base|self|padlink]
 """
 import os
 import sys
@@ -20,6 +20,12 @@ from gym_so100.model import NPAIR, build_model  # noqa: E402
 def main():
     solver = sys.argv[1] if len(sys.argv) > 1 else "newton"
     nsub = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    nsub = nsub or None
+    case = sys.argv[4] if len(sys.argv) > 4 else "overflow"
+    from gym_so100.model import PAIR_SELF0, PAIR_BASE0, PAIR_PADLINK0, PAIR_MOCAPHULL0
+    cases = {"overflow": (0, NPAIR, 29, lambda d: d.ncon > 16), "base": (PAIR_BASE0, PAIR_PADLINK0, 19, None),
+             "self": (PAIR_SELF0, PAIR_BASE0, 17, None), "padlink": (PAIR_PADLINK0, PAIR_MOCAPHULL0, 23, None)}
+    p0, p1, seed, select = cases[case]
     o64, o32 = Oracle(64), Oracle(32)
     orig = T._ensemble_bars
     T._ensemble_bars = lambda r, name="qv": np.zeros(len(r.qv), bool)     # report, do not assert
@@ -32,7 +38,7 @@ def main():
         return r
     T._tf_run = tf
     try:
-        T._arm_contact_parity(solver, o64, o32, 0, NPAIR, "overflow", 29, nsubstep=nsub, select=lambda d: d.ncon > 16)
+        T._arm_contact_parity(solver, o64, o32, p0, p1, case, seed, nsubstep=nsub, select=select)
     except AssertionError as e:
         print("assertion:", e)
     T._ensemble_bars = orig
@@ -46,7 +52,7 @@ def main():
         o64.env_step(model, d, 0, act)
         p64, f64, _, qa64, _ = o64.last_solve(d)
         gp = r.pairs[i]
-        print(f"step {i}: GPU qvel err {r.qv[i]:.3e} qacc {r.qa[i]:.3e} | fp32 oracle {r.fqv[i]:.3e} | ensemble "
+        print(f"step {i}: GPU qvel err {r.qv[i]:.3e} qacc {r.qa[i]:.3e} | fp32 oracle {r.fqv[i]:.3e} (FMA {r.mqv[i]:.3e}) | ensemble "
               f"{np.array2string(np.asarray(r.eqv[i]), precision=2)} | ncon GPU {len(gp)} oracle {len(p64)} same {r.same[i]}")
         if len(gp) != len(p64) or not np.array_equal(gp, p64):
             print("   pairs GPU ", list(gp))
