@@ -2012,6 +2012,13 @@ static void sol_newton(const so100_model* m, so100o_data* d) {
   memcpy(d->qacc, a, sizeof(a));
 }
 
+/* test hook: the Newton cost (Gauss + constraint) at qacc a, on the constraint rows of the last fwd_acceleration */
+double so100o_newton_cost(so100o_data* d, const so100o_real a[NV]) {
+  real jar[NEFC], f[NEFC];
+  jar_at(d, a, jar);
+  return (double)(gauss_cost(d, a) + constraint_cost(d, jar, f));
+}
+
 void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   /* [3P] mj_fwdActuation: position actuator, ctrl clamped to ctrlrange, force clamped to forcerange */
   memset(d->qfrc_actuator, 0, sizeof(d->qfrc_actuator));

@@ -209,7 +209,8 @@ class TF:
 def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, ens=0):
     """Teacher-forced steps: each starts the product kernels, the debug build and both oracles from the
     GPU's fp32 state (act_fn(step) -> [n, 6] float32 actions).  ens = K > 0: also the ensemble floor, the fp64
-    oracle from K independent 1-ulp perturbations of each state (TF.eqv / eqa / eforce)."""
+    oracle and the fp32 restatement from K independent 1-ulp perturbations of each state (TF.eqv / eqa: 2K
+    members per state; eforce: the fp64 members')."""
     res = res or TF()
     n = env.num_envs
     d64, d32, dp, dq = o64.new_data(), o32.new_data(), o64.new_data(), o64.new_data()
@@ -271,8 +272,8 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
             if ens:
                 eq, ea = [], []
                 for _ in range(ens):
-                    o64.set_state(dp, q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)),
-                                  v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12)), w0[i])
+                    qp, vp = q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)), v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12))
+                    o64.set_state(dp, qp, vp, w0[i])
                     if mocap is not None:
                         _set_mocap(dp, mocap[i])
                     o64.env_step(model, dp, task, act[i])
@@ -281,6 +282,14 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
                     ea.append(_rel(qae, qa64))
                     if np.array_equal(pe, p64) and len(pe):
                         res.eforce += list(_force_err(fe, f64))
+                    # the same perturbation through the fp32 restatement: fp32 arithmetic's own discrete flips (an EPA
+                    # face-face witness, whose tie between coplanar facets fp32 rounding breaks either way) on this state
+                    o32.set_state(d32, qp, vp, w0[i])
+                    if mocap is not None:
+                        _set_mocap(d32, mocap[i])
+                    o32.env_step(model, d32, task, act[i])
+                    eq.append(_rel(o32.get_state(d32)[1], ov))
+                    ea.append(_rel(o32.last_solve(d32)[3], qa64))
                 res.eqv.append(eq)
                 res.eqa.append(ea)
                 om = _oracle32fma()
@@ -908,15 +917,16 @@ def test_domain_randomization_config4_shard(solver):
     shard.close()
 
 
-ENS = 8     # the ensemble floor's size: independent 1-ulp perturbations of each state
+ENS = 8     # the ensemble floor's size: independent 1-ulp perturbations of each state (each through fp64 and fp32)
 
 
 def _ensemble_bars(r, name="qv"):
     """The deep-fold gate (round 4): these states (links pushed centimetres into each other) are chaotic, so a
     single perturbation's maximum is a noisy bar that legal fp reorderings can cross.  The GPU's error
-    distribution is graded against the ensemble of ENS independent 1-ulp input perturbations of the fp64 oracle
-    (and the fp32 restatement, host-compiled and FMA-contracted: round 4 found the contraction alone moves the
-    fp32 p99 up to 7x on these states, tools/dev/fp32_floor.py) on the same states: median, p90 and p99 within 2x the floor's (+1e-5 / 1e-4),
+    distribution is graded against the ensemble of ENS independent 1-ulp input perturbations of each state, each run
+    through the fp64 oracle and the fp32 restatement (fp32 rounding breaks discrete ties, e.g. an EPA face-face
+    witness, that fp64 resolves one way: round 4), and the fp32 restatement host-compiled and FMA-contracted (the
+    contraction alone moves the fp32 p99 up to 7x on these states, tools/dev/fp32_floor.py) on the same states: median, p90 and p99 within 2x the floor's (+1e-5 / 1e-4),
     the tail mass (share off by more than 1e-4) within 1.5x the floor's (+0.03), and per state the GPU beyond
     every ensemble member of its own state (2x + 1e-5) at most as often as one member would be (1 / (ENS + 1))."""
     g = getattr(r, name)

@@ -47,10 +47,13 @@ def main():
             o.env_step(model, ds[k], 0, act)
             res[k] = o.last_solve(ds[k])
         p64, f64, _, qa64, _ = res["fp64"]
-        line = f"sub {sub}: ncon GPU {len(gp)} fp64 {len(p64)} | qacc |GPU-fp64| {np.abs(gqa - qa64).max():.3e}"
+        line = (f"sub {sub}: ncon GPU {len(gp)} fp64 {len(p64)} | GPU iters {int(dbg[1])} impr {dbg[2]:.2e}, fp64 "
+                f"{ds['fp64'].solver_iter} {ds['fp64'].solver_improvement:.2e}, fp32 {ds['fp32'].solver_iter} "
+                f"{ds['fp32'].solver_improvement:.2e} | qacc |GPU-fp64| {np.abs(gqa - qa64).max():.3e}")
         for k in ("fp32", "fma"):
             line += f" |{k}-fp64| {np.abs(res[k][3] - qa64).max():.3e}"
         print(line)
+        print(f"   qacc GPU {np.array2string(gqa, precision=4)}\n   qacc fp64 {np.array2string(qa64, precision=4)}")
         for c in range(max(len(gp), len(p64))):
             g = f"{gp[c]:3d} d {gd[c]: .5e} f {np.array2string(gf[c], precision=3)}" if c < len(gp) and c < 16 else "-"
             o = f"{p64[c]:3d} f {np.array2string(f64[c], precision=3)}" if c < len(p64) else "-"
