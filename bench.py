@@ -67,6 +67,8 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-kernel-timing", action="store_true", help="skip the per-launch HIP events")
     p.add_argument("--contact-steps", type=int, default=10, help="untimed steps sampling contacts/env")
+    p.add_argument("--fused-build", type=int, default=0, choices=[0, 2, 3],
+                   help="the fused product build: 2 | 3 waves per SIMD, 0 = the library's choice by size")
     p.add_argument("--solver", default="newton", choices=["newton", "pgs"],
                    help="constraint solver: newton (MuJoCo's default, which the reference runs; default) or pgs")
     p.add_argument("--convex", default="epa", choices=["epa", "mpr"],
@@ -167,6 +169,8 @@ def main(argv=None):
     from gym_so100 import SO100VecEnv
     env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset, solver=args.solver,
                       convex=args.convex)
+    if args.fused_build:
+        env.fused_build = args.fused_build
     env.reset(seed=1000 + offset)   # env i <- RandomState(1000 + global id)
     # the action pool is drawn for all `total` envs from one seed and sliced to this shard, so env i's actions
     # (and its trajectory) do not depend on the number of ranks
