@@ -171,9 +171,9 @@ class TF:
         # (ens > 0) the fp32 restatement compiled with FMA contraction, as the GPU compiler contracts: a second fp32
         # rounding of the same algorithm, qvel and qacc per env step
         self.mqv, self.mqa = [], []
-        # (ens > 0) where the GPU lies beyond the fp64 members and the single fp32 runs of its state: the largest error
-        # the fp32 restatement reaches on that state, over its ensemble members and up to 64 more 1-ulp perturbations
-        # (a search for the same discrete event in fp32 arithmetic), else 0
+        # (ens > 0) where the GPU lies beyond the single fp32 runs of its state (host-compiled and FMA): the largest error
+        # its ensemble members (fp64 and fp32) reach, and up to 64 more fp32 1-ulp perturbations of that state (a search
+        # for the same discrete event in fp32 arithmetic), else 0
         self.aqv, self.aqa = [], []
         self.pqv, self.pqa, self.pforce, self.psame = [], [], [], []
         self.force, self.fforce, self.same, self.fsame, self.pairs = [], [], [], [], []
@@ -275,7 +275,6 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
             res.states.append((q0[i], v0[i], w0[i], act[i]) + ((mocap[i],) if mocap is not None else ()))
             if ens:
                 eq, ea = [], []
-                e32q, e32a = [], []             # the fp32 members alone
                 for _ in range(ens):
                     qp, vp = q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)), v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12))
                     o64.set_state(dp, qp, vp, w0[i])
@@ -295,8 +294,6 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
                     o32.env_step(model, d32, task, act[i])
                     eq.append(_rel(o32.get_state(d32)[1], ov))
                     ea.append(_rel(o32.last_solve(d32)[3], qa64))
-                    e32q.append(eq[-1])
-                    e32a.append(ea[-1])
                 res.eqv.append(eq)
                 res.eqa.append(ea)
                 om = _oracle32fma()
@@ -309,10 +306,8 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
                 res.mqa.append(_rel(om.last_solve(dm)[3], qa64))
                 gqv, gqa_ = res.qv[-1], res.qa[-1]
                 aqv = aqa = 0.0
-                f64q = max(eq[k] for k in range(0, len(eq), 2))      # the fp64 members (even slots)
-                f64a = max(ea[k] for k in range(0, len(ea), 2))
-                if gqv > 2 * max(f64q, res.fqv[-1], res.mqv[-1]) + 1e-5 or gqa_ > 2 * max(f64a, res.fqa[-1], res.mqa[-1]) + 1e-5:
-                    aqv, aqa = max(e32q), max(e32a)
+                if gqv > 2 * max(res.fqv[-1], res.mqv[-1]) + 1e-5 or gqa_ > 2 * max(res.fqa[-1], res.mqa[-1]) + 1e-5:
+                    aqv, aqa = max(eq), max(ea)
                     for _ in range(64):
                         if aqv >= 0.5 * gqv and aqa >= 0.5 * gqa_:
                             break
