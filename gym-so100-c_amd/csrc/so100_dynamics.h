@@ -192,218 +192,27 @@ DEV void weld_fold(const DevModel* __restrict__ m, EnvShared& sh, int lane) {
   __syncthreads();
 }
 
-DEV void dynamics_par_lds(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale DSTAMP_PARAMS) {
-  SerialScratch& S = sh.ser;
-  // ---- comPos (body a = lane): cinert about the tree reference point r = Base xpos; cdof
-  if (lane < 6) {
-    const int a = lane;
-    const float* r = m->base_pos;
-    float xm[9], xp[3], ax[3];
-#pragma unroll
-    for (int k = 0; k < 9; k++) xm[k] = S.xm[a][k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) { xp[k] = S.xp[a][k]; ax[k] = sh.axis[a][k]; }
-    float ip[3], xi[3], IM[9], diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Ib[9], RT[9], Iw[9];
-    mulmv3(ip, xm, m->body_ipos[a]);
-#pragma unroll
-    for (int k = 0; k < 3; k++) xi[k] = xp[k] + ip[k] - r[k];
-    mulmm3(IM, xm, m->body_imat[a]);
-    diag[0] = m->body_inertia[a][0]; diag[4] = m->body_inertia[a][1]; diag[8] = m->body_inertia[a][2];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) RT[3 * i + j] = IM[3 * j + i];
-    mulmm3(Ib, IM, diag);
-    mulmm3(Iw, Ib, RT);
-    const float mass = m->body_mass[a];
-    const float dd2 = dot3(xi, xi);
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) S.cin[a][3 * i + j] = Iw[3 * i + j] + mass * ((i == j ? dd2 : 0.f) - xi[i] * xi[j]);
-#pragma unroll
-    for (int k = 0; k < 3; k++) S.cin[a][9 + k] = mass * xi[k];
-    S.cin[a][12] = mass;
-    float off[3] = {r[0] - xp[0], r[1] - xp[1], r[2] - xp[2]}, lin[3];
-    cross3(lin, ax, off);
-#pragma unroll
-    for (int k = 0; k < 3; k++) { S.cdof[a][k] = ax[k]; S.cdof[a][3 + k] = lin[k]; }
-  }
-  __syncthreads();
-  DSTAMP(2);
-  // ---- CRBA: composite inertia crb_i = cin_5 + ... + cin_i (that order), F_i = crb_i cdof_i
-  if (lane < 6) {
-    const int i = lane;
-    float crb[13];
-#pragma unroll
-    for (int k = 0; k < 13; k++) crb[k] = 0.f;
-#pragma unroll
-    for (int b = 5; b >= 0; b--) {
-      if (b >= i) {
-#pragma unroll
-        for (int k = 0; k < 13; k++) crb[k] += S.cin[b][k];
-      }
-    }
-    float F[6], cd[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) cd[k] = S.cdof[i][k];
-    mul_inert(F, crb, cd);
-#pragma unroll
-    for (int k = 0; k < 6; k++) S.F[i][k] = F[k];
-    // row i of M (j <= i) and its mirror: M(i,j) = cdof_j . F_i
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-      if (j <= i) {
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 6; k++) v += S.cdof[j][k] * F[k];
-        if (j == i) v += m->armature[i];
-        S.M[i][j] = v;
-        S.M[j][i] = v;
-      }
-    }
-  }
-  __syncthreads();
-  DSTAMP(3);
-  if (m->ee) weld_fold(m, sh, lane);
-  // ---- Cholesky of the 6x6 on each of lanes 0..5 (the same instructions on the same values: no serial lane,
-  // no barrier, no LDS round trip), then lane c solves M x = e_c for the M^-1 column c
-  DSTAMP(4);
-  if (lane < 6) {
-    const int c = lane;
-    float L[6][6], Linv[6], z[6], x[6];
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-      float sdiag = S.M[j][j];
-#pragma unroll
-      for (int k = 0; k < j; k++) sdiag -= L[j][k] * L[j][k];
-      const float sd = fmaxf(sdiag, kMinVal);
-      Linv[j] = __builtin_amdgcn_rsqf(sd);          // 1 / L_jj by v_rsq (1 ulp), L_jj = sd / L_jj
-      L[j][j] = sd * Linv[j];
-#pragma unroll
-      for (int i = j + 1; i < 6; i++) {
-        float t = S.M[i][j];
-#pragma unroll
-        for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
-        L[i][j] = t * Linv[j];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-      float sacc = (i == c) ? 1.f : 0.f;
-#pragma unroll
-      for (int k = 0; k < i; k++) sacc -= L[i][k] * z[k];
-      z[i] = sacc * Linv[i];
-    }
-#pragma unroll
-    for (int i = 5; i >= 0; i--) {
-      float sacc = z[i];
-#pragma unroll
-      for (int k = i + 1; k < 6; k++) sacc -= L[k][i] * x[k];
-      x[i] = sacc * Linv[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) S.X[c][i] = x[i];
-  }
-  // ---- RNE (flg_acc = 0), part 1: cvel_a = sum_{k<=a} cdof_k qd_k, cdof_dot_a = cvel_a x cdof_a
-  if (lane < 6) {
-    const int a = lane;
-    float cvel[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int b = 0; b < 6; b++) {
-      if (b <= a) {
-        const float qd = sh.qvel[b];
-#pragma unroll
-        for (int k = 0; k < 6; k++) cvel[k] += S.cdof[b][k] * qd;
-      }
-    }
-    float cd[6], cdd[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) cd[k] = S.cdof[a][k];
-    cross_motion(cdd, cvel, cd);
-#pragma unroll
-    for (int k = 0; k < 6; k++) S.cdd[a][k] = cdd[k];
-  }
-  __syncthreads();
-  DSTAMP(5);
-  // symmetrised M^-1 -> LDS (minv), RNE part 2: cacc_a = -g + sum_{k<=a} cdd_k qd_k, body forces
-  if (lane < 6) {
-    const int a = lane;
-#pragma unroll
-    for (int j = 0; j < 6; j++) sh.minv[a][j] = 0.5f * (S.X[j][a] + S.X[a][j]);
-    float cvel[6] = {0, 0, 0, 0, 0, 0};
-    float cacc[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-#pragma unroll
-    for (int b = 0; b < 6; b++) {
-      if (b <= a) {
-        const float qd = sh.qvel[b];
-#pragma unroll
-        for (int k = 0; k < 6; k++) cvel[k] += S.cdof[b][k] * qd;
-#pragma unroll
-        for (int k = 0; k < 6; k++) cacc[k] += S.cdd[b][k] * qd;
-      }
-    }
-    float cin[13];
-#pragma unroll
-    for (int k = 0; k < 13; k++) cin[k] = S.cin[a][k];
-    float f1[6], Iv[6], f2[6];
-    mul_inert(f1, cin, cacc);
-    mul_inert(Iv, cin, cvel);
-    cross_force(f2, cvel, Iv);
-#pragma unroll
-    for (int k = 0; k < 6; k++) S.cfrc[a][k] = f1[k] + f2[k];
-  }
-  __syncthreads();
-  DSTAMP(6);
-  // ---- bias_a = cdof_a . sum_{k>=a} cfrc_k (suffix, from body 5 down); actuation
-  float tau = 0.f;
-  if (lane < 6) {
-    const int a = lane;
-    float acc[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int b = 5; b >= 0; b--) {
-      if (b >= a) {
-#pragma unroll
-        for (int k = 0; k < 6; k++) acc[k] += S.cfrc[b][k];
-      }
-    }
-    float bias = 0.f;
-#pragma unroll
-    for (int k = 0; k < 6; k++) bias += S.cdof[a][k] * acc[k];
-    const float c = fminf(fmaxf(sh.ctrl[a], m->act_clo[a]), m->act_chi[a]);
-    float f = m->act_kp[a] * c - m->act_kp[a] * sh.qpos[a] - m->act_kv[a] * sh.qvel[a];
-    f = fminf(fmaxf(f, m->act_flo[a]), m->act_fhi[a]);
-    tau = f - bias + (m->ee ? sh.qacc_smooth[a] : 0.f);   // + J'D aref of the weld (weld_fold)
-  }
-  // tau_j to every lane by DPP broadcasts, taken by the whole row before any lane branches (no barrier and
-  // no LDS round trip; minv was written before the last barrier)
-  float tj[6];
-#pragma unroll
-  for (int j = 0; j < 6; j++) tj[j] = bcast_row(tau, j);
-  if (lane < 6) {
-    const int i = lane;
-    float sacc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 6; j++) sacc += sh.minv[i][j] * tj[j];
-    sh.qacc_smooth[i] = sacc;
-  } else if (lane < 9) {
-    // cube (free body): -bias / m = g, gyroscopic term on the rotational dofs
-    const int k = lane - 6;
-    const float mc = m->cube_mass * mscale;
-    const float I3[3] = {m->cube_inertia[0] * mscale, m->cube_inertia[1] * mscale, m->cube_inertia[2] * mscale};
-    const float w[3] = {sh.qvel[9], sh.qvel[10], sh.qvel[11]};
-    float Iw3[3] = {I3[0] * w[0], I3[1] * w[1], I3[2] * w[2]}, gyro[3];
-    cross3(gyro, w, Iw3);
-    const float gk = k == 0 ? gyro[0] : (k == 1 ? gyro[1] : gyro[2]);
-    const float Ik = k == 0 ? I3[0] : (k == 1 ? I3[1] : I3[2]);
-    sh.qacc_smooth[6 + k] = (mc * m->gravity[k]) / mc;
-    sh.qacc_smooth[9 + k] = -gk / Ik;
-    sh.inv_mcube[k] = 1.0f / mc;
-    sh.inv_mcube[3 + k] = 1.0f / Ik;
-  }
+// Sums over the arm's bodies (lanes 0..5 of each 16-lane DPP row; lanes 6..15 hold zeros): inclusive prefix
+// (bodies <= lane) and suffix (bodies >= lane) sums in 3 Hillis-Steele steps, row_shr / row_shl by 1, 2, 4 with
+// bound_ctrl (lanes past the row's edge add 0).  Lane l's suffix is ((a_l + a_l+1) + (a_l+2 + a_l+3)) +
+// (a_l+4 + a_l+5): the same sums as MuJoCo's serial order (engine_core_smooth.c mj_crb / mj_rne) up to rounding.
+// The whole row must be active.
+DEV float row_prefix6(float x) {
+  x += dpp<0x111>(x);
+  x += dpp<0x112>(x);
+  return x + dpp<0x114>(x);
+}
+DEV float row_suffix6(float x) {
+  x += dpp<0x101>(x);
+  x += dpp<0x102>(x);
+  return x + dpp<0x104>(x);
 }
 
-DEV void dynamics_par_bcast(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale DSTAMP_PARAMS) {
+// The arm's dynamics on one env's 16-lane row (body a on lane a): comPos, CRBA, the M^-1 columns, RNE and the
+// actuation.  The bodies' cinert / cdof / cdof_dot / body forces never leave registers: the tree's prefix and
+// suffix sums are DPP scans (round 2 exchanged them through LDS with barriers and summed them serially; round 3
+// by 6 row broadcasts per sum, in the serial order).
+DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale DSTAMP_PARAMS) {
   SerialScratch& S = sh.ser;
   // ---- comPos (body a = lane): cinert about the tree reference point r = Base xpos; cdof.  Lanes >= 6 hold
   // zeros (the CRBA's row scans read them).
@@ -445,24 +254,14 @@ DEV void dynamics_par_bcast(const DevModel* __restrict__ m, EnvShared& sh, int l
     cross3(lin, ax, off);
 #pragma unroll
     for (int k = 0; k < 3; k++) { cdof_r[k] = ax[k]; cdof_r[3 + k] = lin[k]; }
-    // (no LDS copies of cin / cdof: this schedule reads the register copies by row broadcasts only)
   }
   DSTAMP(2);
-  // ---- CRBA: composite inertia crb_i = cin_5 + ... + cin_i (that order) from the bodies' lanes by row broadcasts
-  // (round 2 read them from LDS after a barrier; the same sums bit for bit), F_i = crb_i cdof_i; row i of M
+  // ---- CRBA: composite inertia crb_i = cin_i + ... + cin_5 by a suffix scan, F_i = crb_i cdof_i; row i of M
   // (j <= i) from the row's cdof_j broadcasts, and its mirror
   {
     float crb[13];
 #pragma unroll
-    for (int k = 0; k < 13; k++) crb[k] = 0.f;
-#pragma unroll
-    for (int b = 5; b >= 0; b--) {                 // the serial order (cin_5 first): bitwise the LDS version's sums
-#pragma unroll
-      for (int k = 0; k < 13; k++) {
-        const float x = bcast_row(cin_r[k], b);
-        crb[k] = b >= lane ? crb[k] + x : crb[k];
-      }
-    }
+    for (int k = 0; k < 13; k++) crb[k] = row_suffix6(cin_r[k]);
     float F[6];
     mul_inert(F, crb, cdof_r);
     float mrow[6];
@@ -527,35 +326,15 @@ DEV void dynamics_par_bcast(const DevModel* __restrict__ m, EnvShared& sh, int l
 #pragma unroll
     for (int i = 0; i < 6; i++) S.X[c][i] = x[i];
   }
-  // ---- RNE (flg_acc = 0) from the bodies' lanes by row broadcasts, summed in the serial order (bitwise the sums
-  // of round 2, which read the other bodies' cdof / cdd / cfrc from LDS after two barriers): cvel_a = sum_{k<=a}
-  // cdof_k qd_k, cdof_dot_a = cvel_a x cdof_a, cacc_a = -g + sum_{k<=a} cdd_k qd_k, the body forces,
-  // bias_a = cdof_a . sum_{k>=a} cfrc_k
+  // ---- RNE (flg_acc = 0) by prefix / suffix scans: cvel_a = sum_{k<=a} cdof_k qd_k, cdof_dot_a = cvel_a x cdof_a,
+  // cacc_a = -g + sum_{k<=a} cdd_k qd_k, the body forces, bias_a = cdof_a . sum_{k>=a} cfrc_k
   const float qd_own = lane < 6 ? sh.qvel[lane] : 0.f;
   float cvel[6], cdd[6], cacc[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) cvel[k] = 0.f;
-#pragma unroll
-  for (int b = 0; b < 6; b++) {                   // serial order, as the LDS version
-    const float qd = bcast_row(qd_own, b);
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const float x = bcast_row(cdof_r[k], b);
-      cvel[k] = b <= lane ? cvel[k] + x * qd : cvel[k];
-    }
-  }
+  for (int k = 0; k < 6; k++) cvel[k] = row_prefix6(cdof_r[k] * qd_own);
   cross_motion(cdd, cvel, cdof_r);
-  cacc[0] = cacc[1] = cacc[2] = 0.f;
-  cacc[3] = -m->gravity[0]; cacc[4] = -m->gravity[1]; cacc[5] = -m->gravity[2];
 #pragma unroll
-  for (int b = 0; b < 6; b++) {
-    const float qd = bcast_row(qd_own, b);
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const float x = bcast_row(cdd[k], b);
-      cacc[k] = b <= lane ? cacc[k] + x * qd : cacc[k];
-    }
-  }
+  for (int k = 0; k < 6; k++) cacc[k] = (k < 3 ? 0.f : -m->gravity[k - 3]) + row_prefix6(cdd[k] * qd_own);
   float cfrc[6];
   {
     float f1[6], Iv[6], f2[6];
@@ -565,17 +344,9 @@ DEV void dynamics_par_bcast(const DevModel* __restrict__ m, EnvShared& sh, int l
 #pragma unroll
     for (int k = 0; k < 6; k++) cfrc[k] = f1[k] + f2[k];
   }
-  float facc[6];                                  // sum_{k>=a} cfrc_k, from body 5 down (serial order)
+  float facc[6];                                  // sum_{k>=a} cfrc_k
 #pragma unroll
-  for (int k = 0; k < 6; k++) facc[k] = 0.f;
-#pragma unroll
-  for (int b = 5; b >= 0; b--) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const float x = bcast_row(cfrc[k], b);
-      facc[k] = b >= lane ? facc[k] + x : facc[k];
-    }
-  }
+  for (int k = 0; k < 6; k++) facc[k] = row_suffix6(cfrc[k]);
   __syncthreads();               // the M^-1 columns of the other lanes (S.X)
   DSTAMP(5);
   // symmetrised M^-1 -> LDS (minv; each lane its own row, read back only by itself)
@@ -625,16 +396,5 @@ DEV void dynamics_par_bcast(const DevModel* __restrict__ m, EnvShared& sh, int l
   }
 }
 
-// The arm's dynamics, two schedules of the same arithmetic (bitwise the same results, tools/dev/lib_states.py):
-// dynamics_par_lds exchanges the bodies' cinert / cdof / cdd / cfrc through LDS with barriers; dynamics_par_bcast
-// takes them from the bodies' lanes by row broadcasts, summed in the same serial order.  The broadcast schedule has
-// the shorter latency chain and more VALU instructions: +0.8 % env steps/s at 8,192 envs (2-wave fused build, every
-// wave resident, the step latency-bound), -2.0 % at 65,536 (3-wave build, issue-bound), same-box A/B
-// (profiles/r03_ab_dyn_bcast.txt); the 2-wave fused build takes it (+0.9 % at 8,192, profiles/r03_ab_dyn_bcast_w2.txt).
-template <bool kBcast>
-DEV void dynamics_par(const DevModel* __restrict__ m, EnvShared& sh, int lane, float mscale DSTAMP_PARAMS) {
-  if constexpr (kBcast) dynamics_par_bcast(m, sh, lane, mscale DSTAMP_ARGS);
-  else dynamics_par_lds(m, sh, lane, mscale DSTAMP_ARGS);
-}
 
 }  // namespace so100

@@ -432,7 +432,7 @@ DEV void set_controls(const StageArgs& args, EnvShared& sh, int lane, int e, flo
 // previous substep's Euler): kinematics, CRBA/RNE, actuation, collision, the frictionloss / limit /
 // contact rows.  Newton: the rows go to nr (kFused: kept in registers for newton_solve; split: stored to the
 // HBM record); PGS: the solver record of so100_pgs_kernel.
-template <int kSolver, bool kFused, bool kDebug = true, bool kBcastDyn = false>
+template <int kSolver, bool kFused, bool kDebug = true>
 DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int env, int e, bool valid, float qpos_r,
                   float qvel_r, float warm_r, float mscale, float fscale, int sub, NewtonRows& nr) {
   const DevModel* __restrict__ m = args.m;
@@ -447,7 +447,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     fk_par(m, sh, lane);
     __syncthreads();
     DSTAMP(1);
-    dynamics_par<kBcastDyn>(m, sh, lane, mscale DSTAMP_ARGS);
+    dynamics_par(m, sh, lane, mscale DSTAMP_ARGS);
     __syncthreads();
     DSTAMP(7);
     if constexpr (kSolver == SO100_SOLVER_NEWTON) {
@@ -1142,8 +1142,8 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       sa.m = reinterpret_cast<const DevModel*>(reinterpret_cast<const char*>(args.m) + zero);
     }
     NewtonRows nr;
-    assemble<SO100_SOLVER_NEWTON, true, kDebug, !kDebug && kWaves == 2>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r,
-                                                                        mscale, fscale, sub, nr);
+    assemble<SO100_SOLVER_NEWTON, true, kDebug>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale,
+                                                fscale, sub, nr);
     TL_MARK(0);
     NewtonDiag diag;
     const bool dbg = kDebug && args.b.debug && sub == nsub - 1;
