@@ -92,6 +92,17 @@ DEV float bcast_row(float v, int j) {
 DEV float4 bcast_row4(float4 v, int j) {
   return make_float4(bcast_row(v.x, j), bcast_row(v.y, j), bcast_row(v.z, j), bcast_row(v.w, j));
 }
+// ds_bpermute byte address of lane src (0..15) of this lane's 16-lane row.  The lane id comes from an opaque
+// v_mbcnt pair at each use: __shfl's own lane id is computed once per kernel and, held across the narrowphase and
+// the solve, was a spilled value reloaded inside their loops (3-wave build)
+DEV int row_lane_addr(int src) {
+  int t;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(t));
+  return ((t & ~15) | (src & 15)) << 2;
+}
+DEV float shfl_at(float v, int addr) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+}
 DEV float bcast16(float v, int src) { return __shfl(v, src, kLanes); }
 DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }
 

@@ -500,11 +500,11 @@ DEV bool gjk_simplex(GjkPt* S, int& n, float* d) {
   return false;
 }
 
-// GJK (oracle gjk): true when A - B encloses the origin, S then holds the enclosing tetrahedron
-// dsep: (the unit direction, 1) when the support test proved the pair separated, else w = 0 (so100_convex.h
-// mpr_contacts' separating-direction cache)
-DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, int lane, float4& dsep) {
-  dsep = make_float4(0.f, 0.f, 0.f, 0.f);
+// GJK (oracle gjk): true when A - B encloses the origin, S then holds the enclosing tetrahedron.
+// sc: the pair's entry of mpr_contacts' separating-direction cache, set to (the unit direction, 1) when the support
+// test proves the pair separated (stored here: a direction returned to the caller was a value live across EPA,
+// spilled in the 3-wave build)
+DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, int lane, float4* sc) {
   float d[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) d[k] = o.hc[k] - o.c1[k];
@@ -522,7 +522,7 @@ DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, 
     for (int k = 0; k < 3; k++) a.v[k] = as.v[k];
     a.id = as.id;
     if (dot3(a.v, du) <= 0.f) {
-      dsep = make_float4(du[0], du[1], du[2], 1.f);
+      if (lane == 0) *sc = make_float4(du[0], du[1], du[2], 1.f);
       return false;
     }
 #pragma unroll
@@ -534,19 +534,21 @@ DEV bool gjk_enclose(const DevModel* __restrict__ m, const MprObj& o, GjkPt* S, 
   return false;
 }
 
-// a facet (a, b, c) of the polytope into slot f (oracle epa_face_set); false for a degenerate triangle
+// a facet (a, b, c) of the polytope into slot f (oracle epa_face_set); false for a degenerate triangle (its slot
+// is then written anyway, unused: the caller abandons the polytope; no branch, so the initial tetrahedron's 4
+// facets are straight-line code)
 DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const float* A, const float* B, const float* C) {
   float ab[3], ac[3], n[3];
   sub3(ab, B, A);
   sub3(ac, C, A);
   cross3(n, ab, ac);
   const float l2 = dot3(n, n);
-  if (l2 < kCcdEps * kCcdEps) return false;       // ccd_zero(|n|)
+  const bool good = l2 >= kCcdEps * kCcdEps;      // !ccd_zero(|n|)
   const float il = __builtin_amdgcn_rsqf(l2);     // 1 / |n| (oracle epa_face_set: one division), v_rsq
   n[0] = n[0] * il; n[1] = n[1] * il; n[2] = n[2] * il;
   P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A));
   P.fv[f] = (uint32_t)a | (uint32_t)b << 5 | (uint32_t)c << 10;
-  return true;
+  return good;
 }
 
 // The polytope's vertex positions (the Minkowski-difference points) across the row's lanes: vertex i on lane
@@ -595,7 +597,7 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
       pt_sel(B, C, flip);
       pt_sel(C, Bt, flip);
       const int bb = flip ? c : b, cc = flip ? b : c;
-      ok = ok && epa_face_set(P, i, a, bb, cc, A.v, B.v, C.v);
+      ok = epa_face_set(P, i, a, bb, cc, A.v, B.v, C.v) && ok;
       alive |= 1ull << i;
     }
 #pragma unroll
@@ -703,10 +705,10 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
 #pragma unroll
       for (int q = 0; q < 3; q++) {
         const int vi = (int)((mfv[s3] >> (5 * q)) & 31u);
-        const int src = vi & 15;
-        const float x0 = __shfl(V.x[0], src, kLanes), x1 = __shfl(V.x[1], src, kLanes);
-        const float y0 = __shfl(V.y[0], src, kLanes), y1 = __shfl(V.y[1], src, kLanes);
-        const float z0 = __shfl(V.z[0], src, kLanes), z1 = __shfl(V.z[1], src, kLanes);
+        const int src = row_lane_addr(vi);
+        const float x0 = shfl_at(V.x[0], src), x1 = shfl_at(V.x[1], src);
+        const float y0 = shfl_at(V.y[0], src), y1 = shfl_at(V.y[1], src);
+        const float z0 = shfl_at(V.z[0], src), z1 = shfl_at(V.z[1], src);
         pv[q][0] = vi >= 16 ? x1 : x0; pv[q][1] = vi >= 16 ? y1 : y0; pv[q][2] = vi >= 16 ? z1 : z0;
       }
       float4 fpl[3];
@@ -801,8 +803,7 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
 
 // the mesh pairs' collider of the model (so100_model.convex): GJK + EPA (MuJoCo 3.3.3's default) or MPR
 DEV bool convex_penetration(const DevModel* __restrict__ m, const MprObj& o, float& depth, float* dir, float* pos,
-                            EpaPoly& P, int lane, int grp, float4& dsep) {
-  dsep = make_float4(0.f, 0.f, 0.f, 0.f);
+                            EpaPoly& P, int lane, int grp, float4* sc) {
   if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(m, o, depth, dir, pos, lane);
   GjkPt S[4];
 #pragma unroll
@@ -813,7 +814,7 @@ DEV bool convex_penetration(const DevModel* __restrict__ m, const MprObj& o, flo
   }
   const unsigned long long gt0 = ESTAMP_T();
   ESTAMP_ADD(2, 1);
-  const bool enc = gjk_enclose(m, o, S, lane, dsep);
+  const bool enc = gjk_enclose(m, o, S, lane, sc);
   const unsigned long long gt1 = ESTAMP_T();
   ESTAMP_ADD(0, gt1 - gt0);
   if (!enc) return false;
@@ -1199,9 +1200,8 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
         proved = dot3(as.v, du) < -kSepTol;
       }
       if (!proved) {
-        float4 dsep;
-        hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp, dsep);
-        if (lane == 0) *sc = dsep;
+        if (lane == 0 && c.w != 0.f) sc->w = 0.f;   // stale: invalidated (GJK stores a new one if it separates)
+        hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp, sc);
       }
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first

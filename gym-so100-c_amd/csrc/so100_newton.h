@@ -197,7 +197,8 @@ DEV float4 jx_own(const NewtonRows& r, int c, int lane) {
 }
 // lane src of this lane's 16-lane row, src not a compile-time constant (ds_bpermute)
 DEV float4 shfl_row4(float4 v, int src) {
-  return make_float4(__shfl(v.x, src, kLanes), __shfl(v.y, src, kLanes), __shfl(v.z, src, kLanes), __shfl(v.w, src, kLanes));
+  const int a = row_lane_addr(src);
+  return make_float4(shfl_at(v.x, a), shfl_at(v.y, a), shfl_at(v.z, a), shfl_at(v.w, a));
 }
 // contact c's J x (4 rows) on lane c (the contacts present anywhere in the wave)
 DEV float4 contact_rows(const NewtonRows& rw, float x, int lane, int ncon_max) {
@@ -539,7 +540,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
         for (int c = kJReg; c < ncon_max && c < kMaxCon; c++) {       // J from LDS: one broadcast read per dof
           float hb[10];
 #pragma unroll
-          for (int k = 0; k < 10; k++) hb[k] = __shfl(hc[k], c, kLanes);
+          for (int k = 0, a = row_lane_addr(c); k < 10; k++) hb[k] = shfl_at(hc[k], a);
           const float4* jc_l = r.jx + (c - kJReg) * SO100_NV;
           const float4 w = sym4(hb, jx_own(r, c, lane));
 #pragma unroll
@@ -566,7 +567,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
               float hb[10];
 #pragma unroll
-              for (int t = 0; t < 10; t++) hb[t] = __shfl(ho[t], k, kLanes);
+              for (int t = 0, a = row_lane_addr(k); t < 10; t++) hb[t] = shfl_at(ho[t], a);
               const float4 w = sym4(hb, ovf_j(crec, b0 + k, lane, ncon));
               const bool live = b0 + k < ncon;          // this env's contact (else J is 0)
               const float4* jrow = reinterpret_cast<const float4*>(crec + (size_t)(b0 + k) * kConStride + kJOff);

@@ -1379,9 +1379,12 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, i
       a.w.order = nullptr;
     }
     const int build = fused_build(n, waves, b.debug != nullptr);
+#ifndef SO100_RU_FUSED3_ONLY   // (Makefile ru3: only the 3-wave product build, for register-allocation work)
     if (build == 1) hipLaunchKernelGGL(so100_fused_kernel<true>, grid, dim3(kThreads), 0, s, m, a);
     else if (build == 2) hipLaunchKernelGGL((so100_fused_kernel<false, 2>), grid, dim3(kThreads), 0, s, m, a);
-    else hipLaunchKernelGGL((so100_fused_kernel<false, 3>), grid, dim3(kThreads), 0, s, m, a);
+    else
+#endif
+    hipLaunchKernelGGL((so100_fused_kernel<false, 3>), grid, dim3(kThreads), 0, s, m, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[k++], s);
@@ -1391,6 +1394,9 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, i
   for (int sub = 0; sub <= nsubstep; sub++) {
     a.sub = sub;
     a.par = (int)(w.sub_count & 1u);
+#ifdef SO100_RU_FUSED3_ONLY
+    if (false) {
+#else
     if (solver == SO100_SOLVER_NEWTON) {
       if (sub == 0) hipLaunchKernelGGL((so100_stage_kernel<0, SO100_SOLVER_NEWTON>), grid, dim3(kThreads), 0, s, a);
       else if (sub < nsubstep) hipLaunchKernelGGL((so100_stage_kernel<1, SO100_SOLVER_NEWTON>), grid, dim3(kThreads), 0, s, a);
@@ -1399,6 +1405,7 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, i
       if (sub == 0) hipLaunchKernelGGL((so100_stage_kernel<0, SO100_SOLVER_PGS>), grid, dim3(kThreads), 0, s, a);
       else if (sub < nsubstep) hipLaunchKernelGGL((so100_stage_kernel<1, SO100_SOLVER_PGS>), grid, dim3(kThreads), 0, s, a);
       else hipLaunchKernelGGL((so100_stage_kernel<2, SO100_SOLVER_PGS>), grid, dim3(kThreads), 0, s, a);
+#endif
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
