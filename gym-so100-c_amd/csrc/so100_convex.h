@@ -543,7 +543,7 @@ DEV bool epa_face_set(EpaPoly& P, int f, int a, int b, int c, const float* A, co
   sub3(ac, C, A);
   cross3(n, ab, ac);
   const float l2 = dot3(n, n);
-  const bool good = l2 >= kCcdEps * kCcdEps;      // !ccd_zero(|n|)
+  const bool good = l2 >= kCcdEps * kCcdEps;      // !ccd_zero(|n|) (a NaN facet, from NaN points, also fails)
   const float il = __builtin_amdgcn_rsqf(l2);     // 1 / |n| (oracle epa_face_set: one division), v_rsq
   n[0] = n[0] * il; n[1] = n[1] * il; n[2] = n[2] * il;
   P.plane[f] = make_float4(n[0], n[1], n[2], dot3(n, A));
