@@ -122,18 +122,21 @@ def cpu_baseline(seconds, solver="newton"):
                     "matrices), not MuJoCo; a non-target baseline"}
 
 
-def load_step_traffic(n_envs, mode, solver):
+def load_step_traffic(n_envs, mode, solver, lib_hash):
     """The committed rocprofv3 PMC measurement of one env step's HBM traffic at this size and step mode
     (profiles/r<NN>_pmc_step_*.json, the newest round's, tools/gpurun/pmc_step_traffic.py: FETCH_SIZE and WRITE_SIZE
-    passes, summed over every kernel of a step), or None."""
-    for rnd in ("r04", "r03"):
+    passes, summed over every kernel of a step) and whether it measured these kernels: the file records the
+    so100_source_hash of the library it profiled, and traffic is reported only when that equals the loaded
+    library's (a profile of older kernels is named in pmc_source but never quoted as traffic)."""
+    for rnd in ("r05", "r04", "r03"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_step_{mode}_{solver}_{n_envs}.json")
         if os.path.exists(path):
             try:
-                return json.load(open(path))
+                pmc = json.load(open(path))
             except ValueError:
-                return None
-    return None
+                return None, False
+            return pmc, pmc.get("lib_source_hash") == lib_hash
+    return None, False
 
 
 def main(argv=None):
@@ -207,8 +210,8 @@ def main(argv=None):
         s_ms, s_n, t_ms, t_n = env.profile_read()
         env.profile_enable(0)
         solver_ms, stage_ms = s_ms / max(s_n, 1), t_ms / max(t_n, 1)
-    # untimed: contacts per env per solver launch (the split record bytes) and contacts the 16-per-env cap
-    # dropped (MuJoCo has no cap)
+    # untimed: contacts per env per solver launch (the split record bytes) and contacts left out of an env's list
+    # (a checked invariant: the list holds every contact since round 4, so this is 0)
     accum = torch.zeros(1, dtype=torch.int64, device=dev)
     dropped = torch.zeros(1, dtype=torch.int64, device=dev)
     for i in range(args.contact_steps):
@@ -246,15 +249,18 @@ def main(argv=None):
         # launch, or a split step's 21 launches per chunk with the chunks joined back to this stream)
         per_gpu_rate = count / (step_ms * 1e-3)
         achieved = per_gpu_rate * bpe
-        pmc = load_step_traffic(count, mode, args.solver)
-        traffic = pmc["hbm_bytes_per_step"] / count if pmc else None      # per env step, like achieved
+        from gym_so100 import _native
+        lib_hash = _native.source_hash()
+        pmc, pmc_current = load_step_traffic(count, mode, args.solver, lib_hash)
+        # per env step, like achieved; null unless the profile measured these kernels (the same source hash)
+        traffic = pmc["hbm_bytes_per_step"] / count if (pmc and pmc_current) else None
         if fused:
             rec_per_launch = None
         else:
             per_env, per_con = ((PGS_RECORD_BYTES_PER_ENV, PGS_RECORD_BYTES_PER_CONTACT) if args.solver == "pgs" else
                                 (NEWTON_RECORD_BYTES_PER_ENV, NEWTON_RECORD_BYTES_PER_CONTACT))
             rec_per_launch = n0 * (per_env + per_con * contacts_per_env)
-        valu_insts = pmc.get("valu_insts_per_step") if pmc else None
+        valu_insts = pmc.get("valu_insts_per_step") if (pmc and pmc_current) else None
         valu_busy = valu_insts * 2.0 / (step_ms * 1e-3 * CLOCK_HZ * SIMDS) if valu_insts else None
         line = {
             "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
@@ -276,6 +282,9 @@ def main(argv=None):
                                    f"split step: stage + so100_{args.solver}_kernel x 10 + final stage, {nchunks} chunks",
                          "traffic_over_algorithmic": (traffic / bpe) if traffic else None,
                          "pmc_source": pmc.get("file") if pmc else None,
+                         "pmc_source_hash": pmc.get("lib_source_hash") if pmc else None,
+                         "lib_source_hash": lib_hash,
+                         "pmc_matches_lib": bool(pmc and pmc_current),
                          "valu_busy": valu_busy,
                          "solver_kernel_ms": None if fused else solver_ms,
                          "stage_kernel_ms": None if fused else stage_ms,

@@ -68,9 +68,11 @@ DEV void col3(float* o, const float* R, int c) {          // column c of a row-m
   for (int t = 0; t < 3; t++) o[t] = R[3 * t] * w[0] + R[3 * t + 1] * w[1] + R[3 * t + 2] * w[2];
 }
 
-// collapse: the pair is the cube against the table's mesh, one contact (MuJoCo's convex collider; the oracle's
-// collide_box_pair): the mean of the kept points' positions and the deepest distance, summed in clip order as
-// the kept points would be, without their compaction and 8-slot output (bitwise the same contact)
+// collapse: the pair is a box (the cube, a finger pad) against the table's mesh, one contact (MuJoCo's convex
+// collider; the oracle's collide_box_pair): the exact separating-axis minimum over all 15 axes (no face preference
+// for the edge axes: the convex collider's minimum penetration), the mean of the kept points' positions and the
+// deepest distance, summed in clip order as the kept points would be, without their compaction and 8-slot output
+// (bitwise the same contact)
 DEV void box_box(const float* p1, const float* R1, const float* A, const float* p2, const float* R2,
                  const float* B, float margin, PairContacts& out, bool collapse) {
   out.n = 0;
@@ -86,6 +88,7 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
   float best = -1e30f, nb[3] = {0, 0, 0};
   int code = 0;
   bool invert = false;
+  const float ebias = collapse ? 1.f : 1.05f;      // mjc_BoxBox prefers faces unless an edge axis is clearly better
 #pragma unroll
   for (int i = 0; i < 3; i++) {
     float s = fabsf(pp[i]) - (A[i] + B[0] * Q[3 * i] + B[1] * Q[3 * i + 1] + B[2] * Q[3 * i + 2]);
@@ -115,7 +118,7 @@ DEV void box_box(const float* p1, const float* R1, const float* A, const float* 
       float ex = A[i1] * Q[3 * i2 + j] + A[i2] * Q[3 * i1 + j] + B[j1] * Q[3 * i + j2] + B[j2] * Q[3 * i + j1];
       float s = (fabsf(e) - ex) * linv;
       if (s > margin) return;
-      if (s * 1.05f > best) {
+      if (s * ebias > best) {
         best = s; code = 7 + 3 * i + j; invert = e < 0;
         nb[0] = n[0] * linv; nb[1] = n[1] * linv; nb[2] = n[2] * linv;
       }
@@ -347,38 +350,58 @@ DEV void collide_pair(const DevModel* __restrict__ m, const EnvShared& sh, int p
   float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   const float margin = m->pair_margin[p];
   if (sqrtf(dot3(d, d)) > sqrtf(dot3(A, A)) + sqrtf(dot3(B, B)) + margin) return;
-  // the cube against the table's mesh (geom2 = geom 0): MuJoCo's convex collider, one contact per pair (the
-  // oracle's collide_box_pair): the SAT normal, the deepest distance, the mean of the clipped positions
+  // a box (the cube, a finger pad) against the table's mesh (geom2 = geom 0): MuJoCo's convex collider, one contact
+  // per pair (the oracle's collide_box_pair): the SAT normal, the deepest distance, the mean of the clipped positions
   box_box(p1, R1, A, p2, R2, B, margin, pc, g2 == 0);
 }
 
-// Arm/jaw hulls vs the table top (pairs SO100_NPAIR_BOX + k; oracle collision()): hull k's lowest
-// vertex inside the top face's x-y footprint, a contact when it is below the top.
-//  * broadphase, in parallel: lane k < SO100_NHULL of each env tests hull k's body-frame bounding box
-//    against the top; only hulls that are candidates in some env of the wave are scanned;
-//  * scan: the 16 lanes of the env's row split the vertices (lane, lane + 16, ...) and a 16-lane
-//    lexicographic (z, vertex index) min gives the oracle's first lowest vertex.
-// Needs the link frames of fk_stage (sh.ser.xm / xp).  Lane k < SO100_NHULL returns hull k's contact
-// flag and its lowest vertex.
+// Arm/jaw hulls vs the table (pairs SO100_NPAIR_BOX + k; oracle table_hull_fast).  The table is a mesh, so MuJoCo
+// collides it through its convex collider: the minimum penetration.  Lane k < SO100_NHULL classifies hull k from its
+// body-frame bounding box (world z extent ez, x-y extents ex, ey about the box centre c):
+//  * candidate: the box's lowest point zb = c.z - ez below top + margin (else separated);
+//  * top-face rule (fast): with D = top - zb (>= the hull's depth below the top), every vertex lies inside the top
+//    face's footprint shrunk by D (c.x - ex >= lo.x + D, ...) and the hull's centroid (model constant, inside the
+//    hull) is at least D above the table's bottom.  Then the minimum penetration is exactly the depth d of the lowest
+//    vertex along +z: lifting by d separates, and any shorter translation leaves a point of the hull inside the
+//    table box.  The contact: the lowest vertex (first in hull order among ties) and its projection on the top;
+//  * otherwise (at the table's edges and side faces, or deep): the convex collider (mpr_contacts' slow items).
+// Returns the classification bits of lane k: 1 = candidate, 2 = top-face rule.
+DEV int table_hull_class(const DevModel* __restrict__ m, const EnvShared& sh, int lane, bool valid) {
+  if (!valid || lane >= SO100_NHULL) return 0;
+  const int a = m->hull_body[lane] - 2;
+  const float4 hc = reinterpret_cast<const float4*>(m->hull_center)[lane];
+  const float4 hh = reinterpret_cast<const float4*>(m->hull_half)[lane];
+  const float4 hg = reinterpret_cast<const float4*>(m->hull_centroid)[lane];
+  const float* R = sh.ser.xm[a];
+  const float* P = sh.ser.xp[a];
+  const float top = m->table_top;
+  const float cz = (R[6] * hc.x + R[7] * hc.y + R[8] * hc.z) + P[2];
+  const float ez = fabsf(R[6]) * hh.x + fabsf(R[7]) * hh.y + fabsf(R[8]) * hh.z;
+  if (!(cz - ez < top + m->pair_margin[SO100_NPAIR_BOX + lane])) return 0;
+  const float cx = (R[0] * hc.x + R[1] * hc.y + R[2] * hc.z) + P[0];
+  const float cy = (R[3] * hc.x + R[4] * hc.y + R[5] * hc.z) + P[1];
+  const float ex = fabsf(R[0]) * hh.x + fabsf(R[1]) * hh.y + fabsf(R[2]) * hh.z;
+  const float ey = fabsf(R[3]) * hh.x + fabsf(R[4]) * hh.y + fabsf(R[5]) * hh.z;
+  const float gz = (R[6] * hg.x + R[7] * hg.y + R[8] * hg.z) + P[2];
+  const float D = top - (cz - ez);
+  const bool fast = cx - ex >= m->table_lo[0] + D && cx + ex <= m->table_hi[0] - D && cy - ey >= m->table_lo[1] + D &&
+                    cy + ey <= m->table_hi[1] - D && gz - m->table_bottom >= D;
+  return fast ? 3 : 1;
+}
+
+// The top-face rule's contacts: for the hulls table_hull_class puts under it in some env of the wave, the env's 16
+// lanes split the vertices (lane, lane + 16, ...) and a 16-lane lexicographic (z, vertex index) min gives the
+// oracle's first lowest vertex.  Needs the link frames of fk_stage (sh.ser.xm / xp).  Lane k < SO100_NHULL returns
+// hull k's contact flag (its lowest vertex below top + margin) and its lowest vertex.
 DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lane, int grp, bool valid, float& hx,
                     float& hy, float& hz) {
   bool found = false;
   hx = hy = hz = 0.f;
   const float top = m->table_top;
-  bool cand = false;
-  if (valid && lane < SO100_NHULL) {
-    const int a = m->hull_body[lane] - 2;
-    const float4 hc = reinterpret_cast<const float4*>(m->hull_center)[lane];
-    const float4 hh = reinterpret_cast<const float4*>(m->hull_half)[lane];
-    const float r6 = sh.ser.xm[a][6], r7 = sh.ser.xm[a][7], r8 = sh.ser.xm[a][8];
-    const float cz = (r6 * hc.x + r7 * hc.y + r8 * hc.z) + sh.ser.xp[a][2];
-    const float ext = fabsf(r6) * hh.x + fabsf(r7) * hh.y + fabsf(r8) * hh.z;
-    cand = cz - ext < top + m->pair_margin[SO100_NPAIR_BOX + lane];
-  }
+  const bool cand = table_hull_class(m, sh, lane, valid) == 3;
   const uint64_t cm = __ballot(cand);
   const uint32_t env_cand = (uint32_t)(cm >> (grp * 16)) & 0xFFFFu;
   uint32_t wave_cand = (uint32_t)((cm | (cm >> 16) | (cm >> 32) | (cm >> 48)) & 0xFFFFull);
-  const float lo0 = m->table_lo[0], lo1 = m->table_lo[1], hi0 = m->table_hi[0], hi1 = m->table_hi[1];
   const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert);
   while (wave_cand) {
     const int k = __builtin_ctz(wave_cand);
@@ -398,8 +421,7 @@ DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lan
         const float wx = (r0 * v.x + r1 * v.y + r2 * v.z) + p0;
         const float wy = (r3 * v.x + r4 * v.y + r5 * v.z) + p1;
         const float wz = (r6 * v.x + r7 * v.y + r8 * v.z) + p2;
-        const bool in = wx >= lo0 && wx <= hi0 && wy >= lo1 && wy <= hi1;
-        if (in && wz < bz) { bz = wz; bx = wx; by = wy; bi = i; }
+        if (wz < bz) { bz = wz; bx = wx; by = wy; bi = i; }
       }
     }
     arg_best16<true>(bz, bi, bx, by, bz);   // the score is the point's z (passed as both)

@@ -285,10 +285,20 @@ int build_device_model(const so100_model* s, DevModel* d) {
   if (s->site_ee_body != 6 || s->site_cube_body != SO100_CUBE_BODY) return fail("model: unexpected site bodies");
   for (int p = 0; p < SO100_NPAIR_BOX; p++)
     if (s->pair_condim[p] != 4) return fail("model: box-box pairs must have condim 4");
+  if (s->geom_body[0] != 0 || fabs(s->geom_pos[0][2] + s->geom_size[0][2] - s->table_top) > 1e-9 ||
+      fabs(s->geom_pos[0][0] - s->geom_size[0][0] - s->table_lo[0]) > 1e-6 ||
+      fabs(s->geom_pos[0][0] + s->geom_size[0][0] - s->table_hi[0]) > 1e-6 ||
+      fabs(s->geom_pos[0][1] - s->geom_size[0][1] - s->table_lo[1]) > 1e-6 ||
+      fabs(s->geom_pos[0][1] + s->geom_size[0][1] - s->table_hi[1]) > 1e-6 || fabs(s->geom_quat[0][0] - 1) > 1e-12)
+    return fail("model: geom 0 must be the table box, its top face table_top over table_lo..table_hi");
   for (int p = SO100_NPAIR_BOX; p < SO100_PAIR_MPR0; p++) {
     const int k = p - SO100_NPAIR_BOX;
     if (s->pair_condim[p] != 3 && s->pair_condim[p] != 4) return fail("model: hull pairs must have condim 3 or 4");
     if (s->pair_body1[p] != 0 || s->pair_body2[p] != s->hull_body[k]) return fail("model: hull pair k must be (table, hull k)");
+    // the table is geom 0, a box (its mesh is an exact box) whose top face is table_top: the convex collider takes
+    // it as obj1 (mpr_obj_setup's static box), the top-face rule as its top face and bottom
+    if (s->pair_geom1[p] != 0 || s->pair_geom2[p] != -1 - k) return fail("model: hull pair k must be (geom 0 = the table, hull k)");
+    if (s->pair_margin[p] != 0) return fail("model: table-hull pairs take no margin");
     if (s->hull_body[k] < 2 || s->hull_body[k] > 7) return fail("model: hulls must sit on arm bodies 2..7");
     if (s->hull_start[k] < 0 || s->hull_count[k] < 1 || s->hull_start[k] + s->hull_count[k] > SO100_HULL_NVERT)
       return fail("model: hull vertex range out of bounds");
@@ -520,6 +530,7 @@ int build_device_model(const so100_model* s, DevModel* d) {
   for (int v = 0; v < SO100_HULL_NVERT; v++)
     d->hull_vert[v] = {(float)s->hull_vert[v][0], (float)s->hull_vert[v][1], (float)s->hull_vert[v][2], 0.f};
   d->table_top = (float)s->table_top;
+  d->table_bottom = (float)(s->table_top - 2 * s->geom_size[0][2]);
   for (int k = 0; k < 2; k++) {
     d->table_lo[k] = (float)s->table_lo[k];
     d->table_hi[k] = (float)s->table_hi[k];
@@ -1131,6 +1142,12 @@ int so100_abi_version(void) {
 }
 
 const char* so100_last_error(void) { return so100_last_error_impl(); }
+
+#ifndef SO100_SRC_HASH
+#define SO100_SRC_HASH "unknown"
+#endif
+// the Makefile's content hash of the sources this library was built from (ABI 16)
+const char* so100_source_hash(void) { return SO100_SRC_HASH; }
 
 int so100_hull_cells(const so100_model* model, uint32_t* cells, float* cand, int cap) {
   try {

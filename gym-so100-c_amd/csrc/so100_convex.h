@@ -34,12 +34,13 @@ struct MprObj {
 };
 constexpr float kCcdEps = 2.220446049250313e-16f;   // MuJoCo's double libccd CCD_EPS (absolute tests: see oracle)
 constexpr float kMprTol = 1e-6f;            // MuJoCo ccd_tolerance
-constexpr float kSepTol = 1e-6f;
+constexpr float kSepTol = 1e-6f;            // a cached separating direction must clear the pair by 1 um (mpr_contacts;
+                                            // oracle SEP_TOL)
 // EPA: a facet is visible from the new support point only when the point clears its plane by more than this (the
 // ccd_tolerance; oracle EPA_VISTOL): a point on a facet's plane within fp32 rounding is not "visible", so no facet is
 // built folding back over a coplanar one (an inverted facet, negative distance, that derailed fp32 EPA on face-face
 // hull contacts: DESIGN.md §4 deviation 7)
-constexpr float kEpaVisTol = 1e-6f;            // a cached separating direction must clear the pair by 1 um (mpr_contacts)
+constexpr float kEpaVisTol = 1e-6f;
 constexpr int kMprIters = 50;               // MuJoCo ccd_iterations
 
 DEV bool ccd_zero(float x) { return fabsf(x) < kCcdEps; }
@@ -841,8 +842,9 @@ DEV void hull_frame(const DevModel* __restrict__ m, const EnvShared& sh, int b, 
   }
 }
 
-// Convex pair p (23..142): obj1 = box geom (cube, bin box, finger pad) or hull k1 (self-collision, the Base), obj2 = hull k, both
-// in hull k's body frame H.  Oracle collision().
+// Convex pair p (23..151; 14..22 outside the top-face rule): obj1 = box geom (cube, bin box, finger pad, the marker,
+// the table: geom 0, a static box) or hull k1 (self-collision, the Base), obj2 = hull k, both in hull k's body frame H.
+// Oracle convex_pair.
 DEV void mpr_obj_setup(const DevModel* __restrict__ m, const EnvShared& sh, int p, MprObj& o) {
   const int g = m->pair_g1[p], k = -1 - m->pair_g2[p];
   float RH[9], pH[3];
@@ -1055,8 +1057,12 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
   // each env's candidates go to its dynamics scratch (RNE cdd + tau: dead from the collision on; the contact
   // area holds the rows' EPA polytopes)
-  static_assert(kConvex + SO100_NPAIR_MOCAPHULL <= (int)(sizeof(shm[0].ser.cdd) + sizeof(shm[0].ser.tau)),
-                "an env's candidate list fits");
+  // list items: q < kConvex the wave-shared pairs SO100_PAIR_MPR0 + q, then the EE marker's 9 (pairs 143..151), then
+  // the slow table-hull pairs (kTableItem0 + k: pair SO100_NPAIR_BOX + k)
+  constexpr int kTableItem0 = kConvex + SO100_NPAIR_MOCAPHULL;
+  constexpr int kItems = kTableItem0 + SO100_NHULL;
+  static_assert(kItems <= kSepPairs, "a separating-direction slot per item");
+  static_assert(kItems <= (int)(sizeof(shm[0].ser.cdd) + sizeof(shm[0].ser.tau)), "an env's candidate list fits");
   static_assert(SO100_PAIR_MOCAPHULL0 == SO100_PAIR_MPR0 + kConvex, "the marker pairs follow the wave-shared pairs");
   static_assert(__builtin_offsetof(SerialScratch, cdd) >= sizeof(ConArea), "the candidate lists do not alias the contact area");
   // the sphere table and the sphere survivors' list in the env's MPR staging area
@@ -1097,7 +1103,11 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
   const int s2c = __builtin_amdgcn_readlane(scnt, 32), s3c = __builtin_amdgcn_readlane(scnt, 48);
   const int spre1 = s0c, spre2 = s0c + s1c, spre3 = s0c + s1c + s2c, stotal = spre3 + s3c;
   const bool ee = m->ee;
-  if (stotal == 0 && !ee) return 0;
+  // the table-hull pairs outside the top-face rule (table_hull_class: at the table's edges and side faces, or deep):
+  // lane k < SO100_NHULL of each env, appended to the env's list after the other convex pairs (items kTableItem0 + k)
+  const bool tslow = table_hull_class(m, sh, lane, valid) == 1;
+  const bool anyslow = __ballot(tslow) != 0ull;
+  if (stotal == 0 && !ee && !anyslow) return 0;
   {
     uint8_t* slist = reinterpret_cast<uint8_t*>(&shm[grp].mpr[0]) + kSphObj * sizeof(float4);
 #pragma unroll
@@ -1161,11 +1171,32 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     c0 += __popcll(mb & 0xFFFFull); c1 += __popcll(mb & (0xFFFFull << 16));
     c2 += __popcll(mb & (0xFFFFull << 32)); c3 += __popcll(mb & (0xFFFFull << 48));
   }
+  if (anyslow) {
+    // the slow table-hull pairs (14..22): both broadphase stages on lanes 0..8 of the env's own row (the table box
+    // as obj1, as the bin boxes), the survivors appended to its list in hull order
+    bool cand = false;
+    if (tslow) {
+      const int p = SO100_NPAIR_BOX + lane;
+      if (mpr_sphere(m, sh, p)) {
+        MprObj o;
+        mpr_obj_setup(m, sh, p, o);
+        cand = mpr_broadphase(m, o, lane);
+      }
+    }
+    const uint64_t mb = __ballot(cand);
+    if (cand) {
+      const int base = grp == 0 ? c0 : grp == 1 ? c1 : grp == 2 ? c2 : c3;
+      const uint32_t row = (uint32_t)((mb >> (grp * 16)) & 0xFFFFull);
+      reinterpret_cast<uint8_t*>(&shm[grp].ser.cdd[0][0])[base + __popc(row & ((1u << lane) - 1u))] = (uint8_t)(kTableItem0 + lane);
+    }
+    c0 += __popcll(mb & 0xFFFFull); c1 += __popcll(mb & (0xFFFFull << 16));
+    c2 += __popcll(mb & (0xFFFFull << 32)); c3 += __popcll(mb & (0xFFFFull << 48));
+  }
   const int total = c0 + c1 + c2 + c3;
   if (total == 0) return 0;
   // the list's env offsets (pre_1..3 <= 3 x 129) and the envs' staged counts (<= 129 each) packed into one word each:
   // wave-uniform values held across the narrowphase's register peak (4 + 3 separate ones were spilled)
-  static_assert(3 * (kConvex + SO100_NPAIR_MOCAPHULL) < 1024 && kConvex + SO100_NPAIR_MOCAPHULL < 256, "packed counts");
+  static_assert(3 * kItems < 1024 && kItems < 256, "packed counts");
   const uint32_t prepk = (uint32_t)c0 | (uint32_t)(c0 + c1) << 10 | (uint32_t)(c0 + c1 + c2) << 20;
   __syncthreads();
   uint32_t fpk = 0u;                            // staged contacts of env e in byte e (wave-uniform)
@@ -1181,7 +1212,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     int p = SO100_PAIR_MPR0;
     if (act) {
       const int q = reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_of(ie)];
-      p = SO100_PAIR_MPR0 + q;
+      p = q < kTableItem0 ? SO100_PAIR_MPR0 + q : SO100_NPAIR_BOX + (q - kTableItem0);
       MprObj o;
       mpr_obj_setup(m, shm[ie], p, o);
       o.cells = kCells;

@@ -93,6 +93,7 @@ struct DevModel {
   // with their last candidate): a row loads its cell's candidates with one load issued beside the cell entry's
   const float4_t* hull_blk;
   float table_top, table_lo[2], table_hi[2];
+  float table_bottom;               // the table box's bottom face (table_top - 2 x its half thickness)
 
   // sites
   float site_cube[3];               // cube body frame
@@ -151,7 +152,7 @@ constexpr int kOvfJc = 12, kOvfJs = 16, kOvfF = 20;   // Newton overflow state (
 constexpr int kMprStageOff = 24;            // convex-collider staging (MprStage) of staged contacts >= kMaxCon
 constexpr size_t kConEnv = (size_t)kConCap * kConStride;   // floats per env
 // the convex pairs' separating-direction cache (so100_convex.h mpr_contacts): one float4 per (env, convex pair)
-constexpr int kSepPairs = 132;   // >= the 129 convex pairs (120 wave-shared + the EE marker's 9)
+constexpr int kSepPairs = 140;   // >= the 138 convex items (120 wave-shared pairs, the EE marker's 9, the 9 table hulls)
 enum HdrField : int {
   H_QACC = 0,       // qacc at the solver start (qacc_smooth, plus M^-1 J' f of the kept warmstart)
   H_FRAREF = 3,     // frictionloss rows: aref = -B vel

@@ -247,25 +247,26 @@ DEV void put_box_contacts(EnvShared& sh, float* crec, const PairContacts& pc, in
   }
 }
 
-// Finger pads vs the table and the bin boxes (oracle collision(): pad_table, collide_box_pair).
-//   pairs 152..159 (pad i, table), lane i: the hull-table rule on the pad's 8 corners — the corners inside
-//     the top face's footprint and below the top count; one contact at the deepest corner's distance, at
-//     the counted corners' x-y centroid, midway in z between the deepest corner and the top; normal -z;
-//   pairs 160..199 (pad i, bin box j): a conservative test (the pad's bounding sphere against the static
-//     box, 3 pairs per lane), the candidates compacted in pair order and run through the box-box
-//     collider 16 at a time (a wave runs as many rounds as its busiest env needs; usually none);
-//   (EE variant) pairs 200..208 (cube | pad i, the mocap marker box) join the pad-bin candidates.
+// Finger pads vs the table and the bin boxes (oracle collision(): collide_box_pair), one candidate list in pair
+// order, run through the box-box collider 16 at a time (a wave runs as many rounds as its busiest env needs):
+//   pairs 152..159 (pad i, table): a box against the table mesh, the cube-table rule (the exact separating-axis
+//     minimum penetration, one contact: collide_pair's collapse); candidate when the pad's lowest point (its centre
+//     z minus its half extent along world z) is within 1e-4 of top + margin (else the table's z axis separates);
+//   pairs 160..199 (pad i, bin box j): a conservative test (the pad's bounding sphere against the static box, 3
+//     pairs per lane), behind a wave-uniform prefilter (no pad near the bin's AABB: no candidates);
+//   (EE variant) pairs 200..208 (cube | pad i, the mocap marker box) join the candidates.
 // Contacts are appended after `tot` in pair order; returns the new total.
 DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec, int lane, int grp, bool valid, int tot) {
-  // ---- pad-table (lanes 0..7)
-  bool tfound = false, nearbin = false;
-  float tx = 0.f, ty = 0.f, tz = 0.f;
+  static_assert(SO100_PAIR_PADBIN0 == SO100_PAIR_PAD0 + SO100_NPAD, "the pad-bin pairs follow the pad-table pairs");
+  static_assert(SO100_PAIR_MOCAPBOX0 == SO100_PAIR_PADBIN0 + SO100_NPAIR_PADBIN, "the marker pairs follow the pad-bin pairs");
+  static_assert(SO100_NPAD + SO100_NPAIR_PADBIN + SO100_NPAIR_MOCAPBOX <= 64, "one candidate mask");
+  // ---- pad-table candidates and the pad-bin prefilter (lanes 0..7)
+  bool tcand = false, nearbin = false;
   if (valid && lane < SO100_NPAD) {
     const int p = SO100_PAIR_PAD0 + lane, g = m->pair_g1[p];
     const int b = m->pair_b1[p];                  // = geom_body[g] (so100_create), loaded beside g
     const float* bm = sh.jaw_mat[b - 6];
     const float* gm = m->geom_mat[g];
-    const float top = m->table_top, margin = m->pair_margin[p];
     float pc[3];
     mulmv3(pc, bm, m->geom_pos[g]);
 #pragma unroll
@@ -283,51 +284,14 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec,
     const float rb = m->geom_rbound[g] + bmarg;
     nearbin = ex2 <= rb * rb;
     // table broadphase: the pad's lowest point (centre z minus its half-extent along world z)
-    const float cz = pc[2];
     float ext = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; k++) ext += fabsf(bm[6] * gm[k] + bm[7] * gm[3 + k] + bm[8] * gm[6 + k]) * m->geom_size[g][k];
-    float sx = 0.f, sy = 0.f, zmin = 0.f;
-    int cnt = 0;
-    if (cz - ext - top < margin + 1e-4f) {
-    float c[3], R[9];
-    geom_pose_b(m, sh, g, b, c, R);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const float l0 = (k & 1 ? 1.f : -1.f) * m->geom_size[g][0];
-      const float l1 = (k & 2 ? 1.f : -1.f) * m->geom_size[g][1];
-      const float l2 = (k & 4 ? 1.f : -1.f) * m->geom_size[g][2];
-      const float w0 = R[0] * l0 + R[1] * l1 + R[2] * l2 + c[0];
-      const float w1 = R[3] * l0 + R[4] * l1 + R[5] * l2 + c[1];
-      const float w2 = R[6] * l0 + R[7] * l1 + R[8] * l2 + c[2];
-      const bool in = !(w0 < m->table_lo[0] || w0 > m->table_hi[0] || w1 < m->table_lo[1] || w1 > m->table_hi[1]) &&
-                      (w2 - top < margin);
-      if (in) {
-        sx += w0; sy += w1;
-        zmin = (cnt == 0 || w2 < zmin) ? w2 : zmin;
-        cnt++;
-      }
-    }
-    }
-    tfound = cnt > 0;
-    if (tfound) { tx = sx / (float)cnt; ty = sy / (float)cnt; tz = zmin; }
+    tcand = pc[2] - ext - m->table_top < m->pair_margin[p] + 1e-4f;
   }
-  const uint32_t trow = (uint32_t)((__ballot(tfound) >> (grp * 16)) & 0xFFull);
-  {
-    const int slot = tot + __popc(trow & ((1u << lane) - 1u));
-    if (tfound) {
-      float fr[9] = {0.f, 0.f, -1.f, 0, 0, 0, 0, 0, 0};
-      opaque(fr[2]);              // a constant frame: built here, not hoisted out of the fused substep loop
-      make_frame(fr);
-      const float top = m->table_top;
-      store_contact(sh, crec, slot, fr, tx, ty, 0.5f * (tz + top), tz - top, SO100_PAIR_PAD0 + lane);
-    }
-  }
-  tot += __popc(trow);
-  // ---- pad-bin candidates (3 pairs per lane); the whole wave skips them when no pad is near the bin
   const bool anybin = __ballot(nearbin) != 0ull;
-  if (!anybin && !m->ee) return tot;
-  uint64_t cm = 0ull;
+  uint64_t cm = (__ballot(tcand) >> (grp * 16)) & 0xFFull;      // bit j: pair SO100_PAIR_PAD0 + j
+  // ---- pad-bin candidates (3 pairs per lane); the whole wave skips them when no pad is near the bin
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     if (!anybin) break;
@@ -355,13 +319,11 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec,
       const float rr = m->geom_rbound[g1] + m->pair_margin[p];
       cand = ex2 <= rr * rr;
     }
-    cm |= ((__ballot(cand) >> (grp * 16)) & 0xFFFFull) << (16 * r);
+    cm |= ((__ballot(cand) >> (grp * 16)) & 0xFFFFull) << (SO100_NPAD + 16 * r);
   }
-  // EE variant: the cube and the pads against the marker box (pairs 200..208 = SO100_PAIR_PADBIN0 + 40 + i, after
-  // the pad-bin pairs in pair order): every one a candidate (collide_pair's bounding spheres decide)
-  static_assert(SO100_PAIR_MOCAPBOX0 == SO100_PAIR_PADBIN0 + SO100_NPAIR_PADBIN, "the marker pairs follow the pad-bin pairs");
-  static_assert(SO100_NPAIR_PADBIN + SO100_NPAIR_MOCAPBOX <= 64, "one candidate mask");
-  if (m->ee && valid) cm |= ((1ull << SO100_NPAIR_MOCAPBOX) - 1ull) << SO100_NPAIR_PADBIN;
+  // EE variant: the cube and the pads against the marker box (pairs 200..208, after the pad-bin pairs in pair
+  // order): every one a candidate (collide_pair's bounding spheres decide)
+  if (m->ee && valid) cm |= ((1ull << SO100_NPAIR_MOCAPBOX) - 1ull) << (SO100_NPAD + SO100_NPAIR_PADBIN);
   const int ncand = __popcll(cm);
   const int rounds = (wave_max_i(ncand) + kLanes - 1) / kLanes;
   for (int r = 0; r < rounds; r++) {
@@ -370,7 +332,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec,
     if (idx < ncand) {
       uint64_t x = cm;
       for (int k = 0; k < idx; k++) x &= x - 1ull;
-      p = SO100_PAIR_PADBIN0 + __ffsll((unsigned long long)x) - 1;
+      p = SO100_PAIR_PAD0 + __ffsll((unsigned long long)x) - 1;
     }
     PairContacts pc;
     pc.n = 0;

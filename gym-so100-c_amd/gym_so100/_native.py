@@ -46,7 +46,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 15         # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 16         # include/so100.h SO100_ABI_VERSION
 HULL_CELLG = 8           # SO100_HULL_CELLG
 HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 
@@ -63,6 +63,7 @@ def load():
     lib = ctypes.CDLL(LIB_PATH)
     lib.so100_abi_version.restype = ctypes.c_int
     lib.so100_last_error.restype = ctypes.c_char_p
+    lib.so100_source_hash.restype = ctypes.c_char_p
     lib.so100_create.argtypes = [_P, ctypes.c_int, ctypes.c_int]
     lib.so100_create.restype = _P
     lib.so100_destroy.argtypes = [_P]
@@ -106,12 +107,17 @@ def load():
     return lib
 
 
-EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
+EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_source_hash", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
                     "so100_contact_count", "so100_contact_counts", "so100_chunk_info", "so100_render_mesh", "so100_render",
                     "so100_set_step_mode", "so100_step_mode", "so100_hull_cells", "so100_set_fused_build",
                     "so100_fused_build")
+
+
+def source_hash():
+    """The content hash of the sources the loaded library was built from (so100_source_hash)."""
+    return load().so100_source_hash().decode()
 
 
 def check(rc, what):

@@ -465,9 +465,10 @@ class SO100VecEnv:
 
     def contact_counts(self):
         """int32 device tensor [N]: each env's contact count in the last solver launch (the last substep's list;
-        up to SO100_NCON_MAX, the first 16 held on chip)."""
+        up to SO100_NCON_MAX, the first 16 held on chip).  Zeros before the first solver launch (zero-initialised:
+        the native call writes nothing until a launch has recorded counts)."""
         torch = _torch()
-        out = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        out = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
         _native.check(self.lib.so100_contact_counts(self._handle, _native.ptr(out), self._stream()),
                       "so100_contact_counts")
         return out

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 15  /* 15: the EE variant's mocap marker box collides (SO100_NGEOM 16, SO100_NPAIR 209, SO100_NCON_MAX 643, debug stride 3,922);  14: no per-env contact cap (SO100_NCON_MAX: every pair at its collider's maximum), debug stride 3,436 (SO100_DBG_OVF), ncon_dropped always 0, status -3 for a caught C++ exception;  13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 16  /* 16: so100_source_hash;  15: the EE variant's mocap marker box collides (SO100_NGEOM 16, SO100_NPAIR 209, SO100_NCON_MAX 643, debug stride 3,922);  14: no per-env contact cap (SO100_NCON_MAX: every pair at its collider's maximum), debug stride 3,436 (SO100_DBG_OVF), ncon_dropped always 0, status -3 for a caught C++ exception;  13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -105,6 +105,9 @@ typedef struct so100_env so100_env;   /* opaque: device model copy + launch conf
 
 int         so100_abi_version(void);
 const char* so100_last_error(void);
+/* (ABI 16) the content hash (sha256, 16 hex digits) of the sources the library was built from: ties a committed
+ * measurement (profiles/r05_pmc_step_*.json) to the kernels it measured (bench.py reports traffic only on a match) */
+const char* so100_source_hash(void);
 /* sizeof(so100_model), sizeof(so100_buffers) as compiled — lets bindings verify their mirrors. */
 int         so100_struct_sizes(int* model_bytes, int* buffers_bytes);
 

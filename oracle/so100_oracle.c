@@ -403,7 +403,7 @@ static int clip_rect_quad(const real h[2], const real quad[8], real out[16]) {
 
 /* returns number of contacts written (<= SO100_MAXCONPAIR) */
 static int box_box(const real p1[3], const real R1[9], const real A[3], const real p2[3], const real R2[9],
-                   const real B[3], real margin, so100o_contact out[SO100_MAXCONPAIR]) {
+                   const real B[3], real margin, real ebias, so100o_contact out[SO100_MAXCONPAIR]) {
   real pd[3], pp[3], R[9], Q[9];
   for (int k = 0; k < 3; k++) pd[k] = p2[k] - p1[k];
   mulmtv3(pp, R1, pd);                               /* p in box1 frame */
@@ -427,7 +427,8 @@ static int box_box(const real p1[3], const real R1[9], const real A[3], const re
     if (s > margin) return 0;
     if (s > best) { best = s; code = 4 + j; invert = e < 0; nb[0] = R[j]; nb[1] = R[3 + j]; nb[2] = R[6 + j]; }
   }
-  /* edge x edge: n = e_i x (R col j), in box1 frame; prefer faces unless clearly better (1.05) */
+  /* edge x edge: n = e_i x (R col j), in box1 frame; mjc_BoxBox prefers faces unless an edge axis is clearly better
+   * (ebias 1.05); against the table mesh (the convex collider's exact minimum penetration) ebias is 1 */
   for (int i = 0; i < 3; i++) {
     int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
     for (int j = 0; j < 3; j++) {
@@ -441,7 +442,7 @@ static int box_box(const real p1[3], const real R1[9], const real A[3], const re
       real ex = A[i1] * Q[3 * i2 + j] + A[i2] * Q[3 * i1 + j] + B[j1] * Q[3 * i + j2] + B[j2] * Q[3 * i + j1];
       real s = ((real)fabs((double)e) - ex) / l;
       if (s > margin) return 0;
-      if (s * (real)1.05 > best) {
+      if (s * ebias > best) {
         best = s; code = 7 + 3 * i + j; invert = e < 0;
         nb[0] = n[0] / l; nb[1] = n[1] / l; nb[2] = n[2] / l;
       }
@@ -547,7 +548,7 @@ static int box_box(const real p1[3], const real R1[9], const real A[3], const re
  * rotation and half sizes; returns the contact count, contacts in out[0..n) (frames: the normal only) */
 int so100o_box_box(const so100o_real p1[3], const so100o_real R1[9], const so100o_real A[3], const so100o_real p2[3],
                    const so100o_real R2[9], const so100o_real B[3], so100o_real margin, so100o_contact out[SO100_MAXCONPAIR]) {
-  return box_box(p1, R1, A, p2, R2, B, margin, out);
+  return box_box(p1, R1, A, p2, R2, B, margin, (real)1.05, out);
 }
 
 /* [3P] mju_makeFrame: tangents from the normal (y-axis candidate (0,1,0) unless near-parallel) */
@@ -601,6 +602,8 @@ static void add_contact(so100o_data* d, const so100o_contact* c, int p) {
  * leaves unbounded (discoverPortal's, refinePortal's) stop after the same 50 iterations: no contact. */
 #define MPR_TOL ((real)1e-6)
 #define EPA_VISTOL ((real)1e-6)
+/* the separating-direction cache's certificate: a cached direction must clear the pair by 1 um (kernel kSepTol) */
+#define SEP_TOL ((real)1e-6)
 #define MPR_ITERS 50
 /* libccd's zero/equality tests use MuJoCo's double-precision CCD_EPS (DBL_EPSILON) in both builds: the
  * tests are absolute, and FLT_EPSILON would misclassify mm-scale geometry (e.g. |v0 x v1|^2 ~ 1e-10 read
@@ -1126,7 +1129,8 @@ static int mpr_broadphase(const mpr_obj* o, const real hb[3], const real hh[3]) 
  * The cube against the table (pair 8, geom2 = the table's mesh, scene_so100.xml:3,20): MuJoCo routes
  * box-mesh through its convex collider (mjc_Convex: native GJK/EPA in 3.3.3), one contact per pair without
  * multiccd (so_arm100.xml:4 sets none) [3P-unverified].  The table mesh is an exact box, so the minimum
- * penetration (normal, depth) is the separating-axis result; the one contact takes the SAT normal, the
+ * penetration (normal, depth) is the separating-axis result over all 15 axes (no face preference: ebias 1); the
+ * finger pads against the table (pairs 152..159) take the same rule.  The one contact takes the SAT normal, the
  * deepest point's distance, and the mean of the clipped contact positions (the contact patch's centre: the
  * face centre for a cube resting flat).  EPA's own witness point depends on its polytope triangulation and
  * is not restated (DESIGN.md §4 deviation 1). */
@@ -1140,7 +1144,9 @@ static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
   real margin = (real)m->pair_margin[p];
   if (norm3(dp) > norm3(A) + norm3(B) + margin) return;
   so100o_contact tmp[SO100_MAXCONPAIR];
-  int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin, tmp);
+  /* the table mesh (geom2 = 0): the exact separating-axis minimum (no face preference) */
+  int n = box_box(d->geom_xpos[g1], d->geom_xmat[g1], A, d->geom_xpos[g2], d->geom_xmat[g2], B, margin,
+                  g2 == 0 ? (real)1 : (real)1.05, tmp);
   if (g2 == 0 && n > 1) {                  /* the table mesh: the convex collider's one contact */
     real sp[3] = {0, 0, 0}, dmin = tmp[0].dist;
     for (int c = 0; c < n; c++) {
@@ -1154,150 +1160,150 @@ static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
   for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
 }
 
-/* (pad i, table), pairs 98..105: the hull-table rule applied to the pad's 8 corners (corner k: signs of
- * the half sizes from bits 0, 1, 2 of k, minus first).  The corners inside the top face's x-y footprint
- * and below the top (+ margin) count; one contact (MuJoCo collides the table mesh through its convex
- * collider, one contact per pair) at the deepest corner's distance, positioned at the counted corners'
- * x-y centroid (the face centre when a pad lies flat, where the corners' depths tie) and midway in z
- * between the deepest corner and the top.  Normal from the pad (geom1) into the table: -z. */
-static void pad_table(const so100_model* m, so100o_data* d, int p) {
-  const int g = m->pair_geom1[p];
-  const real top = (real)m->table_top, margin = (real)m->pair_margin[p];
-  const real lo0 = (real)m->table_lo[0], lo1 = (real)m->table_lo[1];
-  const real hi0 = (real)m->table_hi[0], hi1 = (real)m->table_hi[1];
-  real sx = 0, sy = 0, zmin = 0;
-  int cnt = 0;
-  for (int k = 0; k < 8; k++) {
-    real l[3], w[3];
-    for (int t = 0; t < 3; t++) l[t] = ((k >> t) & 1 ? (real)1 : (real)-1) * (real)m->geom_size[g][t];
-    mulmv3(w, d->geom_xmat[g], l);
-    for (int t = 0; t < 3; t++) w[t] += d->geom_xpos[g][t];
-    if (w[0] < lo0 || w[0] > hi0 || w[1] < lo1 || w[1] > hi1) continue;
-    if (!(w[2] - top < margin)) continue;
-    sx += w[0];
-    sy += w[1];
-    if (cnt == 0 || w[2] < zmin) zmin = w[2];
-    cnt++;
+/* one convex pair p through the convex collider (GJK + EPA, or MPR), in H = the body frame of hull k (geom2):
+ *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links;
+ *   98..106 the static Base hull (the cube, then link hulls 1..8); 107..142 (finger pad, link hull k);
+ *   143..151 (EE variant only) the mocap marker box against link hull k;
+ *   14..22 (the table, hull k) where the top-face rule is not exact (table_hull_fast).  The table mesh is an exact
+ *   box (scene_so100.xml:3,20; geom 0, obj1), so GJK + EPA on it is MuJoCo's mjc_Convex on the mesh. */
+static void convex_pair(const so100_model* m, so100o_data* d, int p) {
+  const int k = -1 - m->pair_geom2[p], g = m->pair_geom1[p], b = m->hull_body[k];
+  const real* RH = d->xmat[b];
+  mpr_obj o;
+  memset(&o, 0, sizeof(o));
+  real dp[3], hb[3], hh[3];
+  const real* Rb = g >= 0 ? d->geom_xmat[g] : d->xmat[m->hull_body[-1 - g]];
+  sub3(dp, g >= 0 ? d->geom_xpos[g] : d->xpos[m->hull_body[-1 - g]], d->xpos[b]);
+  mulmtv3(o.c, RH, dp);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) o.ax[3 * i + j] = RH[i] * Rb[j] + RH[3 + i] * Rb[3 + j] + RH[6 + i] * Rb[6 + j];
+  o.hull1 = g >= 0 ? -1 : -1 - g;
+  if (g >= 0) {
+    load3(o.h, m->geom_size[g]);
+    memcpy(o.c1, o.c, sizeof(o.c1));
+    memcpy(o.bc, o.c, sizeof(o.bc));
+    memcpy(o.bh, o.h, sizeof(o.bh));
+  } else {
+    const int k1 = o.hull1;
+    real t[3], l[3];
+    o.vert1 = (const double (*)[3])m->hull_vert[m->hull_start[k1]];
+    o.nvert1 = m->hull_count[k1];
+    load3(l, m->hull_centroid[k1]);
+    mulmv3(t, o.ax, l);
+    for (int q = 0; q < 3; q++) o.c1[q] = t[q] + o.c[q];
+    load3(l, m->hull_center[k1]);
+    mulmv3(t, o.ax, l);
+    for (int q = 0; q < 3; q++) o.bc[q] = t[q] + o.c[q];
+    load3(o.bh, m->hull_half[k1]);
   }
-  if (cnt == 0) return;
+  o.vert = (const double (*)[3])m->hull_vert[m->hull_start[k]];
+  o.nvert = m->hull_count[k];
+  load3(o.hc, m->hull_centroid[k]);
+  load3(hb, m->hull_center[k]);
+  load3(hh, m->hull_half[k]);
+  if (!mpr_broadphase(&o, hb, hh)) return;
+  STAT(0, 1);
+#ifdef SO100O_STATS
+  so100o_item_mark[0] = so100o_stat_cur[3]; so100o_item_mark[1] = so100o_stat_cur[4];
+#endif
+  real depth, dir[3], pos[3];
+  /* the kernels' separating-direction cache (so100_convex.h mpr_contacts), when d->sep_on: a direction that proved
+   * the pair separated in an earlier substep, re-checked with one support, skips GJK when it still clears the pair
+   * by 1e-6; results are unchanged (tests/test_oracle_epa.py::test_separation_cache_changes_nothing) */
+  if (d->sep_on && d->sep[p][3] != 0) {
+    real du[3] = {d->sep[p][0], d->sep[p][1], d->sep[p][2]};
+    mpr_sup a;
+    mpr_support(&o, du, &a);
+    if (dot3(a.v, du) < -SEP_TOL) { d->sep_hits++; return; }
+  }
+  real dsep[4];
+  const int hit_ = convex_penetration(m, &o, &depth, dir, pos, dsep);
+  for (int k = 0; k < 4; k++) d->sep[p][k] = dsep[k];
+  d->sep_sep += dsep[3] != 0;
+#ifdef SO100O_STATS
+  so100o_item_push(hit_, box_axes_separate(&o));
+#endif
+  if (!hit_) return;
+  STAT(2, 1);
   so100o_contact con;
   memset(&con, 0, sizeof(con));
-  con.pos[0] = sx / (real)cnt; con.pos[1] = sy / (real)cnt; con.pos[2] = (real)0.5 * (zmin + top);
-  con.frame[0] = 0; con.frame[1] = 0; con.frame[2] = -1;
-  con.dist = zmin - top;
+  mulmv3(con.frame, RH, dir);
+  mulmv3(con.pos, RH, pos);
+  for (int t = 0; t < 3; t++) con.pos[t] += d->xpos[b][t];
+  con.dist = -depth;
   add_contact(d, &con, p);
+}
+
+/* (table, hull k), pair 14 + k [3P: mjc_Convex on the table mesh, one contact]: the top-face rule where it is provably
+ * the exact minimum penetration, else the convex collider.  From the hull's body-frame bounding box (centre c, world
+ * extents ex, ey, ez): a candidate when its lowest point zb = c.z - ez is below top + margin.  With D = top - zb, an
+ * upper bound of the hull's depth d below the top, the rule applies when every vertex lies inside the top face's x-y
+ * footprint shrunk by D (c.x - ex >= lo.x + D, c.x + ex <= hi.x - D, and in y) and the hull's centroid (inside the
+ * hull) is at least D above the table's bottom.  Then lifting the hull by d separates it, and any shorter translation
+ * t leaves a point of the hull inside the table box (the hull's x-y stays inside the footprint; its z range still
+ * reaches below the top and above the bottom, so by convexity some point lies between them): the minimum penetration
+ * is d along +z.  The contact is EPA's vertex-face witness pair, the lowest vertex (the first in hull order among
+ * ties) and its projection on the top: pos = their midpoint, normal +z (table, geom1 -> hull, geom2).  Otherwise (a
+ * hull at the table's edges or side faces, or deep in it) the pair goes through the convex collider after pairs
+ * 23..151 (the kernels' order).  Returns 1: contact added, 0: no contact, -1: the convex collider. */
+static int table_hull_fast(const so100_model* m, so100o_data* d, int k) {
+  const int p = SO100_NPAIR_BOX + k, b = m->hull_body[k], g = m->pair_geom1[p];
+  const real top = (real)m->table_top, margin = (real)m->pair_margin[p];
+  const real bottom = top - 2 * (real)m->geom_size[g][2];
+  const real* R = d->xmat[b];
+  real c[3], wc[3], cg[3], wg[3];
+  load3(c, m->hull_center[k]);
+  mulmv3(wc, R, c);
+  real e[3];
+  for (int i = 0; i < 3; i++)
+    e[i] = (real)fabs((double)R[3 * i]) * (real)m->hull_half[k][0] + (real)fabs((double)R[3 * i + 1]) * (real)m->hull_half[k][1] +
+           (real)fabs((double)R[3 * i + 2]) * (real)m->hull_half[k][2];
+  const real zb = d->xpos[b][2] + wc[2] - e[2];
+  if (!(zb < top + margin)) return 0;
+  load3(cg, m->hull_centroid[k]);
+  mulmv3(wg, R, cg);
+  const real D = top - zb, cx = d->xpos[b][0] + wc[0], cy = d->xpos[b][1] + wc[1], gz = d->xpos[b][2] + wg[2];
+  if (!(cx - e[0] >= (real)m->table_lo[0] + D && cx + e[0] <= (real)m->table_hi[0] - D &&
+        cy - e[1] >= (real)m->table_lo[1] + D && cy + e[1] <= (real)m->table_hi[1] - D && gz - bottom >= D)) return -1;
+  real best = 0, bx = 0, by = 0;
+  for (int v = 0; v < m->hull_count[k]; v++) {
+    real hv[3], w[3];
+    load3(hv, m->hull_vert[m->hull_start[k] + v]);
+    mulmv3(w, R, hv);
+    for (int t = 0; t < 3; t++) w[t] += d->xpos[b][t];
+    if (v == 0 || w[2] < best) { best = w[2]; bx = w[0]; by = w[1]; }
+  }
+  if (!(best - top < margin)) return 0;
+  so100o_contact con;
+  memset(&con, 0, sizeof(con));
+  con.pos[0] = bx; con.pos[1] = by; con.pos[2] = (real)0.5 * (best + top);
+  con.frame[0] = 0; con.frame[1] = 0; con.frame[2] = 1;
+  con.dist = best - top;
+  add_contact(d, &con, p);
+  return 1;
 }
 
 static void collision(const so100_model* m, so100o_data* d) {
   d->ncon = 0;
   d->ncon_dropped = 0;
   for (int p = 0; p < SO100_NPAIR_BOX; p++) collide_box_pair(m, d, p);
-  const real top = (real)m->table_top;
-  const real lo0 = (real)m->table_lo[0], lo1 = (real)m->table_lo[1];
-  const real hi0 = (real)m->table_hi[0], hi1 = (real)m->table_hi[1];
+  /* pairs 14..22 (table, hull k): the top-face rule where it is the exact minimum penetration, else the convex
+   * collider (table_hull_fast below) */
+  int slow = 0;
   for (int k = 0; k < SO100_NHULL; k++) {
-    const int p = SO100_NPAIR_BOX + k, b = m->hull_body[k];
-    const real margin = (real)m->pair_margin[p];
-    /* broadphase: the lowest point of the hull's body-frame bounding box */
-    real c[3], wc[3];
-    load3(c, m->hull_center[k]);
-    mulmv3(wc, d->xmat[b], c);
-    const real* R = d->xmat[b];
-    real ext = (real)fabs((double)R[6]) * (real)m->hull_half[k][0] + (real)fabs((double)R[7]) * (real)m->hull_half[k][1] +
-               (real)fabs((double)R[8]) * (real)m->hull_half[k][2];
-    if (d->xpos[b][2] + wc[2] - ext >= top + margin) continue;
-    real best = 0, bx = 0, by = 0;
-    int found = 0;
-    for (int v = 0; v < m->hull_count[k]; v++) {
-      real hv[3], w[3];
-      load3(hv, m->hull_vert[m->hull_start[k] + v]);
-      mulmv3(w, d->xmat[b], hv);
-      for (int t = 0; t < 3; t++) w[t] += d->xpos[b][t];
-      if (w[0] < lo0 || w[0] > hi0 || w[1] < lo1 || w[1] > hi1) continue;
-      if (!found || w[2] < best) { best = w[2]; bx = w[0]; by = w[1]; found = 1; }
-    }
-    if (!found || !(best - top < margin)) continue;
-    so100o_contact con;
-    memset(&con, 0, sizeof(con));
-    con.pos[0] = bx; con.pos[1] = by; con.pos[2] = (real)0.5 * (best + top);
-    con.frame[0] = 0; con.frame[1] = 0; con.frame[2] = 1;
-    con.dist = best - top;
-    add_contact(d, &con, p);
+    const int r = table_hull_fast(m, d, k);
+    if (r < 0) slow |= 1 << k;
   }
-  /* pairs 23..151 through the MPR convex collider, in H = the body frame of hull k (geom2):
-   *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links;
-   *   98..106 the static Base hull (the cube, then link hulls 1..8); 107..142 (finger pad, link hull k);
-   *   143..151 (EE variant only) the mocap marker box against link hull k */
+  /* pairs 23..151 through the convex collider, then the table-hull pairs the top-face rule does not cover */
   for (int p = SO100_PAIR_MPR0; p < SO100_PAIR_PAD0; p++) {
     if (p >= SO100_PAIR_MOCAPHULL0 && !m->ee) break;
-    const int k = -1 - m->pair_geom2[p], g = m->pair_geom1[p], b = m->hull_body[k];
-    const real* RH = d->xmat[b];
-    mpr_obj o;
-    memset(&o, 0, sizeof(o));
-    real dp[3], hb[3], hh[3];
-    const real* Rb = g >= 0 ? d->geom_xmat[g] : d->xmat[m->hull_body[-1 - g]];
-    sub3(dp, g >= 0 ? d->geom_xpos[g] : d->xpos[m->hull_body[-1 - g]], d->xpos[b]);
-    mulmtv3(o.c, RH, dp);
-    for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++) o.ax[3 * i + j] = RH[i] * Rb[j] + RH[3 + i] * Rb[3 + j] + RH[6 + i] * Rb[6 + j];
-    o.hull1 = g >= 0 ? -1 : -1 - g;
-    if (g >= 0) {
-      load3(o.h, m->geom_size[g]);
-      memcpy(o.c1, o.c, sizeof(o.c1));
-      memcpy(o.bc, o.c, sizeof(o.bc));
-      memcpy(o.bh, o.h, sizeof(o.bh));
-    } else {
-      const int k1 = o.hull1;
-      real t[3], l[3];
-      o.vert1 = (const double (*)[3])m->hull_vert[m->hull_start[k1]];
-      o.nvert1 = m->hull_count[k1];
-      load3(l, m->hull_centroid[k1]);
-      mulmv3(t, o.ax, l);
-      for (int q = 0; q < 3; q++) o.c1[q] = t[q] + o.c[q];
-      load3(l, m->hull_center[k1]);
-      mulmv3(t, o.ax, l);
-      for (int q = 0; q < 3; q++) o.bc[q] = t[q] + o.c[q];
-      load3(o.bh, m->hull_half[k1]);
-    }
-    o.vert = (const double (*)[3])m->hull_vert[m->hull_start[k]];
-    o.nvert = m->hull_count[k];
-    load3(o.hc, m->hull_centroid[k]);
-    load3(hb, m->hull_center[k]);
-    load3(hh, m->hull_half[k]);
-    if (!mpr_broadphase(&o, hb, hh)) continue;
-    STAT(0, 1);
-#ifdef SO100O_STATS
-    so100o_item_mark[0] = so100o_stat_cur[3]; so100o_item_mark[1] = so100o_stat_cur[4];
-#endif
-    real depth, dir[3], pos[3];
-    /* the kernels' separating-direction cache (so100_convex.h mpr_contacts), when d->sep_on: a direction that proved
-     * the pair separated in an earlier substep, re-checked with one support, skips GJK when it still clears the pair
-     * by 1e-6; results are unchanged (tests/test_oracle_epa.py::test_separation_cache_changes_nothing) */
-    if (d->sep_on && d->sep[p][3] != 0) {
-      real du[3] = {d->sep[p][0], d->sep[p][1], d->sep[p][2]};
-      mpr_sup a;
-      mpr_support(&o, du, &a);
-      if (dot3(a.v, du) < (real)-1e-6) { d->sep_hits++; continue; }
-    }
-    real dsep[4];
-    const int hit_ = convex_penetration(m, &o, &depth, dir, pos, dsep);
-    for (int k = 0; k < 4; k++) d->sep[p][k] = dsep[k];
-    d->sep_sep += dsep[3] != 0;
-#ifdef SO100O_STATS
-    so100o_item_push(hit_, box_axes_separate(&o));
-#endif
-    if (!hit_) continue;
-    STAT(2, 1);
-    so100o_contact con;
-    memset(&con, 0, sizeof(con));
-    mulmv3(con.frame, RH, dir);
-    mulmv3(con.pos, RH, pos);
-    for (int t = 0; t < 3; t++) con.pos[t] += d->xpos[b][t];
-    con.dist = -depth;
-    add_contact(d, &con, p);
+    convex_pair(m, d, p);
   }
-  /* pairs 152..199: the finger pads vs the table (152..159), then vs the bin boxes (box-box) */
-  for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_PADBIN0; p++) pad_table(m, d, p);
+  for (int k = 0; k < SO100_NHULL; k++)
+    if ((slow >> k) & 1) convex_pair(m, d, SO100_NPAIR_BOX + k);
+  /* pairs 152..199: the finger pads vs the table (152..159: a box against the table mesh, the cube-table rule of
+   * collide_box_pair: the separating-axis minimum penetration, one contact), then vs the bin boxes (box-box) */
+  for (int p = SO100_PAIR_PAD0; p < SO100_PAIR_PADBIN0; p++) collide_box_pair(m, d, p);
   for (int p = SO100_PAIR_PADBIN0; p < SO100_PAIR_MOCAPBOX0; p++) collide_box_pair(m, d, p);
   /* pairs 200..208 (EE variant only): the cube and the pads against the mocap marker box (box-box) */
   if (m->ee)

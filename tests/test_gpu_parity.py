@@ -165,16 +165,14 @@ class TF:
 
     def __init__(self):
         self.qp, self.qv, self.fqp, self.fqv, self.qa, self.fqa = [], [], [], [], [], []
-        # the ensemble floor (_tf_run ens=K): per env step the fp64 oracle's error under K independent 1-ulp
-        # input perturbations, qvel and qacc [steps, K], contact forces (lists equal to the fp64 oracle's)
+        # the ensemble floor (_tf_run ens=True): per env step the errors of ENS64 independent 1-ulp input perturbations
+        # through the fp64 oracle and ENS32 more through the fp32 restatement, qvel and qacc [steps, ENS64 + ENS32] (fp64
+        # members first), and the fp64 members' contact forces (lists equal to the fp64 oracle's).  A fixed budget per
+        # state, run before and independently of the GPU's result: nothing in a floor depends on the error it grades
         self.eqv, self.eqa, self.eforce = [], [], []
         # (ens > 0) the fp32 restatement compiled with FMA contraction, as the GPU compiler contracts: a second fp32
         # rounding of the same algorithm, qvel and qacc per env step
         self.mqv, self.mqa = [], []
-        # (ens > 0) where the GPU lies beyond the single fp32 runs of its state (host-compiled and FMA): the largest error
-        # its ensemble members (fp64 and fp32) reach, and up to 64 more fp32 1-ulp perturbations of that state (a search
-        # for the same discrete event in fp32 arithmetic), else 0
-        self.aqv, self.aqa = [], []
         self.pqv, self.pqa, self.pforce, self.psame = [], [], [], []
         self.force, self.fforce, self.same, self.fsame, self.pairs = [], [], [], [], []
         self.drop_gpu, self.drop_ora = [], []
@@ -185,7 +183,7 @@ class TF:
 
     def arrays(self):
         for k in ("qp", "qv", "fqp", "fqv", "qa", "fqa", "pqv", "pqa", "pforce", "psame", "force", "fforce", "same",
-                  "fsame", "drop_gpu", "drop_ora", "near0", "eqv", "eqa", "eforce", "mqv", "mqa", "aqv", "aqa"):
+                  "fsame", "drop_gpu", "drop_ora", "near0", "eqv", "eqa", "eforce", "mqv", "mqa"):
             setattr(self, k, np.array(getattr(self, k)))
         return self
 
@@ -210,53 +208,96 @@ class TF:
                 f"{int(self.drop_gpu.sum())} oracle {int(self.drop_ora.sum())}")
 
 
-def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, ens=0):
+def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, ens=False):
     """Teacher-forced steps: each starts the product kernels, the debug build and both oracles from the
-    GPU's fp32 state (act_fn(step) -> [n, 6] float32 actions).  ens = K > 0: also the ensemble floor, the fp64
-    oracle and the fp32 restatement from K independent 1-ulp perturbations of each state (TF.eqv / eqa: 2K
-    members per state; eforce: the fp64 members')."""
+    GPU's fp32 state (act_fn(step) -> [n, 6] float32 actions).  ens: also the ensemble floor (TF.eqv / eqa), ENS64
+    independent 1-ulp perturbations of each state through the fp64 oracle and ENS32 through the fp32 restatement, and
+    the FMA-contracted fp32 restatement on the state itself (TF.mqv / mqa).  The floors of a state are computed from
+    the oracle runs alone, before the GPU's result is read."""
     res = res or TF()
     n = env.num_envs
     d64, d32, dp, dq = o64.new_data(), o32.new_data(), o64.new_data(), o64.new_data()
     prng = np.random.default_rng(12345)
     erng = np.random.default_rng(777)
+
+    def setm(d, i):
+        if mocap is not None:
+            _set_mocap(d, mocap[i])
+
+    def perturbed(i, q0, v0):
+        return q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)), v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12))
+
     for step in range(steps):
         q0 = env.qpos.cpu().numpy().astype(np.float64)
         v0 = env.qvel.cpu().numpy().astype(np.float64)
         w0 = env.qacc_warmstart.cpu().numpy().astype(np.float64)
         act = np.asarray(act_fn(step), np.float32)
-        gr, gb, gdrop, dbg, res.builds = _step_all_builds(env, act)
-        gq, gv = env.qpos.cpu().numpy(), env.qvel.cpu().numpy()
+        # the oracle side of every state first: the fp64 answer and every floor (single runs and the ensemble)
+        ora = []
         for i in range(n):
             for o, d in ((o64, d64), (o32, d32)):
                 o.set_state(d, q0[i], v0[i], w0[i])
-                if mocap is not None:
-                    _set_mocap(d, mocap[i])
+                setm(d, i)
             o64.set_state(dp, q0[i] * (1 + prng.normal(0, 2.0 ** -24, 13)), v0[i] * (1 + prng.normal(0, 2.0 ** -24, 12)),
                           w0[i])
-            if mocap is not None:
-                _set_mocap(dp, mocap[i])
+            setm(dp, i)
             o64.set_state(dq, q0[i], v0[i], w0[i])
-            if mocap is not None:
-                _set_mocap(dq, mocap[i])
+            setm(dq, i)
             o64.call("so100o_fwd_position", model, dq)
-            res.near0.append(any(abs(dq.con[c].dist) < NEAR0 for c in range(dq.ncon)))
+            near0 = any(abs(dq.con[c].dist) < NEAR0 for c in range(dq.ncon))
             _, r, _ = o64.env_step(model, d64, task, act[i])
             o32.env_step(model, d32, task, act[i])
             o64.env_step(model, dp, task, act[i])
             oq, ov = o64.get_state(d64)[:2]
             fq, fv = o32.get_state(d32)[:2]
-            res.qp.append(np.abs(oq - gq[i]).max())
+            s64, s32, sp = o64.last_solve(d64), o32.last_solve(d32), o64.last_solve(dp)
+            o_ = dict(r=r, oq=oq, ov=ov, fq=fq, fv=fv, bits=o64.contact_bits(d64), s64=s64, s32=s32, sp=sp,
+                      pv=o64.get_state(dp)[1], near0=near0)
+            if ens:
+                eq, ea, ef = [], [], []
+                for _ in range(ENS64):
+                    qp, vp = perturbed(i, q0, v0)
+                    o64.set_state(dp, qp, vp, w0[i])
+                    setm(dp, i)
+                    o64.env_step(model, dp, task, act[i])
+                    pe, fe, _, qae, _ = o64.last_solve(dp)
+                    eq.append(_rel(o64.get_state(dp)[1], ov))
+                    ea.append(_rel(qae, s64[3]))
+                    if np.array_equal(pe, s64[0]) and len(pe):
+                        ef += list(_force_err(fe, s64[1]))
+                # fp32 rounding's own discrete flips (an EPA face-face witness, whose tie between coplanar facets fp32
+                # breaks either way while fp64 resolves it one way) on this state
+                for _ in range(ENS32):
+                    qp, vp = perturbed(i, q0, v0)
+                    o32.set_state(d32, qp, vp, w0[i])
+                    setm(d32, i)
+                    o32.env_step(model, d32, task, act[i])
+                    eq.append(_rel(o32.get_state(d32)[1], ov))
+                    ea.append(_rel(o32.last_solve(d32)[3], s64[3]))
+                om = _oracle32fma()
+                dm = om.new_data()
+                om.set_state(dm, q0[i], v0[i], w0[i])
+                setm(dm, i)
+                om.env_step(model, dm, task, act[i])
+                o_.update(eq=eq, ea=ea, ef=ef, mqv=_rel(om.get_state(dm)[1], ov), mqa=_rel(om.last_solve(dm)[3], s64[3]))
+            ora.append(o_)
+        # then the GPU, graded against them
+        gr, gb, gdrop, dbg, res.builds = _step_all_builds(env, act)
+        gq, gv = env.qpos.cpu().numpy(), env.qvel.cpu().numpy()
+        for i, o_ in enumerate(ora):
+            p64, f64, fr64, qa64, nd64 = o_["s64"]
+            p32, f32, fr32, qa32, _ = o_["s32"]
+            pp, fp, _, qap, _ = o_["sp"]
+            ov = o_["ov"]
+            res.near0.append(o_["near0"])
+            res.qp.append(np.abs(o_["oq"] - gq[i]).max())
             res.qv.append(_rel(gv[i], ov))
-            res.fqp.append(np.abs(oq - fq).max())
-            res.fqv.append(_rel(fv, ov))
-            res.rew_bad += abs(r - gr[i]) > 1e-6
-            res.bit_bad += o64.contact_bits(d64) != gb[i]
+            res.fqp.append(np.abs(o_["oq"] - o_["fq"]).max())
+            res.fqv.append(_rel(o_["fv"], ov))
+            res.rew_bad += abs(o_["r"] - gr[i]) > 1e-6
+            res.bit_bad += o_["bits"] != gb[i]
             gp, gf, gfr, gqa = _gpu_solve(dbg[i])
-            p64, f64, fr64, qa64, nd64 = o64.last_solve(d64)
-            p32, f32, fr32, qa32, _ = o32.last_solve(d32)
-            pp, fp, _, qap, _ = o64.last_solve(dp)
-            res.pqv.append(_rel(o64.get_state(dp)[1], ov))
+            res.pqv.append(_rel(o_["pv"], ov))
             res.qa.append(_rel(gqa, qa64))
             res.fqa.append(_rel(qa32, qa64))
             res.pqa.append(_rel(qap, qa64))
@@ -274,52 +315,11 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
                 res.fforce += list(_force_err(f32, f64))
             res.states.append((q0[i], v0[i], w0[i], act[i]) + ((mocap[i],) if mocap is not None else ()))
             if ens:
-                eq, ea = [], []
-                for _ in range(ens):
-                    qp, vp = q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)), v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12))
-                    o64.set_state(dp, qp, vp, w0[i])
-                    if mocap is not None:
-                        _set_mocap(dp, mocap[i])
-                    o64.env_step(model, dp, task, act[i])
-                    pe, fe, _, qae, _ = o64.last_solve(dp)
-                    eq.append(_rel(o64.get_state(dp)[1], ov))
-                    ea.append(_rel(qae, qa64))
-                    if np.array_equal(pe, p64) and len(pe):
-                        res.eforce += list(_force_err(fe, f64))
-                    # the same perturbation through the fp32 restatement: fp32 arithmetic's own discrete flips (an EPA
-                    # face-face witness, whose tie between coplanar facets fp32 rounding breaks either way) on this state
-                    o32.set_state(d32, qp, vp, w0[i])
-                    if mocap is not None:
-                        _set_mocap(d32, mocap[i])
-                    o32.env_step(model, d32, task, act[i])
-                    eq.append(_rel(o32.get_state(d32)[1], ov))
-                    ea.append(_rel(o32.last_solve(d32)[3], qa64))
-                res.eqv.append(eq)
-                res.eqa.append(ea)
-                om = _oracle32fma()
-                dm = om.new_data()
-                om.set_state(dm, q0[i], v0[i], w0[i])
-                if mocap is not None:
-                    _set_mocap(dm, mocap[i])
-                om.env_step(model, dm, task, act[i])
-                res.mqv.append(_rel(om.get_state(dm)[1], ov))
-                res.mqa.append(_rel(om.last_solve(dm)[3], qa64))
-                gqv, gqa_ = res.qv[-1], res.qa[-1]
-                aqv = aqa = 0.0
-                if gqv > 2 * max(res.fqv[-1], res.mqv[-1]) + 1e-5 or gqa_ > 2 * max(res.fqa[-1], res.mqa[-1]) + 1e-5:
-                    aqv, aqa = max(eq), max(ea)
-                    for _ in range(64):
-                        if aqv >= 0.5 * gqv and aqa >= 0.5 * gqa_:
-                            break
-                        qp, vp = q0[i] * (1 + erng.normal(0, 2.0 ** -24, 13)), v0[i] * (1 + erng.normal(0, 2.0 ** -24, 12))
-                        o32.set_state(d32, qp, vp, w0[i])
-                        if mocap is not None:
-                            _set_mocap(d32, mocap[i])
-                        o32.env_step(model, d32, task, act[i])
-                        aqv = max(aqv, _rel(o32.get_state(d32)[1], ov))
-                        aqa = max(aqa, _rel(o32.last_solve(d32)[3], qa64))
-                res.aqv.append(aqv)
-                res.aqa.append(aqa)
+                res.eqv.append(o_["eq"])
+                res.eqa.append(o_["ea"])
+                res.eforce += o_["ef"]
+                res.mqv.append(o_["mqv"])
+                res.mqa.append(o_["mqa"])
     return res
 
 
@@ -354,6 +354,14 @@ def _force_bars(r, median_abs=None):
             assert np.median(r.force) <= median_abs
     assert np.median(r.qa) <= 2 * r.floor("qa", 0.5) + 1e-6
     assert np.quantile(r.qa, 0.9) <= 2 * r.floor("qa", 0.9) + 1e-4
+    if len(r.force):
+        # the force tail: the share of contacts off by more than 1e-4 and the p99, against the floors' (which the
+        # median / p90 bars above leave unbounded)
+        share = lambda x: np.mean(np.asarray(x) > 1e-4) if np.size(x) else 0.0
+        fshare = max(share(r.fforce), share(r.pforce), share(r.eforce))
+        assert share(r.force) <= 1.5 * fshare + 0.03, (share(r.force), fshare)
+        assert np.quantile(r.force, 0.99) <= 2 * r.floor("force", 0.99) + 1e-3, (np.quantile(r.force, 0.99),
+                                                                                  r.floor("force", 0.99))
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -937,31 +945,36 @@ def test_domain_randomization_config4_shard(solver):
     shard.close()
 
 
-ENS = 8     # the ensemble floor's size: independent 1-ulp perturbations of each state (each through fp64 and fp32)
+ENS64 = 8    # the ensemble floor: independent 1-ulp perturbations of each state through the fp64 oracle
+ENS32 = 32   # ... and through the fp32 restatement
 
 
 def _ensemble_bars(r, name="qv"):
-    """The deep-fold gate (round 4): these states (links pushed centimetres into each other) are chaotic, so a
-    single perturbation's maximum is a noisy bar that legal fp reorderings can cross.  The GPU's error
-    distribution is graded against the ensemble of ENS independent 1-ulp input perturbations of each state, each run
-    through the fp64 oracle and the fp32 restatement (fp32 rounding breaks discrete ties, e.g. an EPA face-face
-    witness, that fp64 resolves one way: round 4), and the fp32 restatement host-compiled and FMA-contracted (the
-    contraction alone moves the fp32 p99 up to 7x on these states, tools/dev/fp32_floor.py) on the same states, and
-    where the GPU lies beyond all of these, the largest error up to 64 more fp32 perturbations of that state reach: median, p90 and p99 within 2x the floor's (+1e-5 / 1e-4),
-    the tail mass (share off by more than 1e-4) within 1.5x the floor's (+0.03), and per state the GPU beyond
-    every ensemble member of its own state (2x + 1e-5) at most as often as one member would be (1 / (ENS + 1))."""
+    """The deep-fold gate (rounds 4-5): these states (links pushed centimetres into each other) are chaotic, so a
+    single perturbation's maximum is a noisy bar that legal fp reorderings can cross.  The GPU's error distribution
+    is graded against a floor computed per state from the oracles alone, with a fixed budget, before the GPU's result
+    is read (_tf_run): ENS64 independent 1-ulp input perturbations through the fp64 oracle, ENS32 through the fp32
+    restatement (fp32 rounding breaks discrete ties, e.g. an EPA face-face witness, that fp64 resolves one way), and
+    the fp32 restatement host-compiled and FMA-contracted (the GPU's arithmetic; the contraction alone moves the fp32
+    p99 up to 7x on these states, tools/dev/fp32_floor.py) on the state itself.  Bars: median, p90 and p99 within 2x
+    the floor's (+1e-5 / 1e-4 / 1e-4); on the steps whose GPU and fp64 contact lists are equal, p99 within 2x the
+    floor's on those steps (+1e-4); the tail mass (share off by more than 1e-4) within 1.5x the floor's (+0.03); and per
+    state the GPU beyond every member of its own state (2x + 1e-5) at most as often as one member would be
+    (1 / (members + 1))."""
     g = getattr(r, name)
-    # the fp32 floor: the restatement in fp32, as compiled for the host and with FMA contraction (the GPU's arithmetic)
-    f = np.maximum.reduce([{"qv": r.fqv, "qa": r.fqa}[name], {"qv": r.mqv, "qa": r.mqa}[name],
-                           {"qv": r.aqv, "qa": r.aqa}[name]])
+    # the single fp32 runs: the restatement as compiled for the host and with FMA contraction (the GPU's arithmetic)
+    f = np.maximum({"qv": r.fqv, "qa": r.fqa}[name], {"qv": r.mqv, "qa": r.mqa}[name])
     E = np.asarray({"qv": r.eqv, "qa": r.eqa}[name])
-    ens = E.ravel()
-    fl = lambda q: max(np.quantile(f, q), np.quantile(ens, q))
+    assert E.shape[1] == ENS64 + ENS32
+    fl = lambda q, m=slice(None): max(np.quantile(f[m], q), np.quantile(E[m].ravel(), q))
     assert np.median(g) <= 2 * fl(0.5) + 1e-5, (name, np.median(g), fl(0.5))
     assert np.quantile(g, 0.9) <= 2 * fl(0.9) + 1e-4, (name, np.quantile(g, 0.9), fl(0.9))
     assert np.quantile(g, 0.99) <= 2 * fl(0.99) + 1e-4, (name, np.quantile(g, 0.99), fl(0.99))
+    same = np.asarray(r.same, bool)
+    if same.sum() >= 10:
+        assert np.quantile(g[same], 0.99) <= 2 * fl(0.99, same) + 1e-4, (name, np.quantile(g[same], 0.99), fl(0.99, same))
     tail = lambda x: np.mean(np.asarray(x) > 1e-4)
-    assert tail(g) <= 1.5 * max(tail(f), tail(ens)) + 0.03, (name, tail(g), tail(f), tail(ens))
+    assert tail(g) <= 1.5 * max(tail(f), tail(E.ravel())) + 0.03, (name, tail(g), tail(f), tail(E.ravel()))
     beyond = g > 2 * np.maximum(E.max(axis=1), f) + 1e-5
     assert beyond.mean() <= 1.0 / (E.shape[1] + 1), (name, beyond.mean())
     return beyond
@@ -992,15 +1005,16 @@ def _arm_contact_parity(solver, oracle64, oracle32, p0, p1, label, seed, nsubste
     env = _new_env(n, solver, nsubstep=nsubstep)
     env.reset(seed=3)
     _set_states(env, states)
-    r = _tf_run(env, model, oracle64, oracle32, 3, lambda step: targets + rng.normal(0, 0.02, (n, 6)), ens=ENS).arrays()
+    r = _tf_run(env, model, oracle64, oracle32, 3, lambda step: targets + rng.normal(0, 0.02, (n, 6)), ens=True).arrays()
     env.close()
     cls = np.array([int(((p >= p0) & (p < p1)).sum()) for p in r.pairs])
     E = r.eqv
     print(f"\nGPU {label} contacts per env mean {cls.mean():.2f} (envs with any: {(cls > 0).mean():.2f}); "
           + r.summary(f"{solver} {label}" + (f", {nsubstep} substep per env step" if nsubstep else "")))
     q = lambda x, p: np.quantile(np.ravel(x), p)
-    print(f"ensemble floor ({E.shape[1]} perturbations x {E.shape[0]} steps): qvel median / p90 / p99 / max "
-          f"{q(E, .5):.2e} / {q(E, .9):.2e} / {q(E, .99):.2e} / {E.max():.2e}; GPU p99 {q(r.qv, .99):.2e}; "
+    print(f"ensemble floor ({ENS64} fp64 + {ENS32} fp32 perturbations x {E.shape[0]} steps): qvel median / p90 / p99 / max "
+          f"{q(E, .5):.2e} / {q(E, .9):.2e} / {q(E, .99):.2e} / {E.max():.2e} (fp64 members p99 {q(E[:, :ENS64], .99):.2e}, "
+          f"fp32 {q(E[:, ENS64:], .99):.2e}; FMA fp32 p99 {q(r.mqv, .99):.2e}); GPU p99 {q(r.qv, .99):.2e}; "
           f"contact-list flips (GPU vs fp64 oracle, last substep): {int((~r.same).sum())} of {len(r.same)}")
     assert (cls > 0).mean() > 0.5
     # a contact one side sees and the other does not (a deep fold's vertex on another hull's boundary) is a
@@ -1036,6 +1050,24 @@ def test_pad_link_contact_parity(solver, oracle64, oracle32):
     link, the actuators holding them; teacher-forced GPU steps at the fp32 floor."""
     from gym_so100.model import PAIR_PADLINK0, PAIR_MOCAPHULL0
     _arm_contact_parity(solver, oracle64, oracle32, PAIR_PADLINK0, PAIR_MOCAPHULL0, "pad-link", 23)
+
+
+@pytest.mark.parametrize("solver", ["newton", "pgs"])
+def test_table_edge_parity(solver, oracle64, oracle32):
+    """Arm hulls and finger pads against the table's edges and side faces (pairs 14..22 and 152..159, SURVEY §8 f.2;
+    round 5): the table is a mesh, so MuJoCo collides these pairs through its convex collider at the minimum
+    penetration.  Random arm poses whose first position stage holds a table contact with a non-vertical normal (a link
+    or pad pushed into a side face, through GJK + EPA or the box-box SAT), the actuators holding them; teacher-forced
+    GPU steps graded against the ensemble floor."""
+    from gym_so100.model import NPAIR_BOX, NHULL, PAIR_PAD0, PAIR_PADBIN0, NPAIR
+    table = lambda p: NPAIR_BOX <= p < NPAIR_BOX + NHULL or PAIR_PAD0 <= p < PAIR_PADBIN0
+
+    def side(d):
+        return any(table(d.con[i].pair) and abs(d.con[i].frame[2]) < 0.99 for i in range(d.ncon))
+    r = _arm_contact_parity(solver, oracle64, oracle32, 0, NPAIR, "table-edge", 31, select=side)
+    nside = np.array([int(sum(table(p) for p in ps)) for ps in r.pairs])
+    print(f"GPU table contacts per env step: mean {nside.mean():.2f}")
+    _force_bars(r)
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])

@@ -6,7 +6,7 @@ import copy
 
 import numpy as np
 
-from gym_so100.model import NPAIR_BOX, NHULL, PAIR_MPR0
+from gym_so100.model import NPAIR_BOX, NHULL, PAIR_MPR0, PAIR_PAD0
 
 NV = 12
 
@@ -31,19 +31,33 @@ def _state(o, m, arm, box=(0.4, 0.95, 0.6, 1, 0, 0, 0)):
 
 
 def _expected(model, d, hulls):
-    """(pair, pos, dist) of every hull below the top: lowest in-footprint vertex, first among ties."""
+    """(pair, pos, dist, fast) of every hull below the top.  fast: the top-face rule provably gives the exact minimum
+    penetration (from the hull's body-frame bounding box: with D = top - its lowest point, an upper bound of the depth,
+    the box's x-y extent lies inside the top face's footprint shrunk by D and the hull's centroid is at least D above
+    the table's bottom): the contact is at the lowest vertex (first among ties), midway to the top.  Otherwise the pair
+    goes through the convex collider (pos None: tests/test_oracle_epa.py grades it against the exact minimum
+    penetration)."""
     top = model.table_top
     lo, hi = np.array(model.table_lo[:]), np.array(model.table_hi[:])
+    bottom = top - 2 * model.geom_size[model.pair_geom1[NPAIR_BOX]][2]
     out = []
     for k, (b, v) in enumerate(hulls):
         R = np.array(d.xmat[b][:]).reshape(3, 3)
-        w = v @ R.T + np.array(d.xpos[b][:])
-        inside = (w[:, 0] >= lo[0]) & (w[:, 0] <= hi[0]) & (w[:, 1] >= lo[1]) & (w[:, 1] <= hi[1])
-        if not inside.any():
+        P = np.array(d.xpos[b][:])
+        c = R @ np.array(model.hull_center[k][:]) + P
+        e = np.abs(R) @ np.array(model.hull_half[k][:])
+        if not c[2] - e[2] < top:
             continue
-        i = np.flatnonzero(inside)[np.argmin(w[inside, 2])]
-        if w[i, 2] - top < 0:
-            out.append((NPAIR_BOX + k, np.array([w[i, 0], w[i, 1], 0.5 * (w[i, 2] + top)]), w[i, 2] - top))
+        D = top - (c[2] - e[2])
+        gz = (R @ np.array(model.hull_centroid[k][:]) + P)[2]
+        fast = (c[0] - e[0] >= lo[0] + D and c[0] + e[0] <= hi[0] - D and c[1] - e[1] >= lo[1] + D and
+                c[1] + e[1] <= hi[1] - D and gz - bottom >= D)
+        w = v @ R.T + P
+        i = int(np.argmin(w[:, 2]))
+        if fast and w[i, 2] - top >= 0:
+            continue                                 # the top-face rule: the lowest vertex above the top, separated
+        pos = np.array([w[i, 0], w[i, 1], 0.5 * (w[i, 2] + top)]) if fast else None
+        out.append((NPAIR_BOX + k, pos, w[i, 2] - top, fast))
     return out
 
 
@@ -60,20 +74,32 @@ def _dipping_configs(model, o, hulls, n, seed=0):
 
 
 def test_hull_table_contacts_match_independent_geometry(model, oracle64):
+    """The top-face rule's contacts (pairs 14..22) equal an independent numpy statement of it: one contact per hull
+    below the top, at its lowest vertex, normal +z (table, geom1 -> hull, geom2), in hull order and ahead of the
+    convex collider's contacts; hulls outside the rule's exact region (the table's edges and side faces) are in the
+    list after the convex pairs 23..151 (tests/test_oracle_epa.py grades their depth against the exact minimum
+    penetration)."""
     hulls = _hulls(model)
     assert sum(model.hull_count[k] for k in range(NHULL)) > 2000
     for arm in _dipping_configs(model, oracle64, hulls, 25):
         d = _state(oracle64, model, arm)
         want = _expected(model, d, hulls)
-        got = [(d.con[i].pair, np.array(d.con[i].pos[:]), d.con[i].dist, np.array(d.con[i].frame[:]))
+        pairs = [d.con[i].pair for i in range(d.ncon)]
+        got = [(i, d.con[i].pair, np.array(d.con[i].pos[:]), d.con[i].dist, np.array(d.con[i].frame[:]))
                for i in range(d.ncon) if NPAIR_BOX <= d.con[i].pair < PAIR_MPR0]
-        assert [g[0] for g in got] == [w[0] for w in want]          # hull order, one contact per hull
-        for (p, pos, dist, fr), (_, wpos, wdist) in zip(got, want):
+        fast = [w for w in want if w[3]]
+        assert [g[1] for g in got[:len(fast)]] == [w[0] for w in fast]      # hull order, one contact per hull
+        for (i, p, pos, dist, fr), (_, wpos, wdist, _) in zip(got, fast):
+            assert all(q < PAIR_MPR0 for q in pairs[:i])                       # ahead of the convex contacts
             np.testing.assert_allclose(pos, wpos, atol=1e-12)
             assert abs(dist - wdist) < 1e-12
             np.testing.assert_allclose(fr[:3], [0, 0, 1], atol=1e-15)  # table (geom1) -> hull (geom2)
             t1, t2 = fr[3:6], fr[6:9]
             assert abs(np.dot(t1, fr[:3])) < 1e-15 and abs(np.dot(t1, t2)) < 1e-15
+        for i, p, _, _, _ in got[len(fast):]:                       # the collider's: after every convex pair
+            assert p not in [w[0] for w in fast]
+            assert all(q < PAIR_PAD0 for q in pairs[:i])
+            assert not any(PAIR_MPR0 <= q < PAIR_PAD0 for q in pairs[i + 1:])
 
 
 def test_hull_contacts_are_condim3_rows_on_arm_dofs(model, oracle64):
@@ -125,39 +151,37 @@ def test_contacts_stop_the_arm_at_the_table(model, oracle64):
 
 
 def test_pad_contacts_match_independent_geometry(model, oracle64):
-    """Finger pads vs the table (pairs 98..105), against an independent numpy statement of
-    the rule: over random arm poses, a pad gets one table contact exactly when one of its 8 corners lies
-    inside the top face's footprint and below the top; distance = the deepest such corner's height, x-y =
-    those corners' centroid, z midway between the deepest corner and the top, normal from the pad
-    (geom1) down into the table."""
+    """Finger pads vs the table (pairs 152..159): a box against the table mesh, the cube-table rule
+    (the separating-axis minimum penetration over all 15 axes, one contact).  Over random arm poses a pad has one
+    table contact exactly when it overlaps the table box; its depth is the exact minimum penetration (an independent
+    scipy hull of the corner differences, within 1e-6) and along its normal the boxes overlap by that depth."""
     from gym_so100.model import PAIR_PAD0, PAIR_PADBIN0
-    top = model.table_top
-    lo, hi = np.array(model.table_lo[:]), np.array(model.table_hi[:])
+    from test_oracle_epa import _exact, _points
     jlo = np.array([r[0] for r in model.jnt_range]); jhi = np.array([r[1] for r in model.jnt_range])
     rng = np.random.default_rng(4)
-    signs = np.array([[1 if k & 1 else -1, 1 if k & 2 else -1, 1 if k & 4 else -1] for k in range(8)], float)
-    touched = 0
+    touched = side = 0
     for _ in range(400):
         d = _state(oracle64, model, rng.uniform(jlo, jhi))
-        if d.ncon_dropped:
-            continue                         # contact set truncated at SO100_MAXCON: not this test's subject
+        assert d.ncon_dropped == 0
         got = {}
         for i in range(d.ncon):
             p = d.con[i].pair
             if PAIR_PAD0 <= p < PAIR_PADBIN0:
                 got.setdefault(p, []).append(d.con[i])
         for pad in range(8):
-            g = model.pair_geom1[PAIR_PAD0 + pad]
-            R = np.array(d.geom_xmat[g][:]).reshape(3, 3)
-            w = (signs * np.array(model.geom_size[g][:])) @ R.T + np.array(d.geom_xpos[g][:])
-            sel = ((w[:, :2] >= lo) & (w[:, :2] <= hi)).all(1) & (w[:, 2] < top)
-            cons = got.get(PAIR_PAD0 + pad, [])
-            assert len(cons) == int(sel.any()), (pad, len(cons), sel)
-            if not cons:
+            p = PAIR_PAD0 + pad
+            A, B = _points(model, d, model.pair_geom1[p]), _points(model, d, 0)
+            ex, _, _, _ = _exact(A, B)
+            cons = got.get(p, [])
+            if ex < -1e-9 or not cons:
+                assert ex < 1e-9 and not cons, (pad, ex, len(cons))
                 continue
+            assert len(cons) == 1
+            c = cons[0]
+            n = np.array(c.frame[:3])
+            # within 1e-6 (EPA's ccd_tolerance): the SAT pads |R| by 1e-6 (mjc_BoxBox's guard), 0.6 um on the table
+            assert abs(-c.dist - ex) < 1e-6, (pad, -c.dist, ex)
+            assert abs(((A @ n).max() - (B @ n).min()) - ex) < 1e-6      # pad (geom1) -> table (geom2)
             touched += 1
-            c, zmin = cons[0], w[sel, 2].min()
-            np.testing.assert_allclose(c.frame[:3], [0, 0, -1], atol=0)
-            assert abs(c.dist - (zmin - top)) < 1e-12
-            np.testing.assert_allclose(c.pos[:], [*w[sel, :2].mean(0), 0.5 * (zmin + top)], atol=1e-12)
-    assert touched >= 20
+            side += n[2] > -0.99
+    assert touched >= 20 and side >= 1, (touched, side)

@@ -9,7 +9,8 @@ S x P dispatches (the timed steps) are summed and divided by S.  FETCH_SIZE and 
 (memory-side L2 -> fabric requests).  gfx950 tallies a 16-B/lane streaming read at half its bytes in
 FETCH_SIZE; the step's loads are mostly 4-B/lane and scalar, so hbm_bytes_per_step uses the raw count and
 hbm_bytes_per_step_fetch_x2 is the upper bound with every read doubled.  bench.py reads the JSON
-(profiles/r03_pmc_step_<mode>_<solver>_<n>.json) for roofline.traffic.
+(profiles/r05_pmc_step_<mode>_<solver>_<n>.json) for roofline.traffic, which it reports only when the file's
+lib_source_hash (so100_source_hash of the library profiled) equals the loaded library's.
 """
 import csv
 import glob
@@ -48,7 +49,10 @@ def main():
     valu = None
     if glob.glob(d + "/sq*counter_collection.csv"):
         valu, _ = per_step(step_rows(d + "/sq*counter_collection.csv", "SQ_INSTS_VALU"), warmup, steps)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "gym-so100-c_amd"))
+    from gym_so100 import _native      # the library the passes profiled (SO100_LIB or the in-tree build)
     res = {"n_envs": n, "mode": mode, "solver": solver, "dispatches_per_step": p,
+           "lib_source_hash": _native.source_hash(), "lib_path": os.path.relpath(_native.LIB_PATH),
            "fetch_kb_per_step": fetch, "write_kb_per_step": write,
            "hbm_bytes_per_step": (fetch + write) * 1024, "hbm_bytes_per_step_fetch_x2": (2 * fetch + write) * 1024,
            "hbm_bytes_per_env_step": (fetch + write) * 1024 / n, "valu_insts_per_step": valu,
