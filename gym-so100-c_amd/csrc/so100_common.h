@@ -95,6 +95,11 @@ DEV float4 bcast_row4(float4 v, int j) {
 // ds_bpermute byte address of lane src (0..15) of this lane's 16-lane row.  The lane id comes from an opaque
 // v_mbcnt pair at each use: __shfl's own lane id is computed once per kernel and, held across the narrowphase and
 // the solve, was a spilled value reloaded inside their loops (3-wave build)
+DEV int row_lane() {
+  int t;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(t));
+  return t & 15;
+}
 DEV int row_lane_addr(int src) {
   int t;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(t));
@@ -102,6 +107,14 @@ DEV int row_lane_addr(int src) {
 }
 DEV float shfl_at(float v, int addr) {
   return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+}
+// max over the wave of a value uniform within each env's 16-lane row (contact and candidate counts); result uniform.
+// Four scalar lane reads: no lane id (__shfl_xor's, computed once per kernel and held across the fused substep loop,
+// was a spilled value of the 3-wave build reloaded every substep)
+DEV int wave_max_row(int v) {
+  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
 }
 DEV float bcast16(float v, int src) { return __shfl(v, src, kLanes); }
 DEV int bcast16i(int v, int src) { return __shfl(v, src, kLanes); }

@@ -613,6 +613,9 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
   int nv = 4, best = -1;
   float bn[3] = {0.f, 0.f, 0.f}, bd = 0.f;
   for (int it = 0; it < kMprIters; it++) {
+    // the lane's position in its row from an opaque v_mbcnt pair each iteration: lane-derived values (the facet slot
+    // addresses, the below-lane mask) held across the iterations were spilled values reloaded inside them
+    lane = row_lane();
     // the nearest live facet: lanes scan slots lane, lane + 16, lane + 32, then a row (dist, slot) min
     const unsigned long long et0 = ESTAMP_T();
     ESTAMP_ADD(4, 1);

@@ -284,10 +284,7 @@ DEV void newton_rows_load(const Workspace& w, int e, int lane, bool valid, float
   for (int j = 0; j < 6; j++) r.mrow[j] = lane < 6 ? hd[N_M + 6 * lane + j] : 0.f;
   r.mcd = (lane >= 6 && dof) ? hd[N_MC + lane - 6] : 0.f;
   r.ncon = valid ? __float_as_int(hd[H_NCON]) : 0;
-  int ncon_max = r.ncon;
-  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
-  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
-  ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
+  const int ncon_max = wave_max_row(r.ncon);
   const float* __restrict__ crec = w.con + (size_t)e * kConEnv;
 #pragma unroll
   for (int c = 0; c < kJReg; c++) {
@@ -380,10 +377,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
   const float* mrow = r.mrow;
   const float mcd = r.mcd;
   const int ncon = r.ncon;
-  int ncon_max = ncon;
-  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
-  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
-  ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
+  const int ncon_max = wave_max_row(ncon);
   const float4* J = r.J;                  // contacts < kJReg; the others: r.jx (LDS)
   const bool own = lane < ncon;                   // lane c owns contact c
   float c_aref[4] = {0.f, 0.f, 0.f, 0.f}, c_D[4] = {1.f, 1.f, 1.f, 1.f}, c_mu = 1.f, c_fr0 = 1.f, c_fr1 = 1.f;
@@ -755,10 +749,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 template <class RecFn>
 DEV float newton_solve_any(const DevModel* __restrict__ m, const NewtonRows& r, int lane, bool valid, bool want_diag,
                            NewtonDiag& diag, RecFn rec) {
-  int ncon_max = r.ncon;
-  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 16));
-  ncon_max = max(ncon_max, __shfl_xor(ncon_max, 32));
-  ncon_max = __builtin_amdgcn_readfirstlane(ncon_max);
+  const int ncon_max = wave_max_row(r.ncon);
   if (ncon_max > kMaxCon) return newton_solve<true>(m, r, lane, valid, want_diag, diag, rec);
   return newton_solve<false>(m, r, lane, valid, want_diag, diag, rec);
 }

@@ -140,12 +140,7 @@ struct StageArgs {
   int par;             // substep parity (heavy-group list set)
 };
 
-DEV int wave_max_i(int v) {
-  // max over the wave (all 4 lane groups); result uniform
-  v = max(v, __shfl_xor(v, 16));
-  v = max(v, __shfl_xor(v, 32));
-  return __builtin_amdgcn_readfirstlane(v);
-}
+DEV int wave_max_i(int v) { return wave_max_row(v); }   // (so100_common.h)
 
 // reset one env (lane-group cooperative): arm start pose, cube spawn, zero velocity/warmstart
 DEV void env_reset_state(const DevModel* __restrict__ m, EnvShared& sh, int lane, uint32_t seed, float& qpos_r,
@@ -514,7 +509,9 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     const bool has_fr = lane < SO100_NV;
     const float fr_R = has_fr ? m->fr_R[lane] : 1.f;
     const float fr_fl = has_fr ? m->fr_floss[lane] : 0.f;
-    const float fr_aref = -m->fr_B * qvel_r;
+    // the velocity from its LDS copy (S1, bitwise qvel_r): qvel_r need not stay live across collision
+    const float qv_r = lane < SO100_NV ? sh.qvel[lane] : 0.f;
+    const float fr_aref = -m->fr_B * qv_r;
     float fr_f;
     {
       const float jar = warm_r - fr_aref;
@@ -529,14 +526,16 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     bool lim_on = false;
     float lim_s = 0.f, lim_aref = 0.f, lim_R = 1.f, lim_f = 0.f;
     if (lane < 6) {
-      const float dlo = qpos_r - m->jnt_lo[lane], dhi = m->jnt_hi[lane] - qpos_r;
+      // the joint position from its LDS copy (S1, bitwise qpos_r): qpos_r need not stay live across collision
+      const float q = sh.qpos[lane];
+      const float dlo = q - m->jnt_lo[lane], dhi = m->jnt_hi[lane] - q;
       float dist = 0.f;
       if (dlo < 0.f) { lim_on = true; lim_s = 1.f; dist = dlo; }
       else if (dhi < 0.f) { lim_on = true; lim_s = -1.f; dist = dhi; }
       if (lim_on) {
         const float imp = getimpedance(m->lim_solimp, dist, 0.f);
         lim_R = fmaxf(kMinVal, (1.f - imp) * __builtin_amdgcn_rcpf(imp) * m->lim_invw[lane]);
-        lim_aref = -m->lim_B * (lim_s * qvel_r) - m->lim_K * imp * dist;
+        lim_aref = -m->lim_B * (lim_s * qv_r) - m->lim_K * imp * dist;
         const float jar = lim_s * warm_r - lim_aref;
         lim_f = jar < 0.f ? -jar * __builtin_amdgcn_rcpf(lim_R) : 0.f;
       }
@@ -568,8 +567,8 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
             else jhi[c - kJReg] = J;
           }
           const bool mine = lane == c;
-          const float v0 = rowsum16(J.x * qvel_r), v1 = rowsum16(J.y * qvel_r);
-          const float v2 = rowsum16(J.z * qvel_r), v3 = rowsum16(J.w * qvel_r);
+          const float v0 = rowsum16(J.x * qv_r), v1 = rowsum16(J.y * qv_r);
+          const float v2 = rowsum16(J.z * qv_r), v3 = rowsum16(J.w * qv_r);
           cVn[0] = mine ? v0 : cVn[0]; cVn[1] = mine ? v1 : cVn[1];
           cVn[2] = mine ? v2 : cVn[2]; cVn[3] = mine ? v3 : cVn[3];
         }
@@ -606,8 +605,8 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
               J = contact_jac_ovf(m, sh, crec, c, lane);
               reinterpret_cast<float4*>(crec + (size_t)c * kConStride + kJOff)[lane] = J;
             }
-            const float v0 = rowsum16(J.x * qvel_r), v1 = rowsum16(J.y * qvel_r);
-            const float v2 = rowsum16(J.z * qvel_r), v3 = rowsum16(J.w * qvel_r);
+            const float v0 = rowsum16(J.x * qv_r), v1 = rowsum16(J.y * qv_r);
+            const float v2 = rowsum16(J.z * qv_r), v3 = rowsum16(J.w * qv_r);
             if (lane == k) { cv[0] = v0; cv[1] = v1; cv[2] = v2; cv[3] = v3; }
           }
           const int c = b0 + lane;
@@ -694,7 +693,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
             const float a = rowsum16(jv[r] * mv[q]);
             cA[k] = mine ? a : cA[k];
           }
-          const float v = rowsum16(jv[r] * qvel_r), ac = rowsum16(jv[r] * qs_r), w = rowsum16(jv[r] * warm_r);
+          const float v = rowsum16(jv[r] * qv_r), ac = rowsum16(jv[r] * qs_r), w = rowsum16(jv[r] * warm_r);
           cV[r] = mine ? v : cV[r];
           cAc[r] = mine ? ac : cAc[r];
           cW[r] = mine ? w : cW[r];
@@ -745,7 +744,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
               const float a = rowsum16(jv[r] * mv[q]);
               oA[q2] = mine ? a : oA[q2];
             }
-            const float v = rowsum16(jv[r] * qvel_r), ac = rowsum16(jv[r] * qs_r), w = rowsum16(jv[r] * warm_r);
+            const float v = rowsum16(jv[r] * qv_r), ac = rowsum16(jv[r] * qs_r), w = rowsum16(jv[r] * warm_r);
             oV[r] = mine ? v : oV[r];
             oAc[r] = mine ? ac : oAc[r];
             oW[r] = mine ? w : oW[r];
@@ -1103,9 +1102,20 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       asm volatile("s_mov_b32 %0, 0" : "=s"(zero));
       sa.m = reinterpret_cast<const DevModel*>(reinterpret_cast<const char*>(args.m) + zero);
     }
+    // the DR scales re-read per substep (from L2: 8 B per env), not carried across the loop in registers (the 3-wave
+    // build spilled them at kernel entry: a scratch store per lane and launch)
+    float mscale_s = 1.f, fscale_s = 1.f;
+    if ((args.flags & SO100_FLAG_DR) && args.b.dr_params) {
+      mscale_s = args.b.dr_params[(size_t)e * 4 + 0];
+      fscale_s = args.b.dr_params[(size_t)e * 4 + 1];
+    }
     NewtonRows nr;
-    assemble<SO100_SOLVER_NEWTON, true, kDebug>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale,
-                                                fscale, sub, nr);
+    assemble<SO100_SOLVER_NEWTON, true, kDebug>(sa, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, mscale_s,
+                                                fscale_s, sub, nr);
+    // the position and velocity state back from their LDS copies (assemble's S1 stores, untouched since): bitwise
+    // the same values, and the registers are not held across collision's register peak (they were spilled there)
+    qpos_r = lane < SO100_NQ ? sh.qpos[lane] : 0.f;
+    qvel_r = lane < SO100_NV ? sh.qvel[lane] : 0.f;
     TL_MARK(0);
     NewtonDiag diag;
     const bool dbg = kDebug && args.b.debug && sub == nsub - 1;
@@ -1135,11 +1145,15 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     const bool valid = env < args.n;
     EnvShared& sh = shm[grp];
     euler_update(sh, lane, h, warm_r, qpos_r, qvel_r);
-    final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, elapsed0, episode0);
+    // the step counters re-read (the kernel writes them only below, so they are the prologue's values): not held in
+    // registers across the substep loop (the 3-wave build spilled them)
+    int el0 = args.b.elapsed ? args.b.elapsed[e] : 0;
+    uint32_t ep0 = args.b.episode ? args.b.episode[e] : 0u;
+    final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, el0, ep0);
     if (valid && lane == 0 && args.b.ncon_dropped) args.b.ncon_dropped[env] = (uint32_t)sh.ndrop;
+    if (args.w.gcost && lane == 0 && grp == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
   }
   TL_MARK(2);
-  if (args.w.gcost && tid == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
 #ifdef SO100_TIMELINE
   if (args.b.debug && env0 < args.n && lane0 == 0) {
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
