@@ -27,6 +27,15 @@ namespace so100 {
 // an opaque copy: the compiler can neither fold nor hoist what is computed from it (the fused kernel's
 // substep loop would otherwise keep loop-invariant results live across it, spilling)
 DEV void opaque(float& v) { asm volatile("" : "+v"(v)); }
+// a value the compiler cannot see through (so it cannot hoist what derives from it out of a loop): a uniform pointer kept
+// scalar (+ an opaque scalar zero), a per-lane value in a VGPR
+template <class T> DEV T* launder_s(T* p) {
+  int zero;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(zero));
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(const_cast<void*>(static_cast<const void*>(p))) + zero);
+}
+DEV int launder_v(int v) { asm volatile("" : "+v"(v)); return v; }
+template <class T> DEV T* launder_v(T* p) { asm volatile("" : "+v"(p)); return p; }
 constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;

@@ -6,6 +6,7 @@
 #include "so100_common.h"
 #include "so100_kin.h"
 #include "so100_boxbox.h"
+#include "so100_pool.h"
 
 namespace so100 {
 
@@ -1025,7 +1026,7 @@ DEV void stage_convex_hit(const DevModel* __restrict__ m, EnvShared& sh, float* 
     MprStage& st = sh.mpr[slot];
     st.pos[0] = sp.x; st.pos[1] = sp.y; st.pos[2] = sp.z; st.pos[3] = sp.w;
     st.nrm[0] = sn.x; st.nrm[1] = sn.y; st.nrm[2] = sn.z; st.nrm[3] = sn.w;
-  } else {
+  } else if (crec) {               // (fused path: an env without a pool record collides again with one)
     float4* stg = reinterpret_cast<float4*>(crec + (size_t)slot * kConStride + kMprStageOff);
     stg[0] = sp;
     stg[1] = sn;
@@ -1053,8 +1054,8 @@ DEV void stage_convex_hit(const DevModel* __restrict__ m, EnvShared& sh, float* 
 // Returns the env's number of convex contacts (uniform across its row).  Staged contacts j >= kMaxCon go to the
 // env's HBM contact record (slot j, kMprStageOff; crec0: the record of the wave's first env).
 template <bool kCells>
-DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec0, float4* sep0, int lane, int grp,
-                     bool valid) {
+DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShared* shm, float* crec0, float4* sep0, int lane,
+                     int grp, bool valid) {
   constexpr int kConvex = SO100_NPAIR_CONVEX;
   constexpr int kRounds = (kConvex + kLanes - 1) / kLanes;   // 8
   static_assert(kRounds <= 8, "candidate masks hold 128 pairs");
@@ -1240,6 +1241,14 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
     const uint64_t hb = __ballot(hit);
+    uint32_t fnew = fpk;                        // the envs' staged counts after this round
+#pragma unroll
+    for (int g = 0; g < kEnvsPerBlock; g++) {
+      const int it = kEnvsPerBlock * rd + g;
+      if (it < total && ((hb >> (16 * g)) & 1ull)) fnew += 1u << (8 * env_of(it));
+    }
+    // fused path: an env whose staged contacts pass kMaxCon takes its pool record before they are staged there
+    if constexpr (kCells) (void)ensure_rec<true>(w, shm[grp], lane, valid, (int)((fnew >> (8 * grp)) & 0xFFu), nullptr);
     int slot = (int)((fpk >> (8 * ie)) & 0xFFu);
 #pragma unroll
     for (int g = 0; g < kEnvsPerBlock; g++) {
@@ -1247,12 +1256,14 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, EnvShared* shm, float* crec
       const bool h = it < total && ((hb >> (16 * g)) & 1ull);
       if (g < grp && h && env_of(it) == ie) slot++;
     }
-    if (hit && lane == 0) stage_convex_hit(m, shm[ie], crec0 + (size_t)ie * kConEnv, slot, p, depth, dir, pos);
-#pragma unroll
-    for (int g = 0; g < kEnvsPerBlock; g++) {
-      const int it = kEnvsPerBlock * rd + g;
-      if (it < total && ((hb >> (16 * g)) & 1ull)) fpk += 1u << (8 * env_of(it));
+    if (hit && lane == 0) {
+      // the env's record: the split path's per-env record (crec0: the wave's first env's), or the fused path's pool
+      // record (crec0: the pool) if the env holds one (else its contacts beyond kMaxCon are not stored: assemble
+      // collides again with a record)
+      float* const rb = kCells ? pool_rec(w, shm[ie].rec) : crec0 + (size_t)ie * kConEnv;
+      stage_convex_hit(m, shm[ie], rb, slot, p, depth, dir, pos);
     }
+    fpk = fnew;
   }
   return (int)((fpk >> (8 * grp)) & 0xFFu);
 }

@@ -60,6 +60,7 @@ struct __attribute__((aligned(16))) EnvShared {
   int con_pair[kMaxCon];
   float con_dist[kMaxCon];
   float mocap[7];                // EE variant: mocap pose (pos, quat wxyz)
+  int rec;                       // fused path: the env's pool contact record this substep (-1: none)
   union {
     struct {
       ConSlot con[kMaxCon];      // geometry (collision -> Jacobian)

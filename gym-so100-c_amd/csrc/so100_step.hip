@@ -16,6 +16,7 @@
 //   so100_convex.h    GJK + EPA / MPR mesh collider and its broadphase          so100_newton.h  Newton solve
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include "so100_device.h"
 #include "so100.h"
 #include "so100_common.h"
@@ -221,7 +222,7 @@ DEV void store_contact(EnvShared& sh, float* crec, int slot, const float* fr, fl
     sh.con[slot].g.pos[2] = p2; sh.con[slot].g.pos[3] = dist;
     sh.con_dist[slot] = dist;
     sh.con_pair[slot] = pair;
-  } else {
+  } else if (crec) {               // (fused path: an env without a pool record collides again with one)
     float4* g = reinterpret_cast<float4*>(crec + (size_t)slot * kConStride + kGeoOff);
     g[0] = make_float4(p0, p1, p2, dist);
     g[1] = make_float4(fr[0], fr[1], fr[2], fr[3]);
@@ -251,7 +252,9 @@ DEV void put_box_contacts(EnvShared& sh, float* crec, const PairContacts& pc, in
 //     pairs per lane), behind a wave-uniform prefilter (no pad near the bin's AABB: no candidates);
 //   (EE variant) pairs 200..208 (cube | pad i, the mocap marker box) join the candidates.
 // Contacts are appended after `tot` in pair order; returns the new total.
-DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec, int lane, int grp, bool valid, int tot) {
+template <bool kFused>
+DEV int pad_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShared& sh, float* crec, int lane, int grp,
+                     bool valid, int tot) {
   static_assert(SO100_PAIR_PADBIN0 == SO100_PAIR_PAD0 + SO100_NPAD, "the pad-bin pairs follow the pad-table pairs");
   static_assert(SO100_PAIR_MOCAPBOX0 == SO100_PAIR_PADBIN0 + SO100_NPAIR_PADBIN, "the marker pairs follow the pad-bin pairs");
   static_assert(SO100_NPAD + SO100_NPAIR_PADBIN + SO100_NPAIR_MOCAPBOX <= 64, "one candidate mask");
@@ -337,6 +340,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, EnvShared& sh, float* crec,
     int off = 0, sum = 0;
 #pragma unroll
     for (int k = 0; k < kLanes; k++) { const int c = sh.cnt[k]; off += (k < lane) ? c : 0; sum += c; }
+    crec = ensure_rec<kFused>(w, sh, lane, valid, tot + sum, crec);
     put_box_contacts(sh, crec, pc, tot + off, p);
     tot += sum;
     __syncthreads();
@@ -385,6 +389,77 @@ DEV void set_controls(const StageArgs& args, EnvShared& sh, int lane, int e, flo
   }
 }
 
+// S3, collision, of the wave's 4 envs: hulls vs the table, the convex pairs (staged in LDS), one box pair per lane, the
+// pads; the contacts compacted in pair order into the env's list (sh.ncon: its length).  The first kMaxCon on chip,
+// the rest in the env's HBM record: crec on the split path; on the fused path the pool record an env takes when its
+// list passes kMaxCon (ensure_rec, before each phase's stores).  recbase: the split path's record of the wave's first
+// env, or the fused path's pool; sep: the wave's first env's separating-direction cache.
+#ifdef SO100_STAGE_STAMPS
+#define SSTAMP_PARAMS , unsigned long long& sst_prev_, unsigned long long* sst_acc_
+#define SSTAMP_PASS , sst_prev_, sst_acc_
+#else
+#define SSTAMP_PARAMS
+#define SSTAMP_PASS
+#endif
+template <bool kFused>
+DEV void collide(const DevModel* __restrict__ m, const Workspace& w, float* recbase, float4* sep, EnvShared& sh, int lane,
+                 int grp, bool valid, float* crec SSTAMP_PARAMS) {
+  const int nmpr = mpr_contacts<kFused>(m, w, &sh - grp, recbase, sep, lane, grp, valid);
+  SSTAMP(7);
+  float hx, hy, hz;
+  const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
+  const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
+  SSTAMP(6);
+  PairContacts pc;
+  pc.n = 0;
+  if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
+#ifdef SO100_STAMP_BOXBOX
+  SSTAMP(0);            // stamps diagnostic: the box-box pairs alone in slot 0 (Euler's, empty in the stage kernel)
+#endif
+  sh.cnt[lane] = pc.n;
+  __syncthreads();
+  {
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
+    // the box, table-hull and convex contacts' total is known here, before any of them is stored
+    crec = ensure_rec<kFused>(w, sh, lane, valid, tot + __popc(hrow) + nmpr, crec);
+    put_box_contacts(sh, crec, pc, off, lane);
+    const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
+    if (hfound) {
+      float fr[9] = {0.f, 0.f, 1.f, 0, 0, 0, 0, 0, 0};
+      opaque(fr[2]);            // a constant frame: built here, not hoisted out of the fused substep loop
+      make_frame(fr);
+      const float top = m->table_top;
+      store_contact(sh, crec, hslot, fr, hx, hy, 0.5f * (hz + top), hz - top, SO100_NPAIR_BOX + lane);
+    }
+    tot += __popc(hrow);
+    // the convex collider's contacts, staged in order: staged contact j is contact tot + j (staged j >= kMaxCon
+    // in the record, mpr_contacts)
+    if (lane < nmpr) {
+      const MprStage st = sh.mpr[lane];
+      float fr[9] = {st.nrm[0], st.nrm[1], st.nrm[2], 0, 0, 0, 0, 0, 0};
+      make_frame(fr);
+      store_contact(sh, crec, tot + lane, fr, st.pos[0], st.pos[1], st.pos[2], st.pos[3], __float_as_int(st.nrm[3]));
+    }
+    for (int j0 = kMaxCon; j0 < wave_max_i(nmpr); j0 += kLanes) {   // rare: more than kMaxCon convex contacts
+      const int j = j0 + lane;
+      if (j < nmpr && crec) {
+        const float4* stg = reinterpret_cast<const float4*>(crec + (size_t)j * kConStride + kMprStageOff);
+        const float4 sp = stg[0], sn = stg[1];
+        float fr[9] = {sn.x, sn.y, sn.z, 0, 0, 0, 0, 0, 0};
+        make_frame(fr);
+        store_contact(sh, crec, tot + j, fr, sp.x, sp.y, sp.z, sp.w, __float_as_int(sn.w));
+      }
+    }
+    tot += nmpr;
+    __syncthreads();
+    tot = pad_contacts<kFused>(m, w, sh, crec, lane, grp, valid, tot);
+    // every contact is kept (kConCap is the list's maximum), so none is dropped: 0 is written as the counter
+    if (lane == 0) sh.ncon = tot;
+  }
+  __syncthreads();
+}
 // One substep's position/velocity stages and constraint assembly on the state in registers (after the
 // previous substep's Euler): kinematics, CRBA/RNE, actuation, collision, the frictionloss / limit /
 // contact rows.  Newton: the rows go to nr (kFused: kept in registers for newton_solve; split: stored to the
@@ -423,69 +498,25 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     // box-hull pairs)
     // (the convex pairs first: the other collision results are then not held across their narrowphase's register
     // peak; the contacts are compacted in pair order below whatever the order of computation)
-    const int nmpr = mpr_contacts<kFused>(m, &sh - grp, args.w.con + (size_t)(env - grp) * kConEnv,
-                                          args.w.sep + (size_t)(env - grp) * kSepPairs, lane, grp, valid);
-    SSTAMP(7);
-    float hx, hy, hz;
-    const bool hfound = hull_table(m, sh, lane, grp, valid, hx, hy, hz);
-    const uint32_t hrow = (uint32_t)((__ballot(hfound) >> (grp * 16)) & 0xFFFFull);
-    SSTAMP(6);
-    // the env's contact record in HBM: the contacts beyond the kMaxCon held on chip (every kernel), and the
-    // split path's solver record
-    float* const crec = args.w.con + (size_t)e * kConEnv;
-    PairContacts pc;
-    pc.n = 0;
-    if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
-#ifdef SO100_STAMP_BOXBOX
-    SSTAMP(0);            // stamps diagnostic: the box-box pairs alone in slot 0 (Euler's, empty in the stage kernel)
-#endif
-    sh.cnt[lane] = pc.n;
-    __syncthreads();
-    {
-      int off = 0, tot = 0;
-#pragma unroll
-      for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
-      put_box_contacts(sh, crec, pc, off, lane);
-      const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
-      if (hfound) {
-        float fr[9] = {0.f, 0.f, 1.f, 0, 0, 0, 0, 0, 0};
-        opaque(fr[2]);            // a constant frame: built here, not hoisted out of the fused substep loop
-        make_frame(fr);
-        const float top = m->table_top;
-        store_contact(sh, crec, hslot, fr, hx, hy, 0.5f * (hz + top), hz - top, SO100_NPAIR_BOX + lane);
+    // the env's contact record in HBM, for the contacts beyond the kMaxCon held on chip: the split path's per-env
+    // record (also its solver record); the fused path's pool record, taken only by an env whose list is longer
+    float* crec = kFused ? nullptr : args.w.con + (size_t)e * kConEnv;
+    float* const recbase = kFused ? args.w.pool : args.w.con + (size_t)(env - grp) * kConEnv;
+    float4* const sep = args.w.sep + (size_t)(env - grp) * kSepPairs;
+    collide<kFused>(m, args.w, recbase, sep, sh, lane, grp, valid, crec SSTAMP_PASS);
+    // the env's record from here on, recomputed at each use (the contacts beyond kMaxCon are rare): not a pointer held
+    // across the rows and the solve (the 3-wave build spilled it)
+    auto recp = [&]() -> float* { return kFused ? pool_rec(args.w, sh.rec) : args.w.con + (size_t)e * kConEnv; };
+    if constexpr (!kFused) {
+      if (valid && lane == 0 && B.ncon_dropped && sub == 0) B.ncon_dropped[env] = 0u;
+    } else {
+      // (the pool's safety valve, never reached in a measured run) no record came free: the first kMaxCon contacts
+      if (valid && lane == 0 && sh.ncon > kMaxCon && sh.rec < 0) {
+        sh.ndrop += sh.ncon - kMaxCon;
+        sh.ncon = launder_v(kMaxCon);     // (a constant materialised here: not one held from the kernel entry)
       }
-      tot += __popc(hrow);
-      // the convex collider's contacts, staged in order: staged contact j is contact tot + j (staged j >= kMaxCon
-      // in the record, mpr_contacts)
-      if (lane < nmpr) {
-        const MprStage st = sh.mpr[lane];
-        float fr[9] = {st.nrm[0], st.nrm[1], st.nrm[2], 0, 0, 0, 0, 0, 0};
-        make_frame(fr);
-        store_contact(sh, crec, tot + lane, fr, st.pos[0], st.pos[1], st.pos[2], st.pos[3], __float_as_int(st.nrm[3]));
-      }
-      for (int j0 = kMaxCon; j0 < wave_max_i(nmpr); j0 += kLanes) {   // rare: more than kMaxCon convex contacts
-        const int j = j0 + lane;
-        if (j < nmpr) {
-          const float4* stg = reinterpret_cast<const float4*>(crec + (size_t)j * kConStride + kMprStageOff);
-          const float4 sp = stg[0], sn = stg[1];
-          float fr[9] = {sn.x, sn.y, sn.z, 0, 0, 0, 0, 0, 0};
-          make_frame(fr);
-          store_contact(sh, crec, tot + j, fr, sp.x, sp.y, sp.z, sp.w, __float_as_int(sn.w));
-        }
-      }
-      tot += nmpr;
       __syncthreads();
-      tot = pad_contacts(m, sh, crec, lane, grp, valid, tot);
-      // every contact is kept (kConCap is the list's maximum), so none is dropped: 0 is written as the counter
-      if (lane == 0) {
-        sh.ncon = tot;
-        if constexpr (kFused) sh.ndrop = 0;              // stored by the fused epilogue
-      }
-      if constexpr (!kFused) {
-        if (valid && lane == 0 && B.ncon_dropped && sub == 0) B.ncon_dropped[env] = 0u;
-      }
     }
-    __syncthreads();
     const int ncon = valid ? sh.ncon : 0;
     const int ncon_max = wave_max_i(ncon);
     SSTAMP(2);
@@ -560,7 +591,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
           float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
           if (c < ncon && lane < SO100_NV) {
             J = contact_jac(m, sh, c, lane);
-            if constexpr (!kFused) reinterpret_cast<float4*>(crec + c * kConStride + kJOff)[lane] = J;
+            if constexpr (!kFused) reinterpret_cast<float4*>(recp() + c * kConStride + kJOff)[lane] = J;
           }
           if constexpr (kFused) {
             if (c < kJReg) nr.J[c] = J;
@@ -602,8 +633,8 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
             const int c = b0 + k;
             float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
             if (c < ncon && lane < SO100_NV) {
-              J = contact_jac_ovf(m, sh, crec, c, lane);
-              reinterpret_cast<float4*>(crec + (size_t)c * kConStride + kJOff)[lane] = J;
+              J = contact_jac_ovf(m, sh, recp(), c, lane);
+              reinterpret_cast<float4*>(recp() + (size_t)c * kConStride + kJOff)[lane] = J;
             }
             const float v0 = rowsum16(J.x * qv_r), v1 = rowsum16(J.y * qv_r);
             const float v2 = rowsum16(J.z * qv_r), v3 = rowsum16(J.w * qv_r);
@@ -611,8 +642,8 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
           }
           const int c = b0 + lane;
           if (c < ncon) {
-            float4* sl = reinterpret_cast<float4*>(crec + (size_t)c * kConStride);
-            const float* g = crec + (size_t)c * kConStride;
+            float4* sl = reinterpret_cast<float4*>(recp() + (size_t)c * kConStride);
+            const float* g = recp() + (size_t)c * kConStride;
             float4 aref4, R4, mu4;
             newton_contact_rows(m, __float_as_int(g[kGeoPair]), g[kGeoDist], cv, fscale, aref4, R4, mu4);
             // the solve's per-contact constants, as newton_solve derives them for the resident contacts (D = 1 / R,
@@ -679,7 +710,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c < ncon && lane < SO100_NV) {
           J = contact_jac(m, sh, c, lane);
-          reinterpret_cast<float4*>(crec + c * kConStride + kJOff)[lane] = J;
+          reinterpret_cast<float4*>(recp() + c * kConStride + kJOff)[lane] = J;
         }
         Jr[c] = J;
         const float4 M = minv_times(J, minv_row, invmc, lane);   // M^-1 J' column of this dof
@@ -706,7 +737,7 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     float cf[4] = {0.f, 0.f, 0.f, 0.f};
     if (lane < ncon)
       pgs_contact_block(m, sh.con_pair[lane], sh.con_dist[lane], fscale, cA, cV, cAc, cW,
-                        reinterpret_cast<float4*>(crec + lane * kConStride), cf, cost_part);
+                        reinterpret_cast<float4*>(recp() + lane * kConStride), cf, cost_part);
     SSTAMP(4);
     // J' f of the warmstart forces: contact c's forces broadcast from lane c
 #pragma unroll
@@ -730,8 +761,8 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
           const int c = b0 + k;
           float4 J = make_float4(0.f, 0.f, 0.f, 0.f);
           if (c < ncon && lane < SO100_NV) {
-            J = contact_jac_ovf(m, sh, crec, c, lane);
-            reinterpret_cast<float4*>(crec + (size_t)c * kConStride + kJOff)[lane] = J;
+            J = contact_jac_ovf(m, sh, recp(), c, lane);
+            reinterpret_cast<float4*>(recp() + (size_t)c * kConStride + kJOff)[lane] = J;
           }
           const float4 M = minv_times(J, minv_row, invmc, lane);
           const float jv[4] = {J.x, J.y, J.z, J.w}, mv[4] = {M.x, M.y, M.z, M.w};
@@ -753,15 +784,15 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         float of[4] = {0.f, 0.f, 0.f, 0.f};
         const int c = b0 + lane;
         if (c < ncon) {
-          float4* cs = reinterpret_cast<float4*>(crec + (size_t)c * kConStride);
-          const float* g = crec + (size_t)c * kConStride;
+          float4* cs = reinterpret_cast<float4*>(recp() + (size_t)c * kConStride);
+          const float* g = recp() + (size_t)c * kConStride;
           pgs_contact_block(m, __float_as_int(g[kGeoPair]), g[kGeoDist], fscale, oA, oV, oAc, oW, cs, of, cost_part);
           cs[kBlkF] = make_float4(of[0], of[1], of[2], of[3]);     // zeroed below if the warmstart is dropped
         }
 #pragma unroll 1
         for (int k = 0; k < kLanes && b0 + k < ncon_max; k++) {
           const float4 fk = shfl_row4(make_float4(of[0], of[1], of[2], of[3]), k);
-          const float4 J = ovf_j(crec, b0 + k, lane, ncon);
+          const float4 J = ovf_j(recp(), b0 + k, lane, ncon);
           phi += J.x * fk.x + J.y * fk.y + J.z * fk.z + J.w * fk.w;
         }
       }
@@ -785,10 +816,10 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     } else {
       qacc_c += dq;
     }
-    if (lane < ncon) reinterpret_cast<float4*>(crec + lane * kConStride)[kBlkF] = make_float4(cf[0], cf[1], cf[2], cf[3]);
+    if (lane < ncon) reinterpret_cast<float4*>(recp() + lane * kConStride)[kBlkF] = make_float4(cf[0], cf[1], cf[2], cf[3]);
     if (ncon_max > kMaxCon && cost > 0.f) {
       for (int c = kMaxCon + lane; c < ncon; c += kLanes)
-        reinterpret_cast<float4*>(crec + (size_t)c * kConStride)[kBlkF] = make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<float4*>(recp() + (size_t)c * kConStride)[kBlkF] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
     // ---------------- solver record -> HBM (consumed by so100_pgs_kernel)
@@ -1081,6 +1112,10 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
   uint32_t episode0;
   load_state(args, lane, e, qpos_r, qvel_r, warm_r, mscale, fscale, sigma, elapsed0, episode0);
   set_controls(args, sh, lane, e, sigma, elapsed0, episode0);
+  if (lane == 0) {
+    sh.rec = -1;                  // no pool contact record held
+    sh.ndrop = 0;                 // contacts left out over the step (the pool's safety valve only)
+  }
   const int nsub = args.m->nsubstep;
   const float h = args.m->timestep;
   for (int sub = 0; sub < nsub; sub++) {
@@ -1124,7 +1159,7 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     auto rec = [&]() -> float* {
       int l2, g2, en2, e2;
       fresh_ids(group, args.n, l2, g2, en2, e2);
-      return args.w.con + (size_t)e2 * kConEnv;
+      return pool_rec(args.w, shm[g2].rec);
     };
     const float qacc = newton_solve_any(sa.m, nr, lane, valid, dbg, diag, rec);
     if (dbg) {
@@ -1134,6 +1169,15 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       if (valid) newton_diag_write_ovf(args.b.debug + (size_t)row * SO100_DBG_STRIDE, rec(), nr.ncon, lane);
     }
     warm_r = lane < SO100_NV ? qacc : 0.f;
+    {
+      // the env's pool record back (its substep is done with it)
+      int l2, g2, en2, e2;
+      fresh_ids(group, args.n, l2, g2, en2, e2);
+      if (l2 == 0 && shm[g2].rec >= 0) {
+        pool_release(args.w, shm[g2].rec);
+        shm[g2].rec = -1;
+      }
+    }
     TL_MARK(1);
   }
   TL_MARK(-1);
@@ -1461,7 +1505,7 @@ hipError_t alloc_workspace(int n, Workspace* w) {
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
   for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist, (void*)w->gcost,
-                  (void*)w->order, (void*)w->sep}) {
+                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
@@ -1470,19 +1514,24 @@ hipError_t free_workspace(Workspace* w) {
   w->gflag = w->gcost = nullptr;
   w->hcount = w->hlist = w->order = nullptr;
   w->sep = nullptr;
+  w->pool = nullptr;
+  w->pool_bm = nullptr;
   return r;
 }
 // The fused path's workspace: the record header (only its contact counts are written), the wave-order buffers,
-// and the per-env contact record of the contacts beyond the kMaxCon held on chip (kConEnv floats per env:
-// 252 KB, 16.5 GB at 65,536 envs, for a list that can hold every contact; touched only where an env has more
-// than kMaxCon contacts).
+// the separating-direction cache, and the contact-record pool (Workspace::pool): per XCD one record per 64 envs of
+// the XCD's share, at least 16 and at most 128 (kConEnv floats = 288 KB each: 295 MB at 65,536 envs, 37 MB at
+// 8,192), for the envs whose list is longer than the kMaxCon held on chip (a record for one substep each).
+int fused_pool_recs(int n) { return std::min(32 * kPoolWords, std::max(16, (n + 64 * kPoolXcd - 1) / (64 * kPoolXcd))); }
 hipError_t alloc_fused_workspace(int n, Workspace* w) {
   *w = Workspace{};
   const size_t ng = (size_t)(n + kEnvsPerBlock - 1) / kEnvsPerBlock;
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
   if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kConEnv * sizeof(float));
-  if (e == hipSuccess) e = hipMemset(w->con, 0, (size_t)n * kConEnv * sizeof(float));
+  w->pool_recs = fused_pool_recs(n);
+  if (e == hipSuccess) e = hipMalloc(&w->pool, (size_t)kPoolXcd * w->pool_recs * kConEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&w->pool_bm, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(w->pool_bm, 0, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->gcost, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->gcost, 0, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->order, ng * sizeof(int));

@@ -1109,6 +1109,60 @@ def test_overflow_contact_parity(solver, nsubstep, oracle64, oracle32):
             assert np.median(r.qv) <= 1e-4 and np.median(r.qa) <= 1e-4
 
 
+def test_pool_contention_bitwise(oracle64):
+    """The fused step's contact-record pool (round 5): an env whose list is longer than the 16 held on chip
+    takes an HBM record of its XCD's pool for the substep.  1,024 envs all holding 17-73 contacts (random folded arm
+    poses, tiled) against 128 records (16 per XCD at this size), so waves wait for records to come free: the fused
+    2- and 3-wave builds equal the split path and the debug build bit for bit over 3 env steps, and no contact is
+    dropped (the pool's safety valve never fires)."""
+    from gym_so100.model import build_model
+    model = build_model()
+    rng = np.random.default_rng(41)
+    lo_j = np.array([r[0] for r in model.jnt_range]); hi_j = np.array([r[1] for r in model.jnt_range])
+    lo, hi = np.array(model.action_lo[:]), np.array(model.action_hi[:])
+    d = oracle64.new_data()
+    states, targets = [], []
+    while len(states) < 64:
+        arm = rng.uniform(lo_j, hi_j)
+        oracle64.reset(model, d, np.array([0.4, 0.95, 0.6, 1, 0, 0, 0]))
+        for k in range(6):
+            d.qpos[k] = arm[k]
+        oracle64.call("so100o_fwd_position", model, d)
+        if d.ncon > 16:
+            q, v, w, _ = oracle64.get_state(d)
+            states.append((q, v * 0, w * 0))
+            targets.append(np.clip((arm - lo) / (hi - lo) * 2 - 1, -1, 1))
+    n = 1024
+    env = _new_env(n, "newton")
+    env.reset(seed=3)
+    _set_states(env, [states[i % len(states)] for i in range(n)])
+    act = np.array([targets[i % len(targets)] for i in range(n)], np.float32)
+    long_lists = []
+    for step in range(3):
+        _, _, ndrop, dbg, builds = _step_all_builds(env, act + rng.normal(0, 0.02, (n, 6)).astype(np.float32))
+        assert int(ndrop.sum()) == 0
+        long_lists.append(float((dbg[:, 0] > 16).mean()))
+    env.close()
+    print(f"\nbuilds {builds} == debug build, bitwise; share of envs with more than 16 contacts per step {long_lists}")
+    assert min(long_lists) > 0.5
+
+
+def test_contact_record_memory():
+    """The contact record by need (round 5): a 65,536-env fused-path env allocates its workspace (the record header, the
+    separating-direction cache and the contact-record pool: 8 XCDs x 128 records x 288 KB) in well under 2 GB (the
+    fixed per-env record of round 4 took 18.9 GB)."""
+    from gym_so100 import SO100VecEnv
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    env = SO100VecEnv(65536, device="cuda:0")
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    used = (free0 - free1) / 2 ** 30
+    env.close()
+    print(f"\n65,536 envs: {used:.2f} GiB of device memory (state tensors, workspace and the contact-record pool)")
+    assert used < 2.0
+
+
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
 def test_cube_on_base_parity(solver, oracle64, oracle32):
     """The cube resting on the static Base (pair 98, box vs the Base hull through MPR, one contact):
