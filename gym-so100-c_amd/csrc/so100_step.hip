@@ -1173,9 +1173,9 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       // the env's pool record back (its substep is done with it)
       int l2, g2, en2, e2;
       fresh_ids(group, args.n, l2, g2, en2, e2);
-      if (l2 == 0 && shm[g2].rec >= 0) {
-        pool_release(args.w, shm[g2].rec);
-        shm[g2].rec = -1;
+      if (l2 == 0) {
+        if (shm[g2].rec >= 0) pool_release(args.w, shm[g2].rec);
+        shm[g2].rec = -1;                 // (also after the safety valve's -2: the next substep tries again)
       }
     }
     TL_MARK(1);

@@ -167,7 +167,7 @@ class TF:
         self.qp, self.qv, self.fqp, self.fqv, self.qa, self.fqa = [], [], [], [], [], []
         # the ensemble floor (_tf_run ens=True): per env step the errors of ENS64 independent 1-ulp input perturbations
         # through the fp64 oracle and ENS32 more through the fp32 restatement, qvel and qacc [steps, ENS64 + ENS32] (fp64
-        # members first), and the fp64 members' contact forces (lists equal to the fp64 oracle's).  A fixed budget per
+        # members first), and the members' contact forces (lists equal to the fp64 oracle's).  A fixed budget per
         # state, run before and independently of the GPU's result: nothing in a floor depends on the error it grades
         self.eqv, self.eqa, self.eforce = [], [], []
         # (ens > 0) the fp32 restatement compiled with FMA contraction, as the GPU compiler contracts: a second fp32
@@ -273,7 +273,10 @@ def _tf_run(env, model, o64, o32, steps, act_fn, task=0, mocap=None, res=None, e
                     setm(d32, i)
                     o32.env_step(model, d32, task, act[i])
                     eq.append(_rel(o32.get_state(d32)[1], ov))
-                    ea.append(_rel(o32.last_solve(d32)[3], s64[3]))
+                    pe, fe, _, qae, _ = o32.last_solve(d32)
+                    ea.append(_rel(qae, s64[3]))
+                    if np.array_equal(pe, s64[0]) and len(pe):
+                        ef += list(_force_err(fe, s64[1]))
                 om = _oracle32fma()
                 dm = om.new_data()
                 om.set_state(dm, q0[i], v0[i], w0[i])
@@ -355,13 +358,16 @@ def _force_bars(r, median_abs=None):
     assert np.median(r.qa) <= 2 * r.floor("qa", 0.5) + 1e-6
     assert np.quantile(r.qa, 0.9) <= 2 * r.floor("qa", 0.9) + 1e-4
     if len(r.force):
-        # the force tail: the share of contacts off by more than 1e-4 and the p99, against the floors' (which the
-        # median / p90 bars above leave unbounded)
+        # the force tail (which the median / p90 bars above leave unbounded): the share of contacts off by more than
+        # 1e-4 against the floors' share; and, where the ensemble floor ran (its fp32 members' forces sample fp32
+        # rounding's own spread of a contact's force, which one fp32 run cannot: PGS stopped at 100 sweeps on resting
+        # contacts splits the force among redundant contacts by rounding), the p99 against the floors' p99
         share = lambda x: np.mean(np.asarray(x) > 1e-4) if np.size(x) else 0.0
         fshare = max(share(r.fforce), share(r.pforce), share(r.eforce))
         assert share(r.force) <= 1.5 * fshare + 0.03, (share(r.force), fshare)
-        assert np.quantile(r.force, 0.99) <= 2 * r.floor("force", 0.99) + 1e-3, (np.quantile(r.force, 0.99),
-                                                                                  r.floor("force", 0.99))
+        if len(r.eqv):
+            assert np.quantile(r.force, 0.99) <= 2 * r.floor("force", 0.99) + 1e-3, (np.quantile(r.force, 0.99),
+                                                                                      r.floor("force", 0.99))
 
 
 @pytest.mark.parametrize("solver", ["newton", "pgs"])
@@ -1314,7 +1320,9 @@ def test_product_builds_bitwise(n):
     ncon = np.concatenate(ncon)
     print(f"\n{n} envs x 10 steps, all builds bitwise equal: contacts/env mean {ncon.mean():.2f}, max {ncon.max()}, "
           f"envs > 8 contacts {(ncon > 8).mean():.3f}, MPR contacts {mpr}, auto-resets {resets}")
-    assert ncon.mean() > 2 and ncon.max() > 8 and mpr > 100 and resets >= n
+    # (contact-rich: 2.2 contacts per env before round 5, 1.96 since the table's edges and side faces collide exactly:
+    # a link hanging past the edge no longer takes a top-face contact)
+    assert ncon.mean() > 1.5 and ncon.max() > 8 and mpr > 100 and resets >= n
 
 
 @pytest.mark.parametrize("fused", [True, False])
