@@ -207,6 +207,9 @@ struct Workspace {
   float* pool;
   uint32_t* pool_bm;
   int pool_recs;
+  // split path, PGS: each env's sweep count in its last solve (so100_pgs_kernel); the next solve groups envs of like
+  // count into its 16-env waves (order: so100_pgs_order_kernel)
+  uint8_t* piters;
 };
 constexpr int kPoolXcd = 8;       // MI355X: 8 XCDs (HW_REG_XCC_ID), one pool each: a record stays in its XCD's L2
 constexpr int kPoolWords = 4;     // <= 128 records per XCD

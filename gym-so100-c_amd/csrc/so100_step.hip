@@ -1499,13 +1499,16 @@ hipError_t alloc_workspace(int n, Workspace* w) {
   if (e == hipSuccess) e = hipMemset(w->hcount, 0, 2 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&w->sep, (size_t)n * kSepPairs * sizeof(float4));
   if (e == hipSuccess) e = hipMemset(w->sep, 0, (size_t)n * kSepPairs * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&w->order, (size_t)n * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&w->piters, (size_t)n);
+  if (e == hipSuccess) e = hipMemset(w->piters, 0, (size_t)n);
   if (e != hipSuccess) (void)free_workspace(w);
   return e;
 }
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
   for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist, (void*)w->gcost,
-                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm}) {
+                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm, (void*)w->piters}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
@@ -1516,6 +1519,7 @@ hipError_t free_workspace(Workspace* w) {
   w->sep = nullptr;
   w->pool = nullptr;
   w->pool_bm = nullptr;
+  w->piters = nullptr;
   return r;
 }
 // The fused path's workspace: the record header (only its contact counts are written), the wave-order buffers,

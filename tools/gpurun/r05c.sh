@@ -1,4 +1,5 @@
-# round 5: the GPU suite on the pool kernels (contact record by need), bench lines at 65,536 / 16,384 / 8,192 envs,
+# round 5: the GPU suite on the pool kernels (contact record by need), bench lines at 65,536 / 16,384 / 8,192 envs, a
+# same-box A/B of the PGS env order (SO100_PGS_ORDER=0: round 4's dispatch),
 # rocprofv3 kernel stats, per-step PMC traffic at the three sizes (with the library's source hash), the wave timeline
 # and the stage / Newton stamps at 8,192 envs
 export TMPDIR=/tmp
@@ -11,6 +12,10 @@ if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
 for n in 16384 8192; do
   timeout -k 10 300 python bench.py --total-envs $n --no-cpu-baseline > $O/bench_$n.json 2> $O/bench_$n.err || exit $?
+done
+for r in 1 2; do
+  SO100_PGS_ORDER=0 timeout -k 10 300 python bench.py --solver pgs --no-cpu-baseline --steps 100 --contact-steps 0 > $O/pgs_noorder_$r.json 2> $O/pgs_noorder_$r.err || exit $?
+  timeout -k 10 300 python bench.py --solver pgs --no-cpu-baseline --steps 100 --contact-steps 0 > $O/pgs_order_$r.json 2> $O/pgs_order_$r.err || exit $?
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o bench --output-format csv -- python bench.py --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_fused -o fused8192 --output-format csv -- python bench.py --total-envs 8192 --steps 60 --warmup 30 --no-cpu-baseline --contact-steps 2 > $O/trace_fused.log 2>&1 || exit $?
