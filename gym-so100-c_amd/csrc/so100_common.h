@@ -154,13 +154,15 @@ DEV int qcqp3_eig(float* x, const float* P, const float* lam, const float* lamin
       const float val = s - r * r;
       if (val < 1e-10f) break;
       const float t = w[0] * w[0] * d[0] + w[1] * w[1] * d[1] + w[2] * w[2] * d[2];
-      const float delta = val / (2.f * t);
+      // (hardware reciprocals, 1 ulp, on the iteration's serial chain: one v_rcp each instead of the IEEE division
+      // sequence, as the Newton solve's chains since round 3; round 5, PGS)
+      const float delta = val * __builtin_amdgcn_rcpf(2.f * t);
       if (delta < 1e-10f) break;
       nit++;
       la += delta;
       if (it == 19) break;
 #pragma unroll
-      for (int i = 0; i < 3; i++) { d[i] = 1.f / (lam[i] + la); w[i] = c[i] * d[i]; }
+      for (int i = 0; i < 3; i++) { d[i] = __builtin_amdgcn_rcpf(lam[i] + la); w[i] = c[i] * d[i]; }
       s = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     }
   }

@@ -1248,7 +1248,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
       if (it < total && ((hb >> (16 * g)) & 1ull)) fnew += 1u << (8 * env_of(it));
     }
     // fused path: an env whose staged contacts pass kMaxCon takes its pool record before they are staged there
-    if constexpr (kCells) (void)ensure_rec<true>(w, shm[grp], lane, valid, (int)((fnew >> (8 * grp)) & 0xFFu), nullptr);
+    if constexpr (kCells) (void)ensure_rec<true>(w, shm, grp, lane, valid, (int)((fnew >> (8 * grp)) & 0xFFu), nullptr);
     int slot = (int)((fpk >> (8 * ie)) & 0xFFu);
 #pragma unroll
     for (int g = 0; g < kEnvsPerBlock; g++) {
@@ -1260,7 +1260,7 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
       // the env's record: the split path's per-env record (crec0: the wave's first env's), or the fused path's pool
       // record (crec0: the pool) if the env holds one (else its contacts beyond kMaxCon are not stored: assemble
       // collides again with a record)
-      float* const rb = kCells ? pool_rec(w, shm[ie].rec) : crec0 + (size_t)ie * kConEnv;
+      float* const rb = kCells ? pool_rec(w, shm[0].rec, ie) : crec0 + (size_t)ie * kConEnv;
       stage_convex_hit(m, shm[ie], rb, slot, p, depth, dir, pos);
     }
     fpk = fnew;

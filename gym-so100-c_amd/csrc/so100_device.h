@@ -200,9 +200,10 @@ struct Workspace {
   // substep re-checks with one support evaluation before it runs GJK (results unchanged: mpr_contacts)
   float4* sep;
   // fused path: the contact records of the envs whose list is longer than the kMaxCon held on chip (every contact
-  // beyond them: geometry, J, the rows and the Newton solve's per-contact state; kConEnv floats each), a pool per XCD
-  // with a free bitmap (pool_bm[xcd * kPoolWords ..]).  A wave's env takes one for a substep when its list exceeds
-  // kMaxCon and returns it after the solve (so100_step.hip pool_acquire / pool_release); pool_recs records per XCD.
+  // beyond them: geometry, J, the rows and the Newton solve's per-contact state; kConEnv floats each), a pool of
+  // entries (a wave's kEnvsPerBlock records) per XCD with a free bitmap (pool_bm[xcd * kPoolWords ..]).  A wave takes
+  // one for a substep when one of its envs' lists passes kMaxCon and returns it after the solve (so100_pool.h);
+  // pool_recs entries per XCD.
   // The split path keeps its per-env record in con.
   float* pool;
   uint32_t* pool_bm;
@@ -212,7 +213,7 @@ struct Workspace {
   uint8_t* piters;
 };
 constexpr int kPoolXcd = 8;       // MI355X: 8 XCDs (HW_REG_XCC_ID), one pool each: a record stays in its XCD's L2
-constexpr int kPoolWords = 4;     // <= 128 records per XCD
+constexpr int kPoolWords = 4;     // <= 128 entries per XCD
 constexpr int kPoolSlots = 32 * kPoolWords;   // a pool id: XCD x kPoolSlots + bitmap entry
 
 }  // namespace so100

@@ -333,7 +333,8 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
 #endif
   // ---------------- qacc -> HBM (the next stage's Euler input and the next substep's warmstart)
   if (valid) {
-    if (q == 0 && a.w.piters) a.w.piters[env] = (uint8_t)min(iters, 255);
+    // the env's ordering key for the next solve: its sweeps (and whether its contacts stream from HBM) this time
+    if (q == 0 && a.w.piters) a.w.piters[env] = (uint8_t)((ncon > kResident ? 128 : 0) | min(iters, 127));
 #pragma unroll
     for (int i = 0; i < 3; i++) a.qacc_out[(size_t)env * SO100_NV + 3 * q + i] = qacc[i];
     if (a.last && a.debug) {
@@ -364,26 +365,35 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
   }
 }
 
-// The PGS waves' env order: a counting sort of the envs on their last solve's sweep count (min(iters, 127)), envs with
-// more than kResident contacts (streamed from HBM every sweep) before all others, the costliest first, one workgroup.
+// The PGS waves' env order: a counting sort of the envs on the key their last solve wrote (its sweep count min(iters,
+// 127), + 128 when its contacts beyond kResident streamed from HBM), the costliest first, one workgroup reading one
+// byte per env.
 // A wave of 16 envs runs until its slowest env converges (MuJoCo's improvement-based exit), and an env's sweep count
 // persists from substep to substep: measured on the bench workload (fp32 oracle, random actions), the envs' mean is 8
 // sweeps but a wave of 16 consecutive envs runs 24.  The order changes the schedule, never a result.
 constexpr int kPgsBuckets = 256;
-__global__ void __launch_bounds__(1024) so100_pgs_order_kernel(const float* __restrict__ hdr,
-                                                               const uint8_t* __restrict__ piters, int n,
+__global__ void __launch_bounds__(1024) so100_pgs_order_kernel(const uint8_t* __restrict__ pkey, int n,
                                                                int* __restrict__ order) {
   __shared__ int hist[kPgsBuckets];
   __shared__ int part[1024];
   const int t = threadIdx.x;
-  auto key = [&](int e) {
-    const int ncon = __float_as_int(hdr[(size_t)e * kHdrEnv + H_NCON]);
-    const int k = (ncon > kResident ? 128 : 0) | min((int)piters[e], 127);
-    return (kPgsBuckets - 1) - k;                 // descending cost
-  };
+  const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   // lane in the wave
+  const uint64_t below = (1ull << ln) - 1ull;
+  // keys concentrate in a few buckets (most envs converge in 2 sweeps): one LDS atomic per distinct key in each
+  // wave, not per env (same-address LDS atomics serialise)
   for (int b = t; b < kPgsBuckets; b += 1024) hist[b] = 0;
   __syncthreads();
-  for (int e = t; e < n; e += 1024) atomicAdd(&hist[key(e)], 1);
+  for (int e0 = 0; e0 < n; e0 += 1024) {
+    const int e = e0 + t;
+    const bool act = e < n;
+    const int k = act ? (kPgsBuckets - 1) - (int)pkey[e] : 0;     // descending cost
+    for (uint64_t rem = __ballot(act); rem != 0ull;) {
+      const int kl = __builtin_amdgcn_readlane(k, __builtin_ctzll(rem));
+      const uint64_t m = __ballot(act && k == kl);
+      if (act && k == kl && (m & below) == 0ull) atomicAdd(&hist[kl], __popcll(m));
+      rem &= ~m;
+    }
+  }
   __syncthreads();
   const int c = t < kPgsBuckets ? hist[t] : 0;
   part[t] = c;
@@ -396,7 +406,21 @@ __global__ void __launch_bounds__(1024) so100_pgs_order_kernel(const float* __re
   }
   if (t < kPgsBuckets) hist[t] = part[t] - c;
   __syncthreads();
-  for (int e = t; e < n; e += 1024) order[atomicAdd(&hist[key(e)], 1)] = e;
+  for (int e0 = 0; e0 < n; e0 += 1024) {
+    const int e = e0 + t;
+    const bool act = e < n;
+    const int k = act ? (kPgsBuckets - 1) - (int)pkey[e] : 0;
+    for (uint64_t rem = __ballot(act); rem != 0ull;) {
+      const int leader = __builtin_ctzll(rem);
+      const int kl = __builtin_amdgcn_readlane(k, leader);
+      const uint64_t m = __ballot(act && k == kl);
+      int base = 0;
+      if (ln == leader) base = atomicAdd(&hist[kl], __popcll(m));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if (act && k == kl) order[base + __popcll(m & below)] = e;
+      rem &= ~m;
+    }
+  }
 }
 
 hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last, int par,
@@ -406,7 +430,7 @@ hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, fl
   static const bool order_on = !(getenv("SO100_PGS_ORDER") && getenv("SO100_PGS_ORDER")[0] == '0');
   const bool ordered = order_on && w.order && w.piters;
   if (ordered) {
-    hipLaunchKernelGGL(so100_pgs_order_kernel, dim3(1), dim3(1024), 0, s, w.hdr, w.piters, n, w.order);
+    hipLaunchKernelGGL(so100_pgs_order_kernel, dim3(1), dim3(1024), 0, s, w.piters, n, w.order);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

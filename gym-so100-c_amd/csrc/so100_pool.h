@@ -7,13 +7,15 @@
 
 namespace so100 {
 
-// The fused path's contact-record pool (Workspace::pool): a record per env whose list is longer than the kMaxCon held on
-// chip, taken for one substep from the pool of the wave's XCD (its L2 holds every access of the record: no cross-XCD
-// coherence is needed) and returned after the solve.  pool_acquire (lane 0 of the env's row): the lowest free record
-// of this XCD's bitmap; with none free it sleeps and retries: every holder is a running wave that returns its record
-// at the end of its substep, and a waiting wave holds none, so one comes free.  After kPoolSpins tries (about a second,
-// never reached in any measured run) it gives up: -2, and the env keeps its first kMaxCon contacts, counted in
-// ncon_dropped (a checked invariant: every test asserts 0).
+// The fused path's contact-record pool (Workspace::pool): entries of kEnvsPerBlock records, one per env of a wave, taken
+// by a wave for one substep the first time one of its envs' contact list passes kMaxCon, from the pool of the wave's
+// XCD (its L2 holds every access of the entry: no cross-XCD coherence is needed), and returned after the solve.  A wave
+// holds at most one entry and takes it whole, so it never waits while holding one: pool_acquire (one lane of the wave)
+// takes the lowest free entry of this XCD's bitmap; with none free it sleeps and retries, and every holder is a running
+// wave that returns its entry at the end of its substep, so one comes free.  (Per-env records, round 5's first cut,
+// deadlocked under contention: a wave holding one env's record waited for another's.)  After kPoolSpins tries (about
+// a second, never reached in any measured run) it gives up: -2, and the envs keep their first kMaxCon contacts, counted
+// in ncon_dropped (a checked invariant: every test asserts 0).
 constexpr int kPoolSpins = 1 << 22;
 DEV int xcc_id() {
   int x;
@@ -40,32 +42,34 @@ DEV int pool_acquire(const Workspace& w) {
   }
   return -2;
 }
-// the record of pool id rec (XCD rec / kPoolSlots, entry rec % kPoolSlots of its bitmap), or nullptr for rec < 0
-DEV float* pool_rec(const Workspace& w, int rec) {
-  if (rec < 0) return nullptr;
-  const int x = rec / kPoolSlots, b = rec % kPoolSlots;
-  return w.pool + ((size_t)x * w.pool_recs + b) * kConEnv;
+// env grp's record in pool entry `ent` (XCD ent / kPoolSlots, bit ent % kPoolSlots of its bitmap), or nullptr for
+// ent < 0 (no entry held)
+DEV float* pool_rec(const Workspace& w, int ent, int grp) {
+  if (ent < 0) return nullptr;
+  const int x = ent / kPoolSlots, b = ent % kPoolSlots;
+  return w.pool + (((size_t)x * w.pool_recs + b) * kEnvsPerBlock + grp) * kConEnv;
 }
-DEV void pool_release(const Workspace& w, int rec) {
-  __builtin_amdgcn_s_waitcnt(0);    // the substep's stores to the record have reached L2 before another wave may take it
-  const int x = rec / kPoolSlots, b = rec % kPoolSlots;
+DEV void pool_release(const Workspace& w, int ent) {
+  __builtin_amdgcn_s_waitcnt(0);    // the substep's stores to the entry have reached L2 before another wave may take it
+  const int x = ent / kPoolSlots, b = ent % kPoolSlots;
   atomicAnd(w.pool_bm + x * kPoolWords + (b >> 5), ~(1u << (b & 31)));
 }
 // The env's record for a list about to reach `total` contacts (every lane of the wave calls it; the envs' counts are
-// uniform in their rows): the split path's per-env record as given; on the fused path an env whose list passes kMaxCon
-// takes a pool record first (lane 0 of its row), and its lanes read it back (nullptr: none held; sh.rec -1: none yet,
-// -2: the pool's safety valve).  Collision calls it before each phase stores its contacts, with that phase's total.
+// uniform in their rows): the split path's per-env record as given; on the fused path, when an env's list passes
+// kMaxCon and its wave holds no entry, the wave takes one (shm[0].rec: the wave's entry; -1: none yet, -2: the pool's
+// safety valve), and the env's lanes read back its record (nullptr: none).  Collision calls it before each phase stores
+// its contacts, with that phase's total.  shm: the wave's 4 envs.
 template <bool kFused>
-DEV float* ensure_rec(const Workspace& w, EnvShared& sh, int lane, bool valid, int total, float* crec) {
+DEV float* ensure_rec(const Workspace& w, EnvShared* shm, int grp, int lane, bool valid, int total, float* crec) {
   if constexpr (!kFused) {
     return crec;
   } else {
-    const bool need = valid && total > kMaxCon && sh.rec == -1;
+    const bool need = valid && total > kMaxCon;
     if (__ballot(need) != 0ull) {
-      if (need && lane == 0) sh.rec = pool_acquire(w);
+      if (lane == 0 && grp == 0 && shm[0].rec == -1) shm[0].rec = pool_acquire(w);
       __syncthreads();
     }
-    return pool_rec(w, sh.rec);
+    return pool_rec(w, shm[0].rec, grp);
   }
 }
 

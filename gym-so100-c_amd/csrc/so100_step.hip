@@ -340,7 +340,7 @@ DEV int pad_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
     int off = 0, sum = 0;
 #pragma unroll
     for (int k = 0; k < kLanes; k++) { const int c = sh.cnt[k]; off += (k < lane) ? c : 0; sum += c; }
-    crec = ensure_rec<kFused>(w, sh, lane, valid, tot + sum, crec);
+    crec = ensure_rec<kFused>(w, &sh - grp, grp, lane, valid, tot + sum, crec);
     put_box_contacts(sh, crec, pc, tot + off, p);
     tot += sum;
     __syncthreads();
@@ -423,7 +423,7 @@ DEV void collide(const DevModel* __restrict__ m, const Workspace& w, float* recb
 #pragma unroll
     for (int k = 0; k < 16; k++) { int c = sh.cnt[k]; off += (k < lane) ? c : 0; tot += c; }
     // the box, table-hull and convex contacts' total is known here, before any of them is stored
-    crec = ensure_rec<kFused>(w, sh, lane, valid, tot + __popc(hrow) + nmpr, crec);
+    crec = ensure_rec<kFused>(w, &sh - grp, grp, lane, valid, tot + __popc(hrow) + nmpr, crec);
     put_box_contacts(sh, crec, pc, off, lane);
     const int hslot = tot + __popc(hrow & ((1u << lane) - 1u));
     if (hfound) {
@@ -506,12 +506,14 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
     collide<kFused>(m, args.w, recbase, sep, sh, lane, grp, valid, crec SSTAMP_PASS);
     // the env's record from here on, recomputed at each use (the contacts beyond kMaxCon are rare): not a pointer held
     // across the rows and the solve (the 3-wave build spilled it)
-    auto recp = [&]() -> float* { return kFused ? pool_rec(args.w, sh.rec) : args.w.con + (size_t)e * kConEnv; };
+    auto recp = [&]() -> float* {
+      return kFused ? pool_rec(args.w, (&sh - grp)->rec, grp) : args.w.con + (size_t)e * kConEnv;
+    };
     if constexpr (!kFused) {
       if (valid && lane == 0 && B.ncon_dropped && sub == 0) B.ncon_dropped[env] = 0u;
     } else {
       // (the pool's safety valve, never reached in a measured run) no record came free: the first kMaxCon contacts
-      if (valid && lane == 0 && sh.ncon > kMaxCon && sh.rec < 0) {
+      if (valid && lane == 0 && sh.ncon > kMaxCon && (&sh - grp)->rec < 0) {
         sh.ndrop += sh.ncon - kMaxCon;
         sh.ncon = launder_v(kMaxCon);     // (a constant materialised here: not one held from the kernel entry)
       }
@@ -1113,7 +1115,7 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
   load_state(args, lane, e, qpos_r, qvel_r, warm_r, mscale, fscale, sigma, elapsed0, episode0);
   set_controls(args, sh, lane, e, sigma, elapsed0, episode0);
   if (lane == 0) {
-    sh.rec = -1;                  // no pool contact record held
+    sh.rec = -1;                  // no pool entry held (the wave's: shm[0].rec)
     sh.ndrop = 0;                 // contacts left out over the step (the pool's safety valve only)
   }
   const int nsub = args.m->nsubstep;
@@ -1159,7 +1161,7 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     auto rec = [&]() -> float* {
       int l2, g2, en2, e2;
       fresh_ids(group, args.n, l2, g2, en2, e2);
-      return pool_rec(args.w, shm[g2].rec);
+      return pool_rec(args.w, shm[0].rec, g2);
     };
     const float qacc = newton_solve_any(sa.m, nr, lane, valid, dbg, diag, rec);
     if (dbg) {
@@ -1173,9 +1175,9 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       // the env's pool record back (its substep is done with it)
       int l2, g2, en2, e2;
       fresh_ids(group, args.n, l2, g2, en2, e2);
-      if (l2 == 0) {
-        if (shm[g2].rec >= 0) pool_release(args.w, shm[g2].rec);
-        shm[g2].rec = -1;                 // (also after the safety valve's -2: the next substep tries again)
+      if (l2 == 0 && g2 == 0) {
+        if (shm[0].rec >= 0) pool_release(args.w, shm[0].rec);
+        shm[0].rec = -1;                  // (also after the safety valve's -2: the next substep tries again)
       }
     }
     TL_MARK(1);
@@ -1523,17 +1525,17 @@ hipError_t free_workspace(Workspace* w) {
   return r;
 }
 // The fused path's workspace: the record header (only its contact counts are written), the wave-order buffers,
-// the separating-direction cache, and the contact-record pool (Workspace::pool): per XCD one record per 64 envs of
-// the XCD's share, at least 16 and at most 128 (kConEnv floats = 288 KB each: 295 MB at 65,536 envs, 37 MB at
-// 8,192), for the envs whose list is longer than the kMaxCon held on chip (a record for one substep each).
-int fused_pool_recs(int n) { return std::min(32 * kPoolWords, std::max(16, (n + 64 * kPoolXcd - 1) / (64 * kPoolXcd))); }
+// the separating-direction cache, and the contact-record pool (Workspace::pool): per XCD one entry (a wave's 4 records
+// of kConEnv floats, 288 KB each) per 256 envs of the XCD's share, at least 8 and at most 32 (295 MB at 65,536 envs,
+// 74 MB at 8,192), for the waves holding an env whose list is longer than the kMaxCon held on chip (for one substep).
+int fused_pool_recs(int n) { return std::min(32, std::max(8, (n + 256 * kPoolXcd - 1) / (256 * kPoolXcd))); }
 hipError_t alloc_fused_workspace(int n, Workspace* w) {
   *w = Workspace{};
   const size_t ng = (size_t)(n + kEnvsPerBlock - 1) / kEnvsPerBlock;
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
   if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
   w->pool_recs = fused_pool_recs(n);
-  if (e == hipSuccess) e = hipMalloc(&w->pool, (size_t)kPoolXcd * w->pool_recs * kConEnv * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&w->pool, (size_t)kPoolXcd * w->pool_recs * kEnvsPerBlock * kConEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->pool_bm, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->pool_bm, 0, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->gcost, ng * sizeof(uint32_t));
