@@ -186,6 +186,7 @@ constexpr int kResident = 4;      // solver: contacts per env held on-chip acros
 constexpr int kHeavyCap = 512;    // solver: groups with > kResident contacts dispatched first (cap)
 struct Workspace {
   float* hdr;
+  int hdr_stride;   // floats per env of hdr: kHdrEnv (the split path's record headers), 1 (the fused path: its counts)
   float* con;
   // heavy-group list, double-buffered by substep parity: the stage kernel flags/list groups holding an
   // env with more than kResident contacts, the solver dispatches those first and clears the other set
@@ -208,9 +209,6 @@ struct Workspace {
   float* pool;
   uint32_t* pool_bm;
   int pool_recs;
-  // split path, PGS: each env's sweep count in its last solve (so100_pgs_kernel); the next solve groups envs of like
-  // count into its 16-env waves (order: so100_pgs_order_kernel)
-  uint8_t* piters;
 };
 constexpr int kPoolXcd = 8;       // MI355X: 8 XCDs (HW_REG_XCC_ID), one pool each: a record stays in its XCD's L2
 constexpr int kPoolWords = 4;     // <= 128 entries per XCD

@@ -14,7 +14,6 @@
 //     sweeps; further contacts (rare: >4 per env; the list holds up to kConCap) stream both from the HBM
 //     record every sweep, loaded at use so the register peak stays at 168 (3 waves/SIMD), forces written
 //     back to the record.
-#include <cstdlib>
 #include "so100_common.h"
 #include "so100.h"
 
@@ -25,7 +24,6 @@ constexpr int kPgsWaves = 3;         // waves per SIMD the register budget is si
 struct PgsArgs {
   const DevModel* m;
   Workspace w;
-  const int* order;              // the envs in wave order (so100_pgs_order_kernel), or nullptr
   float* qacc_out;               // so100_buffers.qacc_warmstart: the solver's qacc (next warmstart)
   float* debug;
   int n;
@@ -86,22 +84,19 @@ DEV void contact_update(const float4 (&v)[kBlk], const float4 (&J)[3], float (&q
   float g[3], gp[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) g[i] = (J[i].x * dl[0] + J[i].y * dl[1]) + (J[i].z * dl[2] + J[i].w * dl[3]);
-  // the diagonal term first, as the cube-only shortcut computes it, then the rest of the row: for an env whose contact is
-  // cube-only the rest is exact zeros, so both paths give it the same bits whichever path its wave takes (the wave's
-  // envs are grouped by sweep count, so100_pgs_order_kernel: an env's results must not depend on its wave-mates)
+  if (!arm) {
+    // cube-only contact (table / bin): J has no arm entries, the arm lanes' g is 0 and the cube block
+    // of M^-1 is diagonal: the full update below reduces to this exactly
 #pragma unroll
-  for (int i = 0; i < 3; i++) qacc[i] += mrow[i][i] * g[i];
-  if (!arm) return;   // cube-only contacts (table / bin) in every env of the wave: J has no arm entries, the cube block
-                      // of M^-1 is diagonal, the rest of the update is zero
+    for (int i = 0; i < 3; i++) qacc[i] += mrow[i][i] * g[i];
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 3; i++) gp[i] = quad_swap1(g[i]);
 #pragma unroll
-  for (int i = 0; i < 3; i++) {
-    float off = (mrow[i][3] * gp[0] + mrow[i][4] * gp[1]) + mrow[i][5] * gp[2];
-#pragma unroll
-    for (int j = 0; j < 3; j++) off += j == i ? 0.f : mrow[i][j] * g[j];
-    qacc[i] += off;
-  }
+  for (int i = 0; i < 3; i++)
+    qacc[i] += (mrow[i][0] * g[0] + mrow[i][1] * g[1] + mrow[i][2] * g[2]) +
+               (mrow[i][3] * gp[0] + mrow[i][4] * gp[1] + mrow[i][5] * gp[2]);
 
 }
 
@@ -111,20 +106,11 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
   const int tid = threadIdx.x;
   const int q = tid & 3;
   const int ew = tid >> 2;
-  // Env order (round 5): the wave's 16 envs are order[16 b ..] (so100_pgs_order_kernel: envs grouped by their last
-  // solve's sweep count, the costliest first), so a wave's sweeps are not set by one slow env among fast ones; its
-  // per-env results do not depend on the grouping.  Without an order (the round-4 dispatch): groups of 16 consecutive
-  // envs, those holding an env with many contacts in the leading blocks so their tail overlaps the bulk (the in-place
-  // block of a listed group exits).
+  // groups holding an env with many contacts take longest: they run in the leading blocks so their
+  // tail overlaps the bulk; the in-place block of a listed group exits
   const int ngroups = (a.n + kPgsEnvs - 1) / kPgsEnvs;
   int grp;
-  if (a.order) {
-    grp = blockIdx.x;
-    if (tid == 0) {
-      a.w.gflag[(a.par ^ 1) * ngroups + grp] = 0u;      // (the stage kernel's heavy-group lists: kept consistent)
-      if (grp == 0) a.w.hcount[a.par ^ 1] = 0;
-    }
-  } else if ((int)blockIdx.x < a.nheavy_slots) {
+  if ((int)blockIdx.x < a.nheavy_slots) {
     const int cnt = min(a.w.hcount[a.par], kHeavyCap);
     if ((int)blockIdx.x >= cnt) return;
     grp = a.w.hlist[a.par * kHeavyCap + blockIdx.x];
@@ -136,9 +122,8 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
     }
     if (a.w.gflag[a.par * ngroups + grp] == 1u) return;
   }
-  const int slot = grp * kPgsEnvs + ew;
-  const bool valid = slot < a.n;
-  const int env = !valid ? slot : a.order ? a.order[slot] : slot;
+  const int env = grp * kPgsEnvs + ew;
+  const bool valid = env < a.n;
   const int e = valid ? env : 0;
   STAMP_DECL
   STAMP(-1);
@@ -333,8 +318,6 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
 #endif
   // ---------------- qacc -> HBM (the next stage's Euler input and the next substep's warmstart)
   if (valid) {
-    // the env's ordering key for the next solve: its sweeps (and whether its contacts stream from HBM) this time
-    if (q == 0 && a.w.piters) a.w.piters[env] = (uint8_t)((ncon > kResident ? 128 : 0) | min(iters, 127));
 #pragma unroll
     for (int i = 0; i < 3; i++) a.qacc_out[(size_t)env * SO100_NV + 3 * q + i] = qacc[i];
     if (a.last && a.debug) {
@@ -365,77 +348,11 @@ __global__ void __launch_bounds__(64, kPgsWaves) so100_pgs_kernel(PgsArgs a) {
   }
 }
 
-// The PGS waves' env order: a counting sort of the envs on the key their last solve wrote (its sweep count min(iters,
-// 127), + 128 when its contacts beyond kResident streamed from HBM), the costliest first, one workgroup reading one
-// byte per env.
-// A wave of 16 envs runs until its slowest env converges (MuJoCo's improvement-based exit), and an env's sweep count
-// persists from substep to substep: measured on the bench workload (fp32 oracle, random actions), the envs' mean is 8
-// sweeps but a wave of 16 consecutive envs runs 24.  The order changes the schedule, never a result.
-constexpr int kPgsBuckets = 256;
-__global__ void __launch_bounds__(1024) so100_pgs_order_kernel(const uint8_t* __restrict__ pkey, int n,
-                                                               int* __restrict__ order) {
-  __shared__ int hist[kPgsBuckets];
-  __shared__ int part[1024];
-  const int t = threadIdx.x;
-  const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   // lane in the wave
-  const uint64_t below = (1ull << ln) - 1ull;
-  // keys concentrate in a few buckets (most envs converge in 2 sweeps): one LDS atomic per distinct key in each
-  // wave, not per env (same-address LDS atomics serialise)
-  for (int b = t; b < kPgsBuckets; b += 1024) hist[b] = 0;
-  __syncthreads();
-  for (int e0 = 0; e0 < n; e0 += 1024) {
-    const int e = e0 + t;
-    const bool act = e < n;
-    const int k = act ? (kPgsBuckets - 1) - (int)pkey[e] : 0;     // descending cost
-    for (uint64_t rem = __ballot(act); rem != 0ull;) {
-      const int kl = __builtin_amdgcn_readlane(k, __builtin_ctzll(rem));
-      const uint64_t m = __ballot(act && k == kl);
-      if (act && k == kl && (m & below) == 0ull) atomicAdd(&hist[kl], __popcll(m));
-      rem &= ~m;
-    }
-  }
-  __syncthreads();
-  const int c = t < kPgsBuckets ? hist[t] : 0;
-  part[t] = c;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {           // inclusive scan of the bucket counts
-    const int v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  if (t < kPgsBuckets) hist[t] = part[t] - c;
-  __syncthreads();
-  for (int e0 = 0; e0 < n; e0 += 1024) {
-    const int e = e0 + t;
-    const bool act = e < n;
-    const int k = act ? (kPgsBuckets - 1) - (int)pkey[e] : 0;
-    for (uint64_t rem = __ballot(act); rem != 0ull;) {
-      const int leader = __builtin_ctzll(rem);
-      const int kl = __builtin_amdgcn_readlane(k, leader);
-      const uint64_t m = __ballot(act && k == kl);
-      int base = 0;
-      if (ln == leader) base = atomicAdd(&hist[kl], __popcll(m));
-      base = __builtin_amdgcn_readlane(base, leader);
-      if (act && k == kl) order[base + __popcll(m & below)] = e;
-      rem &= ~m;
-    }
-  }
-}
-
 hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last, int par,
                       hipStream_t s) {
   const int ngroups = (n + kPgsEnvs - 1) / kPgsEnvs;
-  // SO100_PGS_ORDER=0: the round-4 dispatch (consecutive envs per wave, heavy groups first), for same-box A/Bs
-  static const bool order_on = !(getenv("SO100_PGS_ORDER") && getenv("SO100_PGS_ORDER")[0] == '0');
-  const bool ordered = order_on && w.order && w.piters;
-  if (ordered) {
-    hipLaunchKernelGGL(so100_pgs_order_kernel, dim3(1), dim3(1024), 0, s, w.piters, n, w.order);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  const int heavy = ordered ? 0 : ngroups < kHeavyCap ? ngroups : kHeavyCap;
-  PgsArgs a{m, w, ordered ? w.order : nullptr, qacc_out, debug, n, last, par, heavy};
+  const int heavy = ngroups < kHeavyCap ? ngroups : kHeavyCap;
+  PgsArgs a{m, w, qacc_out, debug, n, last, par, heavy};
   hipLaunchKernelGGL(so100_pgs_kernel, dim3(ngroups + heavy), dim3(64), 0, s, a);
   return hipGetLastError();
 }

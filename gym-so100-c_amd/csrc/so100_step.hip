@@ -671,8 +671,9 @@ DEV void assemble(const StageArgs& args, EnvShared& sh, int lane, int grp, int e
         if constexpr (!kFused) {
           newton_rows_store(args.w, e, lane, nr);
         } else {
-          // the contact counter (so100_contact_count) reads the last substep's count from the record
-          if (lane == 0 && sub == m->nsubstep - 1) args.w.hdr[(size_t)e * kHdrEnv + H_NCON] = __int_as_float(ncon);
+          // the contact counter (so100_contact_count) reads the last substep's count: the fused workspace's header is
+          // one float per env (a 4-B store per env step, where the strided record header dirtied a whole line each)
+          if (lane == 0 && sub == m->nsubstep - 1) args.w.hdr[e] = __int_as_float(ncon);
         }
         SSTAMP(5);
 #ifdef SO100_STAGE_STAMPS
@@ -1444,11 +1445,13 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, i
 }
 
 // Sum of the contact counts in the solver records of the last substep (H_NCON of lane-0 records).
-__global__ void so100_contact_count_kernel(const float* __restrict__ hdr, int n, unsigned long long* accum) {
+// (hdr: the split path's record headers, stride kHdrEnv, or the fused path's compact counts, stride 1)
+__global__ void so100_contact_count_kernel(const float* __restrict__ hdr, int n, int stride, unsigned long long* accum) {
   __shared__ int part[256];
   int s = 0;
+  const int off = stride == 1 ? 0 : H_NCON;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-    s += __float_as_int(hdr[(size_t)i * kHdrEnv + H_NCON]);
+    s += __float_as_int(hdr[(size_t)i * stride + off]);
   part[threadIdx.x] = s;
   __syncthreads();
   for (int d = 128; d > 0; d >>= 1) {
@@ -1469,18 +1472,18 @@ extern "C" int so100_dev_epa_cycles(unsigned long long* out, int reset) {
 }
 namespace so100 {
 #endif
-__global__ void so100_contact_counts_kernel(const float* __restrict__ hdr, int n, int32_t* __restrict__ out) {
+__global__ void so100_contact_counts_kernel(const float* __restrict__ hdr, int n, int stride, int32_t* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] = __float_as_int(hdr[(size_t)i * kHdrEnv + H_NCON]);
+  if (i < n) out[i] = __float_as_int(hdr[(size_t)i * stride + (stride == 1 ? 0 : H_NCON)]);
 }
 hipError_t launch_contact_counts(const Workspace& w, int n, int32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(so100_contact_counts_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w.hdr, n, out);
+  hipLaunchKernelGGL(so100_contact_counts_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w.hdr, n, w.hdr_stride, out);
   return hipGetLastError();
 }
 hipError_t launch_contact_count(const Workspace& w, int n, uint64_t* accum, hipStream_t s) {
   int blocks = (n + 255) / 256;
   if (blocks > 256) blocks = 256;
-  hipLaunchKernelGGL(so100_contact_count_kernel, dim3(blocks), dim3(256), 0, s, w.hdr, n,
+  hipLaunchKernelGGL(so100_contact_count_kernel, dim3(blocks), dim3(256), 0, s, w.hdr, n, w.hdr_stride,
                      reinterpret_cast<unsigned long long*>(accum));
   return hipGetLastError();
 }
@@ -1488,6 +1491,7 @@ hipError_t launch_contact_count(const Workspace& w, int n, uint64_t* accum, hipS
 hipError_t free_workspace(Workspace* w);
 hipError_t alloc_workspace(int n, Workspace* w) {
   *w = Workspace{};
+  w->hdr_stride = kHdrEnv;
   hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->con, (size_t)n * kConEnv * sizeof(float));
   // zero once: record slots a solver lane reads but never uses are then finite, never garbage
@@ -1501,16 +1505,13 @@ hipError_t alloc_workspace(int n, Workspace* w) {
   if (e == hipSuccess) e = hipMemset(w->hcount, 0, 2 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&w->sep, (size_t)n * kSepPairs * sizeof(float4));
   if (e == hipSuccess) e = hipMemset(w->sep, 0, (size_t)n * kSepPairs * sizeof(float4));
-  if (e == hipSuccess) e = hipMalloc(&w->order, (size_t)n * sizeof(int));
-  if (e == hipSuccess) e = hipMalloc(&w->piters, (size_t)n);
-  if (e == hipSuccess) e = hipMemset(w->piters, 0, (size_t)n);
   if (e != hipSuccess) (void)free_workspace(w);
   return e;
 }
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
   for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist, (void*)w->gcost,
-                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm, (void*)w->piters}) {
+                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
@@ -1521,10 +1522,9 @@ hipError_t free_workspace(Workspace* w) {
   w->sep = nullptr;
   w->pool = nullptr;
   w->pool_bm = nullptr;
-  w->piters = nullptr;
   return r;
 }
-// The fused path's workspace: the record header (only its contact counts are written), the wave-order buffers,
+// The fused path's workspace: the contact counts (one float per env), the wave-order buffers,
 // the separating-direction cache, and the contact-record pool (Workspace::pool): per XCD one entry (a wave's 4 records
 // of kConEnv floats, 288 KB each) per 256 envs of the XCD's share, at least 8 and at most 32 (295 MB at 65,536 envs,
 // 74 MB at 8,192), for the waves holding an env whose list is longer than the kMaxCon held on chip (for one substep).
@@ -1532,8 +1532,9 @@ int fused_pool_recs(int n) { return std::min(32, std::max(8, (n + 256 * kPoolXcd
 hipError_t alloc_fused_workspace(int n, Workspace* w) {
   *w = Workspace{};
   const size_t ng = (size_t)(n + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  hipError_t e = hipMalloc(&w->hdr, (size_t)n * kHdrEnv * sizeof(float));
-  if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * kHdrEnv * sizeof(float));
+  w->hdr_stride = 1;                   // the contact counts only, one float per env
+  hipError_t e = hipMalloc(&w->hdr, (size_t)n * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(w->hdr, 0, (size_t)n * sizeof(float));
   w->pool_recs = fused_pool_recs(n);
   if (e == hipSuccess) e = hipMalloc(&w->pool, (size_t)kPoolXcd * w->pool_recs * kEnvsPerBlock * kConEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->pool_bm, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
