@@ -412,7 +412,18 @@ DEV void collide(const DevModel* __restrict__ m, const Workspace& w, float* recb
   SSTAMP(6);
   PairContacts pc;
   pc.n = 0;
+#ifndef SO100_EXP_NOBOX   // (temporary timing bound: box pairs skipped)
   if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
+#endif
+#ifdef SO100_EXP_BOX2     // (temporary timing bound: the box pairs' collider run a second time, result unused)
+  {
+    PairContacts pc2;
+    pc2.n = 0;
+    const int l2 = launder_v(lane);
+    if (l2 < SO100_NPAIR_BOX) collide_pair(m, sh, l2, pc2);
+    asm volatile("" ::"v"(pc2.n), "v"(pc2.dist[0]), "v"(pc2.pos[0][0]), "v"(pc2.normal[0]));
+  }
+#endif
 #ifdef SO100_STAMP_BOXBOX
   SSTAMP(0);            // stamps diagnostic: the box-box pairs alone in slot 0 (Euler's, empty in the stage kernel)
 #endif
@@ -1323,22 +1334,47 @@ hipError_t launch_pgs(const DevModel* m, const Workspace& w, float* qacc_out, fl
 hipError_t launch_newton(const DevModel* m, const Workspace& w, float* qacc_out, float* debug, int n, int last,
                          hipStream_t s);
 
-// Heavy-first wave order for the fused kernel.  Its waves run a whole env step each (0.4-1.8 ms) and the
+// Heavy-first wave order for the fused kernel, per XCD.  Its waves run a whole env step each (0.4-1.8 ms) and the
 // grid exceeds the resident slots (12 per CU) above 12,288 envs: a long wave dispatched late sets the step's
 // tail.  Wave costs persist from step to step (correlation 0.65-0.74, measured), so the groups are launched
-// in descending order of their previous step's cost: a counting sort on a 12-bit float key (exponent + 4
-// mantissa bits, 6 % buckets), one workgroup.  The order changes the schedule, never a result.
-constexpr int kOrderBuckets = 4096;
+// in descending order of their previous step's cost.  Workgroups go to the XCDs round-robin (block b to XCD b % 8), so
+// XCD x runs the blocks b = 8 r + x: they take the groups of one contiguous range (range x, as many groups as XCD x has
+// blocks), its r-th costliest as block 8 r + x.  Neighbouring groups then write their shared cache lines of the state
+// arrays (an env's qpos is 52 B, its reward 4 B: a 64-B line spans 1-16 envs) through one L2, which merges them before
+// write-back, instead of one partial line per XCD (round 4's global order scattered neighbours over the 8 L2s).
+// A counting sort on (range, 9-bit cost key: 5 exponent bits from 2^1 up, 4 mantissa bits, 6 % buckets), one
+// workgroup.  The order changes the schedule, never a result.
+constexpr int kOrderXcd = 8;
+constexpr int kOrderKeys = 512;
+constexpr int kOrderBuckets = kOrderXcd * kOrderKeys;
 constexpr int kOrderMinGroups = 256;           // the order also sets the waves' issue priority
+// blocks of XCD x (b % 8 == x) of a grid of ng blocks; range x starts at the sum of those of the XCDs before it
+DEV int order_cnt(int ng, int x) { return (ng - x + kOrderXcd - 1) / kOrderXcd; }
 __global__ void __launch_bounds__(1024) so100_order_kernel(const uint32_t* __restrict__ gcost, int ng,
                                                            int* __restrict__ order) {
   __shared__ int hist[kOrderBuckets];
   __shared__ int part[1024];
+  __shared__ int rstart[kOrderXcd + 1];
   const int t = threadIdx.x;
-  auto key = [](uint32_t c) { return (kOrderBuckets - 1) - (int)((__float_as_uint((float)c) >> 19) & 0xFFFu); };
+  if (t == 0) {
+    int a = 0;
+    for (int x = 0; x < kOrderXcd; x++) { rstart[x] = a; a += order_cnt(ng, x); }
+    rstart[kOrderXcd] = a;
+  }
   for (int b = t; b < kOrderBuckets; b += 1024) hist[b] = 0;
   __syncthreads();
-  for (int g = t; g < ng; g += 1024) atomicAdd(&hist[key(gcost[g])], 1);
+  auto range_of = [&](int g) {
+    int x = 0;
+#pragma unroll
+    for (int y = 1; y < kOrderXcd; y++) x += g >= rstart[y] ? 1 : 0;
+    return x;
+  };
+  auto key = [&](int g) {
+    const uint32_t u = __float_as_uint((float)gcost[g]);
+    const int ex = min(max((int)(u >> 23) - 128, 0), 31);
+    return range_of(g) * kOrderKeys + (kOrderKeys - 1) - ((ex << 4) | (int)((u >> 19) & 15u));
+  };
+  for (int g = t; g < ng; g += 1024) atomicAdd(&hist[key(g)], 1);
   __syncthreads();
   int loc[kOrderBuckets / 1024], sum = 0;
 #pragma unroll
@@ -1355,7 +1391,11 @@ __global__ void __launch_bounds__(1024) so100_order_kernel(const uint32_t* __res
 #pragma unroll
   for (int k = 0; k < kOrderBuckets / 1024; k++) hist[(kOrderBuckets / 1024) * t + k] = base + loc[k];
   __syncthreads();
-  for (int g = t; g < ng; g += 1024) order[atomicAdd(&hist[key(gcost[g])], 1)] = g;
+  for (int g = t; g < ng; g += 1024) {
+    const int x = range_of(g);
+    const int r = atomicAdd(&hist[key(g)], 1) - rstart[x];     // rank in range x (its keys sort after range x - 1's)
+    order[kOrderXcd * r + x] = g;
+  }
 }
 
 // compute units of the current device (cached per device; 0 if the query fails: the 3-wave build then)
