@@ -412,18 +412,7 @@ DEV void collide(const DevModel* __restrict__ m, const Workspace& w, float* recb
   SSTAMP(6);
   PairContacts pc;
   pc.n = 0;
-#ifndef SO100_EXP_NOBOX   // (temporary timing bound: box pairs skipped)
   if (lane < SO100_NPAIR_BOX) collide_pair(m, sh, lane, pc);
-#endif
-#ifdef SO100_EXP_BOX2     // (temporary timing bound: the box pairs' collider run a second time, result unused)
-  {
-    PairContacts pc2;
-    pc2.n = 0;
-    const int l2 = launder_v(lane);
-    if (l2 < SO100_NPAIR_BOX) collide_pair(m, sh, l2, pc2);
-    asm volatile("" ::"v"(pc2.n), "v"(pc2.dist[0]), "v"(pc2.pos[0][0]), "v"(pc2.normal[0]));
-  }
-#endif
 #ifdef SO100_STAMP_BOXBOX
   SSTAMP(0);            // stamps diagnostic: the box-box pairs alone in slot 0 (Euler's, empty in the stage kernel)
 #endif
