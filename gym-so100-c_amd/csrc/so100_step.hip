@@ -1227,6 +1227,13 @@ struct ResetArgs {
   const uint32_t* seeds;
 };
 
+// The 2-wave product build of the fused kernel lives in its own translation unit (so100_fused2.hip, which includes this
+// file with SO100_FUSED2_TU: only the device code above and launch_fused2 below), compiled with LLVM's iterative-ILP
+// scheduler (Makefile): +3.8 % at 8,192 envs, same box (profiles/r05_ab_sched_8192.txt); the 3-wave build spills under
+// that scheduler (220 B/lane), so it and everything else stay on the default one.
+#ifndef SO100_FUSED2_TU
+hipError_t launch_fused2(const DevModel* m, const StageArgs& a, dim3 grid, hipStream_t s);
+
 __global__ void __launch_bounds__(kThreads) so100_reset_kernel(ResetArgs args) {
   __shared__ EnvShared shm[kEnvsPerBlock];
   const DevModel* __restrict__ m = args.m;
@@ -1433,7 +1440,7 @@ hipError_t launch_step(const DevModel* m, int nsubstep, int solver, int fused, i
     const int build = fused_build(n, waves, b.debug != nullptr);
 #ifndef SO100_RU_FUSED3_ONLY   // (Makefile ru3: only the 3-wave product build, for register-allocation work)
     if (build == 1) hipLaunchKernelGGL(so100_fused_kernel<true>, grid, dim3(kThreads), 0, s, m, a);
-    else if (build == 2) hipLaunchKernelGGL((so100_fused_kernel<false, 2>), grid, dim3(kThreads), 0, s, m, a);
+    else if (build == 2) (void)launch_fused2(m, a, grid, s);
     else
 #endif
     hipLaunchKernelGGL((so100_fused_kernel<false, 3>), grid, dim3(kThreads), 0, s, m, a);
@@ -1600,5 +1607,12 @@ hipError_t launch_goal_reward(const DevModel* m, int n, const float* a, const fl
   hipLaunchKernelGGL(so100_goal_reward_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m, n, a, d, out);
   return hipGetLastError();
 }
+
+#else   // SO100_FUSED2_TU
+hipError_t launch_fused2(const DevModel* m, const StageArgs& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((so100_fused_kernel<false, 2>), grid, dim3(kThreads), 0, s, m, a);
+  return hipGetLastError();
+}
+#endif  // SO100_FUSED2_TU
 
 }  // namespace so100
