@@ -1,5 +1,5 @@
-# round 5 closing measurements on the final kernels, part 1: the GPU suite, the default bench line (65,536 envs + CPU
-# baseline), the shard sizes (32,768 / 16,384 / 8,192 envs per GPU), PGS, rocprofv3 kernel stats (part 2: r05z2.sh)
+# round 5 closing measurements on the final kernels, part 1: the GPU suite, the shard sizes (32,768 / 16,384 / 8,192
+# envs per GPU), PGS, rocprofv3 kernel stats (part 2, r05z2.sh: PMC traffic, then the default bench line quoting it)
 export TMPDIR=/tmp
 O=gpurun_out/r05z
 rm -rf $O; mkdir -p $O
@@ -7,7 +7,6 @@ V=gym-so100-c_amd/gym_so100/_lib_var
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rA --timeout 400 --timeout-method thread -s > $O/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc" >> $O/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
 for n in 32768 16384 8192; do
   timeout -k 10 300 python bench.py --total-envs $n --no-cpu-baseline > $O/bench_$n.json 2> $O/bench_$n.err || exit $?
 done
