@@ -19,7 +19,9 @@
 
 namespace so100 {
 
-constexpr int kPgsWaves = 3;         // waves per SIMD the register budget is sized for
+constexpr int kPgsWaves = 2;         // waves per SIMD the register budget is sized for: 2 (176 VGPRs, no scratch; round 5)
+                                     // beat 3 (168, 52 B/lane of spill slots in the overflow path) by 2 %, and with the
+                                     // memory-clause scheduler (Makefile) by 2.5 % (profiles/r05_ab_pgs_sched.txt)
 
 struct PgsArgs {
   const DevModel* m;
