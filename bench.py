@@ -73,6 +73,8 @@ def parse(argv=None):
                    help="constraint solver: newton (MuJoCo's default, which the reference runs; default) or pgs")
     p.add_argument("--convex", default="epa", choices=["epa", "mpr"],
                    help="mesh-pair collider: epa (GJK + EPA, MuJoCo 3.3.3's default; default) or mpr (libccd)")
+    p.add_argument("--dr", action="store_true",
+                   help="configs[4]: domain-randomised cube mass / friction scales (0.8-1.2) and action noise (0.05)")
     p.add_argument("--dump-state", default="",
                    help="test hook: each rank saves its shard's final state to <dir>/state_rank<r>.npz")
     return p.parse_args(argv)
@@ -122,14 +124,15 @@ def cpu_baseline(seconds, solver="newton"):
                     "matrices), not MuJoCo; a non-target baseline"}
 
 
-def load_step_traffic(n_envs, mode, solver, lib_hash):
+def load_step_traffic(n_envs, mode, solver, lib_hash, kind="base"):
     """The committed rocprofv3 PMC measurement of one env step's HBM traffic at this size and step mode
     (profiles/r<NN>_pmc_step_*.json, the newest round's, tools/gpurun/pmc_step_traffic.py: FETCH_SIZE and WRITE_SIZE
     passes, summed over every kernel of a step) and whether it measured these kernels: the file records the
     so100_source_hash of the library it profiled, and traffic is reported only when that equals the loaded
     library's (a profile of older kernels is named in pmc_source but never quoted as traffic)."""
-    for rnd in ("r05", "r04", "r03"):
-        path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_step_{mode}_{solver}_{n_envs}.json")
+    tag = "" if kind == "base" else f"{kind}_"
+    for rnd in ("r06", "r05", "r04", "r03"):
+        path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_step_{tag}{mode}_{solver}_{n_envs}.json")
         if os.path.exists(path):
             try:
                 pmc = json.load(open(path))
@@ -137,6 +140,18 @@ def load_step_traffic(n_envs, mode, solver, lib_hash):
                 return None, False
             return pmc, pmc.get("lib_source_hash") == lib_hash
     return None, False
+
+
+def workload(kind, total, world, count):
+    """config.workload: the BASELINE.json config the line measures (configs[2] by default; --task so100_goal is
+    configs[3], --dr configs[4]; a 1-GPU run of configs[4] benches one 4-GPU shard with --total-envs 8192)"""
+    per = f"{total} envs over {world} GPU(s) ({count} per GPU)"
+    if kind == "goal":
+        return f"configs[3]: GoalEnv dict-obs (HER) variant, {per}, randomized cube spawn, sparse reward, auto-reset"
+    if kind == "dr":
+        return (f"configs[4]: domain-randomized cube mass / friction (x0.8-1.2) + action noise (sigma 0.05), {per}, "
+                "CubeToBin reward, auto-reset")
+    return f"configs[2]: {per} bin-a-cube envs, joint-space ctrl, fp32 state, CubeToBin reward, auto-reset"
 
 
 def main(argv=None):
@@ -170,8 +185,9 @@ def main(argv=None):
         scaling = "strong"
 
     from gym_so100 import SO100VecEnv
+    dr = dict(mass=(0.8, 1.2), friction=(0.8, 1.2), action_noise=0.05) if args.dr else None
     env = SO100VecEnv(count, task=args.task, device=str(dev), seed=args.seed, env_offset=offset, solver=args.solver,
-                      convex=args.convex)
+                      convex=args.convex, domain_randomization=dr)
     if args.fused_build:
         env.fused_build = args.fused_build
     env.reset(seed=1000 + offset)   # env i <- RandomState(1000 + global id)
@@ -191,6 +207,7 @@ def main(argv=None):
         dist.barrier()
     if not args.no_kernel_timing:
         env.profile_enable(args.steps)      # HIP events on the launch stream around every kernel
+    env.pool_stats(reset=True)              # the fused step's contact-record pool counters, from the timed steps on
     torch.cuda.synchronize(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
@@ -206,6 +223,7 @@ def main(argv=None):
     elapsed = t1 - t0
     step_ms = ev[0].elapsed_time(ev[1]) / args.steps        # device time per env step on this stream
     solver_ms = stage_ms = float("nan")
+    pool_st = env.pool_stats()
     if not args.no_kernel_timing:
         s_ms, s_n, t_ms, t_n = env.profile_read()
         env.profile_enable(0)
@@ -242,7 +260,7 @@ def main(argv=None):
         fused = env.fused
         nchunks, n0 = env.chunk_info()
         mode = "fused" if fused else "split"
-        kind = "goal" if args.task == "so100_goal" else "base"
+        kind = "dr" if args.dr else ("goal" if args.task == "so100_goal" else "base")
         bpe = BYTES_PER_ENV_STEP[kind]
         # achieved = env steps/s per GPU x algorithmic bytes per env step.  Per GPU from this
         # rank's device time per step (HIP events on the launch stream around the timed steps: the fused
@@ -251,7 +269,7 @@ def main(argv=None):
         achieved = per_gpu_rate * bpe
         from gym_so100 import _native
         lib_hash = _native.source_hash()
-        pmc, pmc_current = load_step_traffic(count, mode, args.solver, lib_hash)
+        pmc, pmc_current = load_step_traffic(count, mode, args.solver, lib_hash, kind)
         # per env step, like achieved; null unless the profile measured these kernels (the same source hash)
         traffic = pmc["hbm_bytes_per_step"] / count if (pmc and pmc_current) else None
         if fused:
@@ -266,15 +284,18 @@ def main(argv=None):
             "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": (f"configs[2]: {total} bin-a-cube envs sharded over {world} GPU(s) "
-                                    f"({count} per GPU), joint-space ctrl, fp32 state, CubeToBin reward, "
-                                    "auto-reset"),
+            "config": {"workload": workload(kind, total, world, count),
                        "envs_total": total, "envs_per_gpu": count, "task": args.task, "substeps": 10,
+                       "domain_randomization": dr,
                        "solver": args.solver, "solver_iterations": env.model.iterations, "convex": args.convex,
                        "step_mode": mode, "fused_build": env.fused_build if fused else None,
                        "parallelism": f"env-sharded x{world}, no collectives (gloo barrier + MAX for timing)",
                        "actions": "U[-1,1]^6 pool resident in HBM"},
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "roofline": {"bound": "hbm",
+                         "limiter": ("latency: each wave's dependent per-env chain (10 substeps of FK -> dynamics -> "
+                                     "collision -> rows -> Newton steps); HBM is the roofline priced, not the limiter, "
+                                     "valu_busy is the issue share (DESIGN.md §3.5, §8)"),
+                         "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "bytes_per_env_step": bpe, "env_steps_per_s_per_gpu": per_gpu_rate,
                          "step_device_ms": step_ms,
@@ -292,6 +313,9 @@ def main(argv=None):
                          "split_record_bytes_per_solver_launch": rec_per_launch, "envs_per_launch": n0,
                          "contacts_per_env": contacts_per_env,
                          "contacts_dropped_per_env_step": dropped_per_env_step,
+                         "pool_entries_taken_per_step": pool_st["taken"] / args.steps if fused else None,
+                         "pool_requests_none_free": pool_st["none_free"] if fused else None,
+                         "pool_entries_per_xcd": pool_st["entries_per_xcd"] if fused else None,
                          "note": ("achieved = env steps/s per GPU x SURVEY §8(d)'s algorithmic bytes per env step "
                                   "(state/action in, state/outputs out; GoalEnv 418, DR 426): nothing else is "
                                   "algorithmic. traffic = measured HBM bytes per env step from rocprofv3 "

@@ -1048,6 +1048,23 @@ static int so100_contact_counts_impl(so100_env* env, int32_t* out, void* stream)
   return e == hipSuccess ? 0 : fail_hip("so100_contact_counts", e);
 }
 
+static int so100_pool_stats_impl(so100_env* env, uint64_t* out, int reset) {
+  if (!env || !out) return fail("so100_pool_stats: bad arguments");
+  DeviceGuard g(env->device);
+  unsigned long long st[2] = {0, 0};
+  hipError_t e = hipSuccess;
+  if (env->fws.pool_stat) {
+    e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(st, env->fws.pool_stat, sizeof(st), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) e = hipMemset(env->fws.pool_stat, 0, sizeof(st));
+  }
+  if (e != hipSuccess) return fail_hip("so100_pool_stats", e);
+  out[0] = st[0];
+  out[1] = st[1];
+  out[2] = (uint64_t)env->fws.pool_recs;
+  return 0;
+}
+
 static int so100_goal_reward_impl(so100_env* env, int n, const float* a, const float* d, float* out, void* stream) {
   if (!env || !a || !d || !out || n < 0) return fail("so100_goal_reward: bad arguments");
   if (n == 0) return 0;
@@ -1275,6 +1292,14 @@ int so100_contact_count(so100_env* env, uint64_t* accum, void* stream) {
     return so100_contact_count_impl(env, accum, stream);
   } catch (...) {
     return caught("so100_contact_count");
+  }
+}
+
+int so100_pool_stats(so100_env* env, uint64_t* out, int reset) {
+  try {
+    return so100_pool_stats_impl(env, out, reset);
+  } catch (...) {
+    return caught("so100_pool_stats");
   }
 }
 

@@ -204,14 +204,17 @@ struct Workspace {
   // beyond them: geometry, J, the rows and the Newton solve's per-contact state; kConEnv floats each), a pool of
   // entries (a wave's kEnvsPerBlock records) per XCD with a free bitmap (pool_bm[xcd * kPoolWords ..]).  A wave takes
   // one for a substep when one of its envs' lists passes kMaxCon and returns it after the solve (so100_pool.h);
-  // pool_recs entries per XCD.
+  // pool_recs entries per XCD: as many as the XCD can hold fused-kernel waves resident, so one is always free.
+  // pool_stat [2]: entries taken (wave-substeps that held one) and scans that found none (0 by the sizing), summed
+  // over steps (so100_pool_stats).
   // The split path keeps its per-env record in con.
   float* pool;
   uint32_t* pool_bm;
   int pool_recs;
+  unsigned long long* pool_stat;
 };
 constexpr int kPoolXcd = 8;       // MI355X: 8 XCDs (HW_REG_XCC_ID), one pool each: a record stays in its XCD's L2
-constexpr int kPoolWords = 4;     // <= 128 entries per XCD
+constexpr int kPoolWords = 16;    // <= 512 entries per XCD (32 CUs x 12 resident fused waves = 384)
 constexpr int kPoolSlots = 32 * kPoolWords;   // a pool id: XCD x kPoolSlots + bitmap entry
 
 }  // namespace so100

@@ -1547,7 +1547,7 @@ hipError_t alloc_workspace(int n, Workspace* w) {
 hipError_t free_workspace(Workspace* w) {
   hipError_t r = hipSuccess;
   for (void* p : {(void*)w->hdr, (void*)w->con, (void*)w->gflag, (void*)w->hcount, (void*)w->hlist, (void*)w->gcost,
-                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm}) {
+                  (void*)w->order, (void*)w->sep, (void*)w->pool, (void*)w->pool_bm, (void*)w->pool_stat}) {
     if (!p) continue;
     hipError_t e = hipFree(p);
     if (r == hipSuccess) r = e;
@@ -1558,13 +1558,30 @@ hipError_t free_workspace(Workspace* w) {
   w->sep = nullptr;
   w->pool = nullptr;
   w->pool_bm = nullptr;
+  w->pool_stat = nullptr;
   return r;
 }
-// The fused path's workspace: the contact counts (one float per env), the wave-order buffers,
-// the separating-direction cache, and the contact-record pool (Workspace::pool): per XCD one entry (a wave's 4 records
-// of kConEnv floats, 288 KB each) per 256 envs of the XCD's share, at least 8 and at most 32 (295 MB at 65,536 envs,
-// 74 MB at 8,192), for the waves holding an env whose list is longer than the kMaxCon held on chip (for one substep).
-int fused_pool_recs(int n) { return std::min(32, std::max(8, (n + 256 * kPoolXcd - 1) / (256 * kPoolXcd))); }
+// The fused path's workspace: the contact counts (one float per env), the wave-order buffers, the separating-direction
+// cache, and the contact-record pool (Workspace::pool): per XCD one entry (a wave's 4 records of kConEnv floats, 288 KB
+// each) per fused-kernel wave the XCD can hold resident at once — its CUs (the device's CUs / kPoolXcd) x the resident
+// workgroups per CU of the fused instantiations (the occupancy API: 12, LDS-bound, for the 3-wave and debug builds;
+// 8 for the 2-wave build), and no more than the grid's waves — so a wave that asks always finds a free entry
+// (so100_pool.h).  3.5 GB at 6,144 envs and up (8 x 384 entries; 288 GB of HBM per GPU), for the waves holding an env
+// whose list is longer than the kMaxCon held on chip (for one substep).
+int fused_pool_recs(int n) {
+  int dev = 0, cus = 256, occ3 = 0, occd = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, so100_fused_kernel<false, 3>, kThreads, 0) != hipSuccess) occ3 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occd, so100_fused_kernel<true, 3>, kThreads, 0) != hipSuccess) occd = 0;
+  (void)hipGetLastError();
+  // 160 KB of LDS per CU over the kernels' static LDS caps every build (the 2-wave build at 8 by its registers)
+  const int lds_cap = (160 * 1024) / (int)(sizeof(EnvShared) * kEnvsPerBlock);
+  const int per_cu = std::max({occ3, occd, lds_cap});
+  const int cus_per_xcd = (cus + kPoolXcd - 1) / kPoolXcd;
+  const int waves = (n + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  return std::max(1, std::min({kPoolSlots, cus_per_xcd * per_cu, waves}));
+}
 hipError_t alloc_fused_workspace(int n, Workspace* w) {
   *w = Workspace{};
   const size_t ng = (size_t)(n + kEnvsPerBlock - 1) / kEnvsPerBlock;
@@ -1575,6 +1592,8 @@ hipError_t alloc_fused_workspace(int n, Workspace* w) {
   if (e == hipSuccess) e = hipMalloc(&w->pool, (size_t)kPoolXcd * w->pool_recs * kEnvsPerBlock * kConEnv * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&w->pool_bm, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->pool_bm, 0, (size_t)kPoolXcd * kPoolWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&w->pool_stat, 2 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(w->pool_stat, 0, 2 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMalloc(&w->gcost, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(w->gcost, 0, ng * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&w->order, ng * sizeof(int));

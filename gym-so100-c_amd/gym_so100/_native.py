@@ -46,7 +46,7 @@ class NativeLibraryError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 16         # include/so100.h SO100_ABI_VERSION
+ABI_VERSION = 17         # include/so100.h SO100_ABI_VERSION
 HULL_CELLG = 8           # SO100_HULL_CELLG
 HULL_NCELL = 6 * HULL_CELLG * HULL_CELLG
 
@@ -79,6 +79,7 @@ def load():
     lib.so100_profile_read.argtypes = [_P, _P, _P, _P, _P]
     lib.so100_contact_count.argtypes = [_P, _P, _P]
     lib.so100_contact_counts.argtypes = [_P, _P, _P]
+    lib.so100_pool_stats.argtypes = [_P, _P, ctypes.c_int]
     lib.so100_chunk_info.argtypes = [_P, _P, _P]
     lib.so100_set_step_mode.argtypes = [_P, ctypes.c_int]
     lib.so100_step_mode.argtypes = [_P]
@@ -90,7 +91,7 @@ def load():
     for fn in ("so100_destroy", "so100_num_envs", "so100_configure", "so100_reset", "so100_step",
                "so100_goal_reward", "so100_eval_reward", "so100_spawn_pose", "so100_unnormalize",
                "so100_profile_enable", "so100_profile_read", "so100_contact_count", "so100_contact_counts",
-               "so100_chunk_info", "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells",
+               "so100_pool_stats", "so100_chunk_info", "so100_render_mesh", "so100_render", "so100_set_step_mode", "so100_step_mode", "so100_hull_cells",
                "so100_set_fused_build", "so100_fused_build"):
         getattr(lib, fn).restype = ctypes.c_int
     lib.so100_struct_sizes.argtypes = [_P, _P]
@@ -110,7 +111,8 @@ def load():
 EXPORTED_SYMBOLS = ("so100_abi_version", "so100_last_error", "so100_source_hash", "so100_struct_sizes", "so100_create", "so100_destroy", "so100_num_envs",
                     "so100_configure", "so100_reset", "so100_step", "so100_goal_reward", "so100_eval_reward",
                     "so100_spawn_pose", "so100_unnormalize", "so100_profile_enable", "so100_profile_read",
-                    "so100_contact_count", "so100_contact_counts", "so100_chunk_info", "so100_render_mesh", "so100_render",
+                    "so100_contact_count", "so100_contact_counts", "so100_pool_stats", "so100_chunk_info", "so100_render_mesh",
+                    "so100_render",
                     "so100_set_step_mode", "so100_step_mode", "so100_hull_cells", "so100_set_fused_build",
                     "so100_fused_build")
 

@@ -458,6 +458,15 @@ class SO100VecEnv:
         _native.check(self.lib.so100_chunk_info(self._handle, ctypes.byref(k), ctypes.byref(n0)), "so100_chunk_info")
         return k.value, n0.value
 
+    def pool_stats(self, reset=False):
+        """The fused step's contact-record pool, summed over the steps since construction or the last
+        reset: {"taken": entries taken (wave-substeps whose env lists passed the 16 held on chip), "none_free": entry
+        requests that found none free (0 by construction: each XCD's pool holds an entry per wave it can hold
+        resident), "entries_per_xcd": the pool's size}.  Synchronises the device."""
+        out = (ctypes.c_uint64 * 3)()
+        _native.check(self.lib.so100_pool_stats(self._handle, out, int(bool(reset))), "so100_pool_stats")
+        return {"taken": int(out[0]), "none_free": int(out[1]), "entries_per_xcd": int(out[2])}
+
     def contact_count(self, accum):
         """accum (int64 device tensor, 1 element) += contacts in the last solver launch, summed over envs."""
         _native.check(self.lib.so100_contact_count(self._handle, _native.ptr(accum), self._stream()),

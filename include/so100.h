@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SO100_ABI_VERSION 16  /* 16: so100_source_hash;  15: the EE variant's mocap marker box collides (SO100_NGEOM 16, SO100_NPAIR 209, SO100_NCON_MAX 643, debug stride 3,922);  14: no per-env contact cap (SO100_NCON_MAX: every pair at its collider's maximum), debug stride 3,436 (SO100_DBG_OVF), ncon_dropped always 0, status -3 for a caught C++ exception;  13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
+#define SO100_ABI_VERSION 17  /* 17: so100_pool_stats (the fused step's contact-record pool, sized never to run out);  16: so100_source_hash;  15: the EE variant's mocap marker box collides (SO100_NGEOM 16, SO100_NPAIR 209, SO100_NCON_MAX 643, debug stride 3,922);  14: no per-env contact cap (SO100_NCON_MAX: every pair at its collider's maximum), debug stride 3,436 (SO100_DBG_OVF), ncon_dropped always 0, status -3 for a caught C++ exception;  13: so100_buffers.ep_return / ep_final / ep_accum (device-side episode statistics);  12: so100_model.convex (GJK/EPA mesh collider, MuJoCo 3.3.3 default), box-box up to 8 contacts, cube-table one convex contact;  11: so100_buffers.ncon_dropped, debug stride 160 (contact friction forces), so100_set_fused_build;  10: so100_hull_cells (MPR support lookup);  9: pad/link-hull pairs (SO100_NPAIR 191);  8: fused step kernel, so100_set_step_mode;  7: reward64 buffer;  6: Base hull + pad pairs (SO100_NPAIR 155, SO100_NHULL_ALL 10); 5: EE/mocap weld, render API */
 
 /* tasks (gym_so100/__init__.py:4-32 ids; single_arm.py task classes) */
 #define SO100_TASK_CUBE_TO_BIN 0          /* gym_so100/SO100CubeToBin-v0, TimeLimit 700 */
@@ -183,6 +183,11 @@ int so100_contact_count(so100_env* env, uint64_t* accum, void* stream);
 /* Writes each env's contact count of the last solver launch (the last substep's list) to out (DEVICE int32 [N]).
  * Enqueued on `stream`, no synchronisation.  (ABI 14) */
 int so100_contact_counts(so100_env* env, int32_t* out, void* stream);
+/* (ABI 17) The fused step's contact-record pool: out[0] = pool entries taken (wave-substeps whose
+ * env lists passed the 16 held on chip), out[1] = entry requests that found none free (0 by construction: each XCD's
+ * pool holds as many entries as the XCD can hold fused waves resident), out[2] = entries per XCD; the first two summed
+ * over the steps since so100_create or the last reset != 0 call.  Synchronises the device (a benchmark / test hook). */
+int so100_pool_stats(so100_env* env, uint64_t* out, int reset);
 
 /* ---- camera images: the reference's default observation, obs_type
  * "so100_pixels_agent_pos" (gym_so100/__init__.py:4-32) = the `top` camera rendered by dm_control

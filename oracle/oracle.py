@@ -72,13 +72,14 @@ def ensure_built():
 class Oracle:
     """One precision flavour of the oracle library (bits=64 default, 32 = same code in float)."""
 
-    def __init__(self, bits=64, fma=False):
-        """fma (bits=32 only): the build with multiply-adds contracted to FMAs, as the GPU compiler does"""
+    def __init__(self, bits=64, fma=False, path=None):
+        """fma (bits=32 only): the build with multiply-adds contracted to FMAs, as the GPU compiler does; path: another
+        build of the same precision (tools/dev experiments)"""
         ensure_built()
         self.bits = bits
         self.real = ctypes.c_double if bits == 64 else ctypes.c_float
         self.np_real = np.float64 if bits == 64 else np.float32
-        self.lib = ctypes.CDLL(os.path.join(HERE, "build", f"liboracle{bits}{'fma' if fma else ''}.so"))
+        self.lib = ctypes.CDLL(path or os.path.join(HERE, "build", f"liboracle{bits}{'fma' if fma else ''}.so"))
         self.Contact, self.Data = _make_types(self.real)
         L = self.lib
         P = ctypes.c_void_p

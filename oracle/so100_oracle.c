@@ -1,3 +1,4 @@
+#include <stdio.h>
 /* so100_oracle.c — CPU restatement of the SO-ARM100 bin-a-cube hot path (TEST INFRASTRUCTURE).
  *
  * ORACLE ONLY: loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
@@ -961,6 +962,7 @@ static int gjk(const mpr_obj* o, mpr_sup S[4], real dsep[4]) {
   return 0;
 }
 
+int so100o_epa_debug = 0;     /* tools/dev: print each EPA's final facet */
 static int epa_face_set(epa_face* f, const mpr_sup* V, int a, int b, int c) {
   real ab[3], ac[3], n[3];
   sub3(ab, V[b].v, V[a].v);
@@ -973,6 +975,78 @@ static int epa_face_set(epa_face* f, const mpr_sup* V, int a, int b, int c) {
   f->v[0] = a; f->v[1] = b; f->v[2] = c;
   f->dist = dot3(f->n, V[a].v);
   f->alive = 1;
+  return 1;
+}
+
+/* The contact of EPA's final facet from the features it spans (round 6).  A facet of the Minkowski difference
+ * obj1 - obj2 lies on one of its faces: obj1's vertex against obj2's face (one distinct obj1 support, three of obj2),
+ * obj1's face against obj2's vertex (three, one), or an edge of each (two, two).  Its witness points, normal and depth
+ * are then those features' exact contact — the vertex and its projection on the face plane, or the two edges' closest
+ * points with the normal along their cross product — computed from the supports' own coordinates (short edges from
+ * the hull's cm-sized vertices; obj1's are its own).  The barycentric interpolation over the facet (the fallback for
+ * any other facet) depends on which triangle of the face EPA stopped on, and on a sliver facet (a 1.2 m table edge
+ * beside a mm-long hull edge) its fp32 solve lost 1e-2 of the weight along the long edge: the contact moved by
+ * centimetres between the fp32 and fp64 restatements (tools/dev/collision_precision.py).  Returns 0 to fall back. */
+static int same3(const real a[3], const real b[3]) { return a[0] == b[0] && a[1] == b[1] && a[2] == b[2]; }
+static int epa_feature_witness(const mpr_sup* V, const epa_face* f, real* depth, real dir[3], real pos[3]) {
+  const mpr_sup* P[3] = {&V[f->v[0]], &V[f->v[1]], &V[f->v[2]]};
+  /* distinct supports of each object, in facet order */
+  const real* u1[3]; const real* u2[3];
+  int n1 = 0, n2 = 0;
+  for (int k = 0; k < 3; k++) {
+    int seen = 0;
+    for (int j = 0; j < n1; j++) seen |= same3(u1[j], P[k]->v1);
+    if (!seen) u1[n1++] = P[k]->v1;
+    seen = 0;
+    for (int j = 0; j < n2; j++) seen |= same3(u2[j], P[k]->v2);
+    if (!seen) u2[n2++] = P[k]->v2;
+  }
+  real nn[3], p1[3], p2[3], e1[3], e2[3];
+  if (n1 == 2 && n2 == 2) {                    /* edge (u1[0], u1[1]) of obj1 against edge (u2[0], u2[1]) of obj2 */
+    sub3(e1, u1[1], u1[0]);
+    sub3(e2, u2[1], u2[0]);
+    cross3(nn, e1, e2);
+    real w0[3];
+    sub3(w0, u1[0], u2[0]);
+    const real a = dot3(e1, e1), b = dot3(e1, e2), c = dot3(e2, e2), dd = dot3(e1, w0), e = dot3(e2, w0);
+    const real den = a * c - b * b;
+    if (!(den > (real)1e-6 * a * c)) return 0;  /* (nearly) parallel edges: no single closest pair */
+    const real t = (b * e - c * dd) / den, u = (a * e - b * dd) / den;
+    for (int q = 0; q < 3; q++) { p1[q] = u1[0][q] + t * e1[q]; p2[q] = u2[0][q] + u * e2[q]; }
+  } else if (n1 == 1 && n2 == 3) {             /* obj1's vertex against obj2's face */
+    sub3(e1, u2[1], u2[0]);
+    sub3(e2, u2[2], u2[0]);
+    cross3(nn, e1, e2);
+  } else if (n1 == 3 && n2 == 1) {             /* obj1's face against obj2's vertex */
+    sub3(e1, u1[1], u1[0]);
+    sub3(e2, u1[2], u1[0]);
+    cross3(nn, e1, e2);
+  } else {
+    return 0;
+  }
+  const real l = (real)sqrt((double)dot3(nn, nn));
+  if (ccd_zero(l)) return 0;
+  const real il = (dot3(nn, f->n) < 0 ? -1 : 1) / l;   /* oriented as the facet's outward normal */
+  for (int q = 0; q < 3; q++) nn[q] *= il;
+  real dep;
+  if (n1 == 2) {
+    real w[3];
+    sub3(w, p1, p2);
+    dep = dot3(nn, w);
+  } else if (n1 == 1) {
+    real w[3];
+    sub3(w, u1[0], u2[0]);
+    dep = dot3(nn, w);
+    for (int q = 0; q < 3; q++) { p1[q] = u1[0][q]; p2[q] = u1[0][q] - dep * nn[q]; }
+  } else {
+    real w[3];
+    sub3(w, u1[0], u2[0]);
+    dep = dot3(nn, w);
+    for (int q = 0; q < 3; q++) { p2[q] = u2[0][q]; p1[q] = u2[0][q] + dep * nn[q]; }
+  }
+  if (!(dep > 0) || ccd_zero(dep)) return 0;
+  *depth = dep;
+  for (int q = 0; q < 3; q++) { dir[q] = nn[q]; pos[q] = (real)0.5 * (p1[q] + p2[q]); }
   return 1;
 }
 
@@ -1054,6 +1128,14 @@ static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir
     real den = d00 * d11 - d01 * d01;
     if (ccd_zero(den)) { l[0] = 1; l[1] = 0; l[2] = 0; }
     else { l[1] = (d11 * d20 - d01 * d21) / den; l[2] = (d00 * d21 - d01 * d20) / den; l[0] = 1 - l[1] - l[2]; }
+  }
+  if (epa_feature_witness(V, f, depth, dir, pos)) return 1;
+  if (so100o_epa_debug) {
+    fprintf(stderr, "EPA%d facet n %.9g %.9g %.9g dist %.9g l %.6g %.6g %.6g\n", (int)sizeof(real), (double)f->n[0],
+            (double)f->n[1], (double)f->n[2], (double)f->dist, (double)l[0], (double)l[1], (double)l[2]);
+    for (int k = 0; k < 3; k++)
+      fprintf(stderr, "   v1 %.9g %.9g %.9g  v2 %.9g %.9g %.9g\n", (double)V[f->v[k]].v1[0], (double)V[f->v[k]].v1[1],
+              (double)V[f->v[k]].v1[2], (double)V[f->v[k]].v2[0], (double)V[f->v[k]].v2[1], (double)V[f->v[k]].v2[2]);
   }
   for (int t = 0; t < 3; t++) {
     real w1 = 0, w2 = 0;
@@ -1160,6 +1242,46 @@ static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
   for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
 }
 
+/* A hull-table contact from GJK + EPA whose normal lies within kTableSnap of one of the table box's face normals
+ * (world axes: the table is axis-aligned) is that face's contact: EPA stops within its tolerance of the face normal
+ * (1e-6 of the facet distance: normals off by up to ~1e-6 rad), and the witness it interpolates on a Minkowski facet
+ * then depends on that residual tilt (a hull corner a centimetre away wins under a 1e-7 rad tilt when the hull lies
+ * flat on the face): fp32 and fp64 took different corners (tools/dev/collision_precision.py).  The face's contact is
+ * restated exactly: normal the face's axis u (table -> hull), depth the face plane's distance past the hull's extreme
+ * vertex along -u, the witness that vertex (the first in hull order among ties, compared in hull-relative
+ * coordinates) and its projection on the face: pos their midpoint.  The top-face rule (table_hull_fast) is this on the
+ * top face where it is provably the minimum penetration; here EPA has established that the face is. */
+#define TABLE_SNAP ((real)1e-5)
+static void table_face_snap(const so100_model* m, so100o_data* d, int k, so100o_contact* con) {
+  int ax = 0;
+  for (int i = 1; i < 3; i++)
+    if ((real)fabs((double)con->frame[i]) > (real)fabs((double)con->frame[ax])) ax = i;
+  const real off = (real)sqrt((double)(con->frame[(ax + 1) % 3] * con->frame[(ax + 1) % 3] +
+                                       con->frame[(ax + 2) % 3] * con->frame[(ax + 2) % 3]));
+  if (!(off < TABLE_SNAP)) return;
+  const real sgn = con->frame[ax] > 0 ? (real)1 : (real)-1;
+  const int p = SO100_NPAIR_BOX + k, b = m->hull_body[k], g = m->pair_geom1[p];
+  const real top = (real)m->table_top, bottom = top - 2 * (real)m->geom_size[g][2];
+  const real lo = ax == 2 ? bottom : (real)m->table_lo[ax], hi = ax == 2 ? top : (real)m->table_hi[ax];
+  const real face = sgn > 0 ? hi : lo;                     /* the face's coordinate on axis ax */
+  const real* R = d->xmat[b];
+  real best = 0, wb[3] = {0, 0, 0};
+  for (int v = 0; v < m->hull_count[k]; v++) {
+    real hv[3], w[3];
+    load3(hv, m->hull_vert[m->hull_start[k] + v]);
+    mulmv3(w, R, hv);
+    const real h = sgn * w[ax];                           /* hull-relative height along u */
+    if (v == 0 || h < best) { best = h; wb[0] = w[0]; wb[1] = w[1]; wb[2] = w[2]; }
+  }
+  for (int t = 0; t < 3; t++) wb[t] += d->xpos[b][t];
+  const real dist = sgn * wb[ax] - sgn * face;            /* < 0: the vertex lies past the face, inside the table */
+  memset(con->frame, 0, sizeof(con->frame));
+  con->frame[ax] = sgn;
+  for (int t = 0; t < 3; t++) con->pos[t] = wb[t];
+  con->pos[ax] = (real)0.5 * (wb[ax] + face);
+  con->dist = dist;
+}
+
 /* one convex pair p through the convex collider (GJK + EPA, or MPR), in H = the body frame of hull k (geom2):
  *   23..76 (cube | bin box, hull k); 77..97 (hull k1, hull k2) self-collision of non-adjacent links;
  *   98..106 the static Base hull (the cube, then link hulls 1..8); 107..142 (finger pad, link hull k);
@@ -1231,6 +1353,7 @@ static void convex_pair(const so100_model* m, so100o_data* d, int p) {
   mulmv3(con.pos, RH, pos);
   for (int t = 0; t < 3; t++) con.pos[t] += d->xpos[b][t];
   con.dist = -depth;
+  if (g == 0) table_face_snap(m, d, k, &con);
   add_contact(d, &con, p);
 }
 
@@ -1265,14 +1388,19 @@ static int table_hull_fast(const so100_model* m, so100o_data* d, int k) {
   const real D = top - zb, cx = d->xpos[b][0] + wc[0], cy = d->xpos[b][1] + wc[1], gz = d->xpos[b][2] + wg[2];
   if (!(cx - e[0] >= (real)m->table_lo[0] + D && cx + e[0] <= (real)m->table_hi[0] - D &&
         cy - e[1] >= (real)m->table_lo[1] + D && cy + e[1] <= (real)m->table_hi[1] - D && gz - bottom >= D)) return -1;
+  /* the lowest vertex by (R v).z, the hull-relative height (cm-sized: its fp32 rounding is ~1e-9 m), the body's world
+   * z added once after: compared in world z (~0.5 m, rounding 3e-8 m) a hull face lying nearly flat tied its corners,
+   * and fp32 rounding picked another lowest corner than fp64, centimetres away (tools/dev/collision_precision.py) */
   real best = 0, bx = 0, by = 0;
   for (int v = 0; v < m->hull_count[k]; v++) {
     real hv[3], w[3];
     load3(hv, m->hull_vert[m->hull_start[k] + v]);
     mulmv3(w, R, hv);
-    for (int t = 0; t < 3; t++) w[t] += d->xpos[b][t];
     if (v == 0 || w[2] < best) { best = w[2]; bx = w[0]; by = w[1]; }
   }
+  best += d->xpos[b][2];
+  bx += d->xpos[b][0];
+  by += d->xpos[b][1];
   if (!(best - top < margin)) return 0;
   so100o_contact con;
   memset(&con, 0, sizeof(con));
@@ -1788,19 +1916,24 @@ static void sol_pgs(const so100_model* m, so100o_data* d, const real* AR) {
  * The start is qacc_warmstart if its cost is below qacc_smooth's (mj_fwdConstraint).  The line search
  * is ours (a safeguarded 1-D Newton on c'(alpha) to relative precision; MuJoCo brackets to ls_tolerance
  * 0.01), so the iterates differ from MuJoCo's path but converge to the same unique minimiser. */
-/* Precision-dependent stops.  fp64 (the checker): the line search to |c'| <= 1e-12 |c'(0)|, no extra outer
- * stop.  fp32 (the GPU's arithmetic, mirrored by so100_newton.hip): MuJoCo's ls_tolerance 0.01, a relative
- * step stop 1e-4 (fp32 cannot resolve c' near the minimum: the search otherwise ran 14 evaluations), and
- * an outer stop at a relative cost improvement of 1e-6 (MuJoCo's absolute 1e-8 is below fp32 resolution
- * of the cost); accuracy against fp64 unchanged, 30 -> 6.5 derivative evaluations per substep. */
-#ifdef SO100O_FLOAT
+/* Precision-dependent stops.  fp64 (the checker): the line search to |c'| <= 1e-12 |c'(0)|, MuJoCo's outer tests only.
+ * fp32 (the GPU's arithmetic, mirrored by so100_newton.h): MuJoCo's ls_tolerance 0.01, a relative step stop 1e-4 (fp32
+ * cannot resolve c' near the minimum: the search otherwise ran 14 evaluations), and the Newton decrement: with the
+ * direction s = -H^-1 g in hand, a full step would lower the cost by -g's/2, and the solve stops when that (scaled) is
+ * below MuJoCo's tolerance.  MuJoCo's own stops are below fp32's resolution there (scale |g| never reaches 1e-8 under
+ * fp32 rounding of g, and the cost difference is noise at 1e-8), and rounds 3-5 stopped at a relative cost improvement
+ * of 1e-6 instead, which on the EE variant (the weld folded into M: a large cost) ended solves short of the minimiser:
+ * EE qvel p90 5e-4 against fp64 (tools/dev/mixed_precision.py).  The decrement resolves where fp32 can (g's noise
+ * enters squared) and matches fp64's iteration counts: 1.20 line searches per substep on the bench workload
+ * (fp64 1.22, the relative stop 1.88), EE qvel p90 2.5e-5. */
+#if defined(SO100O_FLOAT) && !defined(LS_TOL)
 #define LS_TOL ((real)1e-2)
 #define LS_STEP ((real)1e-4)
-#define NEWTON_RELTOL ((real)1e-6)
-#else
+#define NEWTON_DECREMENT 1
+#elif !defined(LS_TOL)
 #define LS_TOL ((real)1e-12)
 #define LS_STEP ((real)0)
-#define NEWTON_RELTOL ((real)0)
+#define NEWTON_DECREMENT 0
 #endif
 
 /* cost, force (= -d cost / d jar) and cost Hessian of the constraint block at row i; returns its rows */
@@ -2002,6 +2135,11 @@ static void sol_newton(const so100_model* m, so100o_data* d) {
     real s[NV], mg[NV];
     for (int k = 0; k < NV; k++) mg[k] = -grad[k];
     if (!chol_solve(H, mg, s)) break;
+    if (NEWTON_DECREMENT) {
+      real gs = 0;
+      for (int k = 0; k < NV; k++) gs += grad[k] * s[k];
+      if (scale * (real)-0.5 * gs < (real)m->tolerance) break;
+    }
     const real alpha = line_search(d, a, s, jar);
     d->solver_iter = it + 1;
     if (alpha == 0) break;
@@ -2012,7 +2150,6 @@ static void sol_newton(const so100_model* m, so100o_data* d) {
     cost = nc;
     d->solver_improvement = improvement;
     if (improvement < (real)m->tolerance) break;
-    if (improvement < NEWTON_RELTOL * scale * (real)fabs((double)cost)) break;
   }
   constraint_cost(d, jar, d->efc_force);
   memcpy(d->qacc, a, sizeof(a));
@@ -2025,7 +2162,8 @@ double so100o_newton_cost(so100o_data* d, const so100o_real a[NV]) {
   return (double)(gauss_cost(d, a) + constraint_cost(d, jar, f));
 }
 
-void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
+/* mj_fwdActuation + the smooth acceleration + mj_referenceConstraint (the solve's inputs) */
+static void acc_smooth(const so100_model* m, so100o_data* d) {
   /* [3P] mj_fwdActuation: position actuator, ctrl clamped to ctrlrange, force clamped to forcerange */
   memset(d->qfrc_actuator, 0, sizeof(d->qfrc_actuator));
   for (int i = 0; i < SO100_NU; i++) {
@@ -2043,11 +2181,15 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   real rhs[NV];
   for (int k = 0; k < NV; k++) rhs[k] = d->qfrc_actuator[k] - d->qfrc_bias[k] + d->weld_f[k];
   solve_m(d, d->qacc_smooth, rhs);
+  /* [3P] mj_referenceConstraint: aref */
+  for (int i = 0; i < d->nefc; i++)
+    d->efc_aref[i] = -d->efc_B[i] * d->efc_vel[i] - d->efc_K[i] * d->efc_imp[i] * (d->efc_pos[i] - d->efc_margin[i]);
+}
+
+/* the constraint solve (mj_fwdConstraint): Newton (MuJoCo's default) or PGS */
+static void acc_solve(const so100_model* m, so100o_data* d) {
   const int nefc = d->nefc;
   if (nefc == 0) { memcpy(d->qacc, d->qacc_smooth, sizeof(d->qacc)); d->solver_iter = 0; return; }
-  /* [3P] mj_referenceConstraint: aref */
-  for (int i = 0; i < nefc; i++)
-    d->efc_aref[i] = -d->efc_B[i] * d->efc_vel[i] - d->efc_K[i] * d->efc_imp[i] * (d->efc_pos[i] - d->efc_margin[i]);
   if (m->solver == SO100_SOLVER_NEWTON) { sol_newton(m, d); return; }
   /* [3P] mj_projectConstraint: b, AR = J M^-1 J' + R (nefc x nefc, on the heap: the list may be long) */
   static __thread real MJT[NEFC][NV];
@@ -2091,6 +2233,11 @@ void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
   }
 }
 
+void so100o_fwd_acceleration(const so100_model* m, so100o_data* d) {
+  acc_smooth(m, d);
+  acc_solve(m, d);
+}
+
 /* [3P] mj_Euler (no dof damping) -> mj_advance: qvel += h qacc; integratePos with the NEW qvel;
  * free-joint quaternion via mju_quatIntegrate (body-frame angular velocity); warmstart = qacc */
 void so100o_euler(const so100_model* m, so100o_data* d) {
@@ -2107,6 +2254,29 @@ void so100o_euler(const so100_model* m, so100o_data* d) {
   }
   quat_normalize(d->qpos + 9);
   memcpy(d->qacc_warmstart, d->qacc, sizeof(d->qacc));
+}
+
+/* One stage of a substep (the parts of so100o_substep, in order), for the mixed-precision attribution tool
+ * (tools/dev/mixed_precision.py: each stage run in fp64 or fp32 on the same state, the data converted between):
+ * SO100O_STAGE_KIN kinematics + com_pos, _CRB crb (+ the weld fold) + the M factor, _COLL collision, _CONSTR the
+ * constraint rows, _VEL the velocity stage, _SMOOTH actuation + qacc_smooth + aref, _SOLVE the solver, _EULER. */
+void so100o_stage(const so100_model* m, so100o_data* d, int k) {
+  switch (k) {
+    case SO100O_STAGE_KIN: kinematics(m, d); com_pos(m, d); break;
+    case SO100O_STAGE_CRB:
+      crb(m, d);
+      if (m->ee) weld_fold(m, d);
+      else memset(d->weld_f, 0, sizeof(d->weld_f));
+      factor_m(d);
+      break;
+    case SO100O_STAGE_COLL: collision(m, d); break;
+    case SO100O_STAGE_CONSTR: make_constraint(m, d); break;
+    case SO100O_STAGE_VEL: so100o_fwd_velocity(m, d); break;
+    case SO100O_STAGE_SMOOTH: acc_smooth(m, d); break;
+    case SO100O_STAGE_SOLVE: acc_solve(m, d); break;
+    case SO100O_STAGE_EULER: so100o_euler(m, d); break;
+    default: break;
+  }
 }
 
 void so100o_substep(const so100_model* m, so100o_data* d) {

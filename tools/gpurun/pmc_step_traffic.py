@@ -9,8 +9,10 @@ S x P dispatches (the timed steps) are summed and divided by S.  FETCH_SIZE and 
 (memory-side L2 -> fabric requests).  gfx950 tallies a 16-B/lane streaming read at half its bytes in
 FETCH_SIZE; the step's loads are mostly 4-B/lane and scalar, so hbm_bytes_per_step uses the raw count and
 hbm_bytes_per_step_fetch_x2 is the upper bound with every read doubled.  bench.py reads the JSON
-(profiles/r05_pmc_step_<mode>_<solver>_<n>.json) for roofline.traffic, which it reports only when the file's
-lib_source_hash (so100_source_hash of the library profiled) equals the loaded library's.
+(profiles/r06_pmc_step_[goal_|dr_]<mode>_<solver>_<n>.json) for roofline.traffic, which it reports only when the
+file's lib_source_hash equals the loaded library's.  That hash is the one the PROFILED processes loaded: each pass's
+bench.py stdout (<pmc dir>.<pass>.log, the JSON line's roofline.lib_source_hash) is read, and the passes must agree
+(round 6, ADVICE r5: a rebuild between profiling and this script no longer relabels the profile).
 """
 import csv
 import glob
@@ -41,6 +43,18 @@ def per_step(rows, warmup, steps):
     return sum(v for _, v, _ in last) / steps, p
 
 
+def profiled_hashes(d):
+    """roofline.lib_source_hash of every profiled bench.py run (<pmc dir>.<pass>.log: its one JSON line)"""
+    out = []
+    for f in sorted(glob.glob(d.rstrip("/") + ".*.log")):
+        for line in open(f, errors="replace"):
+            if line.startswith("{") and '"roofline"' in line:
+                out.append(json.loads(line)["roofline"]["lib_source_hash"])
+    if not out:
+        raise SystemExit(f"no bench.py JSON line in {d}.*.log: the profiled runs' library hash is unknown")
+    return out
+
+
 def main():
     d, n, mode, solver, warmup, steps, out = sys.argv[1:8]
     n, warmup, steps = int(n), int(warmup), int(steps)
@@ -49,10 +63,11 @@ def main():
     valu = None
     if glob.glob(d + "/sq*counter_collection.csv"):
         valu, _ = per_step(step_rows(d + "/sq*counter_collection.csv", "SQ_INSTS_VALU"), warmup, steps)
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "gym-so100-c_amd"))
-    from gym_so100 import _native      # the library the passes profiled (SO100_LIB or the in-tree build)
+    hashes = profiled_hashes(d)
+    if len(set(hashes)) != 1:
+        raise SystemExit(f"the profiled passes' bench.py lines name {sorted(set(hashes))} library hashes")
     res = {"n_envs": n, "mode": mode, "solver": solver, "dispatches_per_step": p,
-           "lib_source_hash": _native.source_hash(), "lib_path": os.path.relpath(_native.LIB_PATH),
+           "lib_source_hash": hashes[0], "hash_source": f"{len(hashes)} profiled bench.py lines ({d}.*.log)",
            "fetch_kb_per_step": fetch, "write_kb_per_step": write,
            "hbm_bytes_per_step": (fetch + write) * 1024, "hbm_bytes_per_step_fetch_x2": (2 * fetch + write) * 1024,
            "hbm_bytes_per_env_step": (fetch + write) * 1024 / n, "valu_insts_per_step": valu,
