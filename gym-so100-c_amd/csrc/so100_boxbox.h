@@ -410,24 +410,25 @@ DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lan
     float bz = __builtin_inff(), bx = 0.f, by = 0.f;
     int bi = 0x7fffffff;
     if (mine) {
-      const int a = m->hull_body[k] - 2;
-      const float* R = sh.ser.xm[a];
-      const float* P = sh.ser.xp[a];
+      const float* R = sh.ser.xm[m->hull_body[k] - 2];
       const float r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5], r6 = R[6], r7 = R[7], r8 = R[8];
-      const float p0 = P[0], p1 = P[1], p2 = P[2];
       const int n = m->hull_count[k], s0 = m->hull_start[k];
+      // the lowest vertex by (R v).z, the hull-relative height (cm-sized, rounding ~1e-9 m), the body's position added
+      // once after the min: compared in world z (~0.5 m, rounding 3e-8 m) the corners of a hull face lying nearly flat
+      // tied, and fp32 picked another lowest corner than fp64, centimetres away (round 6; oracle table_hull_fast)
       for (int i = lane; i < n; i += kLanes) {
         const float4 v = verts[s0 + i];
-        const float wx = (r0 * v.x + r1 * v.y + r2 * v.z) + p0;
-        const float wy = (r3 * v.x + r4 * v.y + r5 * v.z) + p1;
-        const float wz = (r6 * v.x + r7 * v.y + r8 * v.z) + p2;
+        const float wx = r0 * v.x + r1 * v.y + r2 * v.z;
+        const float wy = r3 * v.x + r4 * v.y + r5 * v.z;
+        const float wz = r6 * v.x + r7 * v.y + r8 * v.z;
         if (wz < bz) { bz = wz; bx = wx; by = wy; bi = i; }
       }
     }
     arg_best16<true>(bz, bi, bx, by, bz);   // the score is the point's z (passed as both)
     if (lane == k) {
-      found = mine && bi != 0x7fffffff && (bz - top < m->pair_margin[SO100_NPAIR_BOX + k]);
-      hx = bx; hy = by; hz = bz;
+      const float* P = sh.ser.xp[m->hull_body[k] - 2];
+      hx = bx + P[0]; hy = by + P[1]; hz = bz + P[2];
+      found = mine && bi != 0x7fffffff && (hz - top < m->pair_margin[SO100_NPAIR_BOX + k]);
     }
   }
   return found;

@@ -570,6 +570,96 @@ DEV void everts_set(EpaVerts& V, int i, const float* v, int lane) {
   }
 }
 
+// The contact of EPA's final facet from the features it spans (round 6; oracle epa_feature_witness).  The facet lies on
+// a face of the Minkowski difference obj1 - obj2: obj1's vertex against obj2's face (one distinct obj1 support id,
+// three of obj2), obj1's face against obj2's vertex (three, one), or an edge of each (two, two); the contact is then
+// those features' exact one (the vertex and its projection on the face plane, or the edges' closest points with the
+// normal along their cross product), from the supports' own coordinates.  The barycentric interpolation over the facet
+// (the fallback for any other facet) depends on which triangle of the face EPA stopped on, and on a sliver facet (a
+// 1.2 m table edge beside a mm-long hull edge) fp32 lost 1e-2 of the weight along the long edge: the contact moved
+// centimetres between fp32 and fp64 (tools/dev/collision_precision.py).  Row-redundant; false: fall back.
+// The case is decided from the support ids alone, and only the 4 points it needs are rebuilt (P0 = obj1's point of
+// the facet's first vertex, P3 = obj2's; P1, P2 the features' other points): the 3 whole supports of the barycentric
+// path held across it spilled the 3-wave build.
+// obj1's (which = 1) or obj2's (2) point of the support with id `id`, by mpr_support's arithmetic (sup_from_id's)
+DEV void sup_point(const DevModel* __restrict__ m, const MprObj& o, uint32_t id, int which, float* r) {
+  float v1[3];
+#pragma unroll
+  for (int t = 0; t < 3; t++) v1[t] = o.c[t];
+  if (o.hull1 < 0) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const float sz = (id >> i) & 1u ? o.h[i] : -o.h[i];
+#pragma unroll
+      for (int t = 0; t < 3; t++) v1[t] += sz * o.ax[3 * t + i];
+    }
+  } else {
+    const float4 hv = reinterpret_cast<const float4*>(m->hull_vert)[o.s1 + (int)(id & 1023u)];
+    const float vv[3] = {hv.x, hv.y, hv.z};
+    float w[3];
+    mulmv3(w, o.ax, vv);
+#pragma unroll
+    for (int t = 0; t < 3; t++) v1[t] += w[t];
+  }
+  const float4 v2 = reinterpret_cast<const float4*>(m->hull_vert)[o.s0 + (int)((id >> 10) & 1023u)];
+  r[0] = which == 1 ? v1[0] : v2.x;
+  r[1] = which == 1 ? v1[1] : v2.y;
+  r[2] = which == 1 ? v1[2] : v2.z;
+}
+DEV bool epa_feature_witness(const DevModel* __restrict__ m, const MprObj& o, uint32_t ia, uint32_t ib, uint32_t ic,
+                             const float* fn, float& depth, float4& fdir, float4& fpos) {
+  const uint32_t a1 = ia & 1023u, b1 = ib & 1023u, c1 = ic & 1023u;
+  const uint32_t a2 = (ia >> 10) & 1023u, b2 = (ib >> 10) & 1023u, c2 = (ic >> 10) & 1023u;
+  const int n1 = 1 + (b1 != a1) + (c1 != a1 && c1 != b1);
+  const int n2 = 1 + (b2 != a2) + (c2 != a2 && c2 != b2);
+  const bool ee = n1 == 2 && n2 == 2, vf = n1 == 1 && n2 == 3, fvx = n1 == 3 && n2 == 1;
+  if (!(ee || vf || fvx)) return false;
+  // ee: P1 = obj1's other edge end, P2 = obj2's; vf: P1, P2 = obj2's face corners B2, C2; fvx: obj1's B1, C1
+  float P0[3], P1[3], P2[3], P3[3];
+  sup_point(m, o, ia, 1, P0);
+  sup_point(m, o, ia, 2, P3);
+  sup_point(m, o, ee ? (b1 != a1 ? ib : ic) : ib, vf ? 2 : 1, P1);
+  sup_point(m, o, ee ? (b2 != a2 ? ib : ic) : ic, fvx ? 1 : 2, P2);
+  float e1[3], e2[3], nn[3], w0[3], p1[3], p2[3];
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    e1[t] = P1[t] - (vf ? P3[t] : P0[t]);
+    e2[t] = P2[t] - (fvx ? P0[t] : P3[t]);
+    w0[t] = P0[t] - P3[t];
+  }
+  cross3(nn, e1, e2);
+  if (ee) {
+    const float a = dot3(e1, e1), b = dot3(e1, e2), c = dot3(e2, e2), dd = dot3(e1, w0), e = dot3(e2, w0);
+    const float den = a * c - b * b;
+    if (!(den > 1e-6f * a * c)) return false;   // (nearly) parallel edges: no single closest pair
+    const float t_ = (b * e - c * dd) / den, u_ = (a * e - b * dd) / den;
+#pragma unroll
+    for (int t = 0; t < 3; t++) { p1[t] = P0[t] + t_ * e1[t]; p2[t] = P3[t] + u_ * e2[t]; }
+  }
+  const float l = sqrtf(dot3(nn, nn));
+  if (ccd_zero(l)) return false;
+  const float il = (dot3(nn, fn) < 0.f ? -1.f : 1.f) / l;   // oriented as the facet's outward normal
+  nn[0] *= il; nn[1] *= il; nn[2] *= il;
+  float dep;
+  if (ee) {
+    float w[3];
+    sub3(w, p1, p2);
+    dep = dot3(nn, w);
+  } else {
+    dep = dot3(nn, w0);
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      p1[t] = vf ? P0[t] : P3[t] + dep * nn[t];
+      p2[t] = vf ? P0[t] - dep * nn[t] : P3[t];
+    }
+  }
+  if (!(dep > 0.f) || ccd_zero(dep)) return false;
+  depth = dep;
+  fdir = make_float4(nn[0], nn[1], nn[2], 0.f);
+  fpos = make_float4(0.5f * (p1[0] + p2[0]), 0.5f * (p1[1] + p2[1]), 0.5f * (p1[2] + p2[2]), 0.f);
+  return true;
+}
+
 // EPA from GJK's tetrahedron (oracle epa_penetration, the same bookkeeping order): true and (depth, dir
 // geom1 -> geom2, pos) on the facet reached.  P: the row's LDS polytope; lane: 0..15 in the row.
 DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const GjkPt* S, float& depth, float* dir,
@@ -778,12 +868,34 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
   if (best < 0) return false;
   depth = bd;
   if (ccd_zero(depth) || depth < 0.f) return false;
-  // witness points: barycentric coordinates of the origin's projection p = n dist on the facet
+  // the contact's witness is computed after the round's narrowphase, by one lane (epa_contact): the final facet's 3
+  // support ids go out in pos (as bits), its normal in dir (round 6: computed here, inside the narrowphase's register
+  // peak, the feature witness spilled the 3-wave build)
   const uint32_t fv = P.fv[best];
+  pos[0] = __uint_as_float(P.vid[fv & 31u]);
+  pos[1] = __uint_as_float(P.vid[(fv >> 5) & 31u]);
+  pos[2] = __uint_as_float(P.vid[(fv >> 10) & 31u]);
+#pragma unroll
+  for (int t = 0; t < 3; t++) dir[t] = bn[t];
+  return true;
+}
+
+// EPA's contact from its final facet (the support ids a, b, c and the facet's plane (n, dist)): the features' exact
+// contact (epa_feature_witness), else the witness points from the barycentric coordinates of the origin's projection
+// p = n dist on the facet (oracle epa_penetration).  In H: odir (normal), opos (xyz, the depth in w).
+DEV void epa_contact(const DevModel* __restrict__ m, const MprObj& o, uint32_t ia, uint32_t ib, uint32_t ic,
+                     const float* bn, float bd, float4& odir, float4& opos) {
+  float4 fdir, fpos;
+  float fdepth = bd;
+  if (epa_feature_witness(m, o, ia, ib, ic, bn, fdepth, fdir, fpos)) {
+    odir = fdir;
+    opos = make_float4(fpos.x, fpos.y, fpos.z, fdepth);
+    return;
+  }
   MprSup A, B, C;
-  sup_from_id(m, o, P.vid[fv & 31u], A);
-  sup_from_id(m, o, P.vid[(fv >> 5) & 31u], B);
-  sup_from_id(m, o, P.vid[(fv >> 10) & 31u], C);
+  sup_from_id(m, o, ia, A);
+  sup_from_id(m, o, ib, B);
+  sup_from_id(m, o, ic, C);
   const float p[3] = {bn[0] * bd, bn[1] * bd, bn[2] * bd};
   float l0, l1, l2;
   {
@@ -794,16 +906,17 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
     if (ccd_zero(den)) { l0 = 1.f; l1 = 0.f; l2 = 0.f; }
     else { l1 = (d11 * d20 - d01 * d21) / den; l2 = (d00 * d21 - d01 * d20) / den; l0 = 1.f - l1 - l2; }
   }
+  float q[3];
 #pragma unroll
   for (int t = 0; t < 3; t++) {
     float w1 = 0.f, w2 = 0.f;
     w1 += l0 * A.v1[t]; w2 += l0 * A.v2[t];
     w1 += l1 * B.v1[t]; w2 += l1 * B.v2[t];
     w1 += l2 * C.v1[t]; w2 += l2 * C.v2[t];
-    pos[t] = 0.5f * (w1 + w2);
-    dir[t] = bn[t];
+    q[t] = 0.5f * (w1 + w2);
   }
-  return true;
+  odir = make_float4(bn[0], bn[1], bn[2], 0.f);
+  opos = make_float4(q[0], q[1], q[2], bd);
 }
 
 // the mesh pairs' collider of the model (so100_model.convex): GJK + EPA (MuJoCo 3.3.3's default) or MPR
@@ -1011,22 +1124,90 @@ DEV float4 sphere_obj(const DevModel* __restrict__ m, const EnvShared& sh, int o
   return make_float4(c[0], c[1], c[2], r);
 }
 
-// a convex pair's contact (in hull k's body frame H) to the world, staged as the env's convex contact `slot`:
-// the LDS staging area, or (rare: beyond kMaxCon) the env's HBM contact record crec
+// A table-hull contact from GJK + EPA (pair p = 14 + k) whose world normal lies within 1e-5 rad of one of the table
+// box's face normals (world axes) is that face's contact (round 6; oracle table_face_snap): EPA stops within its
+// tolerance of the face normal, and under that residual tilt a hull lying flat on the face tied its corners, fp32 and
+// fp64 taking different ones.  Restated exactly: normal the face's axis u (table -> hull), the hull's extreme vertex
+// along -u (the first in hull order among ties, compared in hull-relative coordinates: the row's 16 lanes split the
+// vertices, a (score, index) min), depth from the face plane, pos the midpoint of the vertex and its projection on the
+// face.  Row-uniform; true when the contact snapped, with its WORLD-frame position and depth (wp: xyz, -depth in w)
+// and normal (wn: xyz) in their own registers (written into dir / pos, the arrays went to scratch).
+DEV bool table_face_snap(const DevModel* __restrict__ m, const EnvShared& sh, int p, const float* dir, int lane,
+                         float4& wpo, float4& wno) {
+  const int k = -1 - m->pair_g2[p];
+  float RH[9], pH[3], wn[3];
+  hull_frame(m, sh, m->hull_body[k], RH, pH);
+  mulmv3(wn, RH, dir);
+  const float a0 = fabsf(wn[0]), a1 = fabsf(wn[1]), a2 = fabsf(wn[2]);
+  const int ax = a1 > a0 ? (a2 > a1 ? 2 : 1) : (a2 > a0 ? 2 : 0);
+  const float o1 = ax == 0 ? wn[1] : wn[0], o2 = ax == 2 ? wn[1] : wn[2];
+  if (!(sqrtf(o1 * o1 + o2 * o2) < 1e-5f)) return false;
+  const float wa = ax == 0 ? wn[0] : ax == 1 ? wn[1] : wn[2];
+  const float sgn = wa > 0.f ? 1.f : -1.f;
+  const float lo = ax == 2 ? m->table_bottom : ax == 1 ? m->table_lo[1] : m->table_lo[0];
+  const float hi = ax == 2 ? m->table_top : ax == 1 ? m->table_hi[1] : m->table_hi[0];
+  const float face = sgn > 0.f ? hi : lo;
+  // the row of RH that gives the world coordinate on axis ax
+  const float ra = ax == 0 ? RH[0] : ax == 1 ? RH[3] : RH[6];
+  const float rb = ax == 0 ? RH[1] : ax == 1 ? RH[4] : RH[7];
+  const float rc = ax == 0 ? RH[2] : ax == 1 ? RH[5] : RH[8];
+  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert);
+  const int n = m->hull_count[k], s0 = m->hull_start[k];
+  float best = __builtin_inff(), bx = 0.f, by = 0.f;
+  int bi = 0x7fffffff;
+  for (int i = lane; i < n; i += kLanes) {
+    const float4 v = verts[s0 + i];
+    const float h = sgn * (ra * v.x + rb * v.y + rc * v.z);
+    if (h < best) { best = h; bx = v.x; by = v.y; bi = i; }
+  }
+  float bz = 0.f;
+  {
+    float hz = 0.f;
+    // (score, index) min over the row; the winner's body-frame x, y ride along, z from the vertex table after
+    arg_best16<true>(best, bi, bx, by, hz);
+    const float4 v = verts[s0 + (bi == 0x7fffffff ? 0 : bi)];
+    bz = v.z;
+    bx = v.x; by = v.y;
+  }
+  const float hv[3] = {bx, by, bz};
+  float wb[3];
+  mulmv3(wb, RH, hv);
+  wb[0] += pH[0]; wb[1] += pH[1]; wb[2] += pH[2];
+  const float wax = ax == 0 ? wb[0] : ax == 1 ? wb[1] : wb[2];
+  const float mid = 0.5f * (wax + face);
+  wpo = make_float4(ax == 0 ? mid : wb[0], ax == 1 ? mid : wb[1], ax == 2 ? mid : wb[2], sgn * wax - sgn * face);
+  wno = make_float4(ax == 0 ? sgn : 0.f, ax == 1 ? sgn : 0.f, ax == 2 ? sgn : 0.f, 0.f);
+  return true;
+}
+
+// a convex pair's contact (in hull k's body frame H; world: already in the world frame, table_face_snap) to the world,
+// staged as the env's convex contact `slot`: the LDS staging area, or (rare: beyond kMaxCon) the env's HBM contact
+// record crec
 DEV void stage_convex_hit(const DevModel* __restrict__ m, EnvShared& sh, float* crec, int slot, int p, float depth,
-                          const float* dir, const float* pos) {
+                          const float* dir_in, const float* pos_in, bool world, float4 wpo, float4 wno) {
   const int k = -1 - m->pair_g2[p];
   float RH[9], pH[3], wn[3], wp[3];
+  float4 hd = make_float4(dir_in[0], dir_in[1], dir_in[2], 0.f), hp = make_float4(pos_in[0], pos_in[1], pos_in[2], depth);
+  if (m->convex != SO100_CONVEX_MPR && !world) {
+    // GJK + EPA: the contact from the final facet's support ids (pos_in) and plane (dir_in, depth)
+    MprObj o;
+    mpr_obj_setup(m, sh, p, o);
+    epa_contact(m, o, __float_as_uint(pos_in[0]), __float_as_uint(pos_in[1]), __float_as_uint(pos_in[2]), dir_in, depth,
+                hd, hp);
+  }
+  const float dir[3] = {hd.x, hd.y, hd.z}, pos[3] = {hp.x, hp.y, hp.z};
+  depth = hp.w;
   hull_frame(m, sh, m->hull_body[k], RH, pH);
   mulmv3(wn, RH, dir);
   mulmv3(wp, RH, pos);
-  const float4 sp = make_float4(wp[0] + pH[0], wp[1] + pH[1], wp[2] + pH[2], -depth);
-  const float4 sn = make_float4(wn[0], wn[1], wn[2], __int_as_float(p));
+  const float4 sp = world ? wpo : make_float4(wp[0] + pH[0], wp[1] + pH[1], wp[2] + pH[2], -depth);
+  const float4 sn = world ? make_float4(wno.x, wno.y, wno.z, __int_as_float(p))
+                          : make_float4(wn[0], wn[1], wn[2], __int_as_float(p));
   if (slot < kMaxCon) {
     MprStage& st = sh.mpr[slot];
     st.pos[0] = sp.x; st.pos[1] = sp.y; st.pos[2] = sp.z; st.pos[3] = sp.w;
     st.nrm[0] = sn.x; st.nrm[1] = sn.y; st.nrm[2] = sn.z; st.nrm[3] = sn.w;
-  } else if (crec) {               // (fused path: an env without a pool record collides again with one)
+  } else if (crec) {               // (fused path: no record only if the pool ran out, which its sizing rules out)
     float4* stg = reinterpret_cast<float4*>(crec + (size_t)slot * kConStride + kMprStageOff);
     stg[0] = sp;
     stg[1] = sn;
@@ -1212,7 +1393,8 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
     const bool act = item < total;
     const int ie = env_of(item);
     float depth = 0.f, dir[3] = {0.f, 0.f, 0.f}, pos[3] = {0.f, 0.f, 0.f};
-    bool hit = false;
+    bool hit = false, world = false;
+    float4 wpo = make_float4(0.f, 0.f, 0.f, 0.f), wno = wpo;    // table_face_snap's world-frame contact
     int p = SO100_PAIR_MPR0;
     if (act) {
       const int q = reinterpret_cast<const uint8_t*>(&shm[ie].ser.cdd[0][0])[item - pre_of(ie)];
@@ -1237,6 +1419,8 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
       if (!proved) {
         if (lane == 0 && c.w != 0.f) sc->w = 0.f;   // stale: invalidated (GJK stores a new one if it separates)
         hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp, sc);
+        if (hit && q >= kTableItem0 && m->convex != SO100_CONVEX_MPR)
+          world = table_face_snap(m, shm[ie], p, dir, lane, wpo, wno);
       }
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first
@@ -1258,10 +1442,10 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
     }
     if (hit && lane == 0) {
       // the env's record: the split path's per-env record (crec0: the wave's first env's), or the fused path's pool
-      // record (crec0: the pool) if the env holds one (else its contacts beyond kMaxCon are not stored: assemble
-      // collides again with a record)
+      // record (crec0: the pool) if the env holds one (none only if the pool ran out, which its sizing rules out: the
+      // contacts beyond kMaxCon are then not stored, and assemble counts them in ncon_dropped)
       float* const rb = kCells ? pool_rec(w, shm[0].rec, ie) : crec0 + (size_t)ie * kConEnv;
-      stage_convex_hit(m, shm[ie], rb, slot, p, depth, dir, pos);
+      stage_convex_hit(m, shm[ie], rb, slot, p, depth, dir, pos, world, wpo, wno);
     }
     fpk = fnew;
   }

@@ -665,8 +665,13 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           if (kOvf && ncon_max > kMaxCon) l1 += ovf_l10;
           d10 = rowsum16(l1) + A1;
         }
+        // the Newton decrement (fp32 stop, round 6; oracle NEWTON_DECREMENT): a full step along s = -H^-1 g would
+        // lower the cost by -c'(0) / 2; below MuJoCo's tolerance (scaled) the solve is done.  It replaces the relative
+        // cost-improvement stop of rounds 3-5 (1e-6 of |cost|), which ended EE solves (the weld folded into M: a large
+        // cost) short of the minimiser; MuJoCo's own stops are below fp32 resolution here (DESIGN.md §4 deviation 8)
+        const bool converged = scale * (-0.5f * d10) < tolerance;
         float alpha = 0.f;
-        if (d10 < 0.f) {
+        if (!converged && d10 < 0.f) {
           // fp32 stops (oracle LS_TOL / LS_STEP): MuJoCo's ls_tolerance 0.01 on |c'|, or a relative step 1e-4
           const float tol_ls = 1e-2f * -d10;
           float lo = 0.f, hi = -1.f;
@@ -684,7 +689,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             alpha = nxt;
           }
         }
-        iters = it + 1;
+        if (!converged) iters = it + 1;
         STAMP(5);
         if (alpha == 0.f) {
           done = true;
@@ -718,8 +723,8 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           const float improvement = scale * (cost - nc);
           cost = nc;
           last_impr = improvement;
-          // MuJoCo's test, and the fp32 relative one (oracle NEWTON_RELTOL): 1e-8 is below fp32 resolution
-          if (improvement < tolerance || improvement < 1e-6f * scale * fabsf(cost)) done = true;
+          // MuJoCo's test (the Newton decrement above is the fp32 stop that resolves)
+          if (improvement < tolerance) done = true;
         }
         STAMP(6);
       }

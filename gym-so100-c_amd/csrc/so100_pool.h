@@ -19,7 +19,9 @@ namespace so100 {
 // count, 8-32 entries per XCD, and let a wave finding none sleep and retry, then after about a second keep its first
 // kMaxCon contacts: a dropped contact depended on timing.)  The scan is bounded by kPoolScans; not finding an entry
 // there would contradict the sizing, and is reported, not hidden: the entry is -2, the envs keep their first kMaxCon
-// contacts counted in ncon_dropped (every test asserts 0) and Workspace::pool_stat[1] counts the event.
+// contacts counted in ncon_dropped (every test asserts 0) and Workspace::pool_stat[1] counts the event (the wave counts
+// its takes and failures in LDS, shm[1].rec / shm[2].rec, and adds them to pool_stat once, in the epilogue: an atomic
+// here, inside the collision phase's register peak, spilled the 3-wave build).
 constexpr int kPoolScans = 64;
 DEV int xcc_id() {
   int x;
@@ -40,15 +42,11 @@ DEV int pool_acquire(const Workspace& w) {
         // acquire: the entry's previous holder's accesses, released below, happen before this holder's;
         // the agent-scope acquire also drops this CU's L1 copies of the entry's lines
         const uint32_t old = __hip_atomic_fetch_or(bm + k, 1u << b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (!(old & (1u << b))) {
-          if (w.pool_stat) __hip_atomic_fetch_add(w.pool_stat, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return x * kPoolSlots + 32 * k + b;
-        }
+        if (!(old & (1u << b))) return x * kPoolSlots + 32 * k + b;
         cur = old | (1u << b);
       }
     }
   }
-  if (w.pool_stat) __hip_atomic_fetch_add(w.pool_stat + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return -2;
 }
 // env grp's record in pool entry `ent` (XCD ent / kPoolSlots, bit ent % kPoolSlots of its bitmap), or nullptr for

@@ -222,7 +222,7 @@ DEV void store_contact(EnvShared& sh, float* crec, int slot, const float* fr, fl
     sh.con[slot].g.pos[2] = p2; sh.con[slot].g.pos[3] = dist;
     sh.con_dist[slot] = dist;
     sh.con_pair[slot] = pair;
-  } else if (crec) {               // (fused path: an env without a pool record collides again with one)
+  } else if (crec) {               // (fused path: no record only if the pool ran out, which its sizing rules out)
     float4* g = reinterpret_cast<float4*>(crec + (size_t)slot * kConStride + kGeoOff);
     g[0] = make_float4(p0, p1, p2, dist);
     g[1] = make_float4(fr[0], fr[1], fr[2], fr[3]);
@@ -1116,8 +1116,10 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
   load_state(args, lane, e, qpos_r, qvel_r, warm_r, mscale, fscale, sigma, elapsed0, episode0);
   set_controls(args, sh, lane, e, sigma, elapsed0, episode0);
   if (lane == 0) {
-    sh.rec = -1;                  // no pool entry held (the wave's: shm[0].rec)
-    sh.ndrop = 0;                 // contacts left out over the step (the pool's safety valve only)
+    // shm[0].rec: the wave's pool entry (-1: none held); shm[1].rec / shm[2].rec: the entries it took and the requests
+    // that found none free over the step (added to Workspace::pool_stat in the epilogue)
+    sh.rec = grp == 0 ? -1 : 0;
+    sh.ndrop = 0;                 // contacts left out over the step (0: the pool is sized never to run out)
   }
   const int nsub = args.m->nsubstep;
   const float h = args.m->timestep;
@@ -1177,8 +1179,10 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
       int l2, g2, en2, e2;
       fresh_ids(group, args.n, l2, g2, en2, e2);
       if (l2 == 0 && g2 == 0) {
-        if (shm[0].rec >= 0) pool_release(args.w, shm[0].rec);
-        shm[0].rec = -1;                  // (also after the safety valve's -2: the next substep tries again)
+        const int ent = shm[0].rec;
+        if (ent >= 0) pool_release(args.w, ent);
+        if (ent != -1) shm[ent >= 0 ? 1 : 2].rec++;
+        shm[0].rec = -1;                  // (also after a failed request's -2: the next substep asks again)
       }
     }
     TL_MARK(1);
@@ -1199,6 +1203,11 @@ __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const Dev
     final_stage(args, sh, lane, grp, env, e, valid, qpos_r, qvel_r, warm_r, el0, ep0);
     if (valid && lane == 0 && args.b.ncon_dropped) args.b.ncon_dropped[env] = (uint32_t)sh.ndrop;
     if (args.w.gcost && lane == 0 && grp == 0) args.w.gcost[group] = (uint32_t)(__builtin_amdgcn_s_memtime() - cost_t0);
+    if (lane == 0 && grp == 0 && args.w.pool_stat) {
+      const int took = shm[1].rec, none = shm[2].rec;
+      if (took) __hip_atomic_fetch_add(args.w.pool_stat, (unsigned long long)took, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (none) __hip_atomic_fetch_add(args.w.pool_stat + 1, (unsigned long long)none, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   TL_MARK(2);
 #ifdef SO100_TIMELINE

@@ -1055,7 +1055,7 @@ static int epa_feature_witness(const mpr_sup* V, const epa_face* f, real* depth,
  * distance; a face is visible from w when n . w - dist > 0; the horizon is the visible faces' edges whose twin
  * lies on no visible face, in (slot, edge) order; each horizon edge (a, b) in turn gets the face (a, b, w) in the
  * lowest free slot (a degenerate face takes none). */
-static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir[3], real pos[3]) {
+static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir[3], real pos[3], real fn[3]) {
   mpr_sup V[EPA_MAXV];
   epa_face F[EPA_MAXF];
   int nv = 4;
@@ -1118,6 +1118,7 @@ static int epa_penetration(const mpr_obj* o, mpr_sup S[4], real* depth, real dir
   const epa_face* f = &F[best];
   *depth = f->dist;
   if (ccd_zero(*depth) || *depth < 0) return 0;           /* touching: no normal (as MPR) */
+  for (int t = 0; t < 3; t++) fn[t] = f->n[t];             /* the facet's normal (table_face_snap tests it) */
   /* barycentric coordinates of the origin's projection p = n dist on the facet */
   real p[3] = {f->n[0] * f->dist, f->n[1] * f->dist, f->n[2] * f->dist}, l[3];
   {
@@ -1169,13 +1170,17 @@ static int box_axes_separate(const mpr_obj* o) {
 #endif
 
 static int convex_penetration(const so100_model* m, const mpr_obj* o, real* depth, real dir[3], real pos[3],
-                              real dsep[4]) {
+                              real dsep[4], real fn[3]) {
   dsep[0] = dsep[1] = dsep[2] = dsep[3] = 0;
-  if (m->convex == SO100_CONVEX_MPR) return mpr_penetration(o, depth, dir, pos);
+  if (m->convex == SO100_CONVEX_MPR) {
+    const int r = mpr_penetration(o, depth, dir, pos);
+    for (int t = 0; t < 3; t++) fn[t] = dir[t];
+    return r;
+  }
   mpr_sup S[4];
   if (!gjk(o, S, dsep)) return 0;
   STAT(1, 1);
-  return epa_penetration(o, S, depth, dir, pos);
+  return epa_penetration(o, S, depth, dir, pos, fn);
 }
 
 /* conservative broadphase for (box, hull k) in H: bounding spheres, then OBB-OBB separating axes
@@ -1242,7 +1247,8 @@ static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
   for (int c = 0; c < n; c++) add_contact(d, &tmp[c], p);
 }
 
-/* A hull-table contact from GJK + EPA whose normal lies within kTableSnap of one of the table box's face normals
+/* A hull-table contact from GJK + EPA whose final facet's normal (wn, world) lies within TABLE_SNAP of one of the table
+ * box's face normals
  * (world axes: the table is axis-aligned) is that face's contact: EPA stops within its tolerance of the face normal
  * (1e-6 of the facet distance: normals off by up to ~1e-6 rad), and the witness it interpolates on a Minkowski facet
  * then depends on that residual tilt (a hull corner a centimetre away wins under a 1e-7 rad tilt when the hull lies
@@ -1252,14 +1258,13 @@ static void collide_box_pair(const so100_model* m, so100o_data* d, int p) {
  * coordinates) and its projection on the face: pos their midpoint.  The top-face rule (table_hull_fast) is this on the
  * top face where it is provably the minimum penetration; here EPA has established that the face is. */
 #define TABLE_SNAP ((real)1e-5)
-static void table_face_snap(const so100_model* m, so100o_data* d, int k, so100o_contact* con) {
+static void table_face_snap(const so100_model* m, so100o_data* d, int k, const real wn[3], so100o_contact* con) {
   int ax = 0;
   for (int i = 1; i < 3; i++)
-    if ((real)fabs((double)con->frame[i]) > (real)fabs((double)con->frame[ax])) ax = i;
-  const real off = (real)sqrt((double)(con->frame[(ax + 1) % 3] * con->frame[(ax + 1) % 3] +
-                                       con->frame[(ax + 2) % 3] * con->frame[(ax + 2) % 3]));
+    if ((real)fabs((double)wn[i]) > (real)fabs((double)wn[ax])) ax = i;
+  const real off = (real)sqrt((double)(wn[(ax + 1) % 3] * wn[(ax + 1) % 3] + wn[(ax + 2) % 3] * wn[(ax + 2) % 3]));
   if (!(off < TABLE_SNAP)) return;
-  const real sgn = con->frame[ax] > 0 ? (real)1 : (real)-1;
+  const real sgn = wn[ax] > 0 ? (real)1 : (real)-1;
   const int p = SO100_NPAIR_BOX + k, b = m->hull_body[k], g = m->pair_geom1[p];
   const real top = (real)m->table_top, bottom = top - 2 * (real)m->geom_size[g][2];
   const real lo = ax == 2 ? bottom : (real)m->table_lo[ax], hi = ax == 2 ? top : (real)m->table_hi[ax];
@@ -1338,8 +1343,8 @@ static void convex_pair(const so100_model* m, so100o_data* d, int p) {
     mpr_support(&o, du, &a);
     if (dot3(a.v, du) < -SEP_TOL) { d->sep_hits++; return; }
   }
-  real dsep[4];
-  const int hit_ = convex_penetration(m, &o, &depth, dir, pos, dsep);
+  real dsep[4], fn[3];
+  const int hit_ = convex_penetration(m, &o, &depth, dir, pos, dsep, fn);
   for (int k = 0; k < 4; k++) d->sep[p][k] = dsep[k];
   d->sep_sep += dsep[3] != 0;
 #ifdef SO100O_STATS
@@ -1353,7 +1358,11 @@ static void convex_pair(const so100_model* m, so100o_data* d, int p) {
   mulmv3(con.pos, RH, pos);
   for (int t = 0; t < 3; t++) con.pos[t] += d->xpos[b][t];
   con.dist = -depth;
-  if (g == 0) table_face_snap(m, d, k, &con);
+  if (g == 0 && m->convex != SO100_CONVEX_MPR) {
+    real wfn[3];
+    mulmv3(wfn, RH, fn);
+    table_face_snap(m, d, k, wfn, &con);
+  }
   add_contact(d, &con, p);
 }
 
