@@ -389,49 +389,4 @@ DEV int table_hull_class(const DevModel* __restrict__ m, const EnvShared& sh, in
   return fast ? 3 : 1;
 }
 
-// The top-face rule's contacts: for the hulls table_hull_class puts under it in some env of the wave, the env's 16
-// lanes split the vertices (lane, lane + 16, ...) and a 16-lane lexicographic (z, vertex index) min gives the
-// oracle's first lowest vertex.  Needs the link frames of fk_stage (sh.ser.xm / xp).  Lane k < SO100_NHULL returns
-// hull k's contact flag (its lowest vertex below top + margin) and its lowest vertex.
-DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lane, int grp, bool valid, float& hx,
-                    float& hy, float& hz) {
-  bool found = false;
-  hx = hy = hz = 0.f;
-  const float top = m->table_top;
-  const bool cand = table_hull_class(m, sh, lane, valid) == 3;
-  const uint64_t cm = __ballot(cand);
-  const uint32_t env_cand = (uint32_t)(cm >> (grp * 16)) & 0xFFFFu;
-  uint32_t wave_cand = (uint32_t)((cm | (cm >> 16) | (cm >> 32) | (cm >> 48)) & 0xFFFFull);
-  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert);
-  while (wave_cand) {
-    const int k = __builtin_ctz(wave_cand);
-    wave_cand &= wave_cand - 1u;
-    const bool mine = (env_cand >> k) & 1u;
-    float bz = __builtin_inff(), bx = 0.f, by = 0.f;
-    int bi = 0x7fffffff;
-    if (mine) {
-      const float* R = sh.ser.xm[m->hull_body[k] - 2];
-      const float r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5], r6 = R[6], r7 = R[7], r8 = R[8];
-      const int n = m->hull_count[k], s0 = m->hull_start[k];
-      // the lowest vertex by (R v).z, the hull-relative height (cm-sized, rounding ~1e-9 m), the body's position added
-      // once after the min: compared in world z (~0.5 m, rounding 3e-8 m) the corners of a hull face lying nearly flat
-      // tied, and fp32 picked another lowest corner than fp64, centimetres away (round 6; oracle table_hull_fast)
-      for (int i = lane; i < n; i += kLanes) {
-        const float4 v = verts[s0 + i];
-        const float wx = r0 * v.x + r1 * v.y + r2 * v.z;
-        const float wy = r3 * v.x + r4 * v.y + r5 * v.z;
-        const float wz = r6 * v.x + r7 * v.y + r8 * v.z;
-        if (wz < bz) { bz = wz; bx = wx; by = wy; bi = i; }
-      }
-    }
-    arg_best16<true>(bz, bi, bx, by, bz);   // the score is the point's z (passed as both)
-    if (lane == k) {
-      const float* P = sh.ser.xp[m->hull_body[k] - 2];
-      hx = bx + P[0]; hy = by + P[1]; hz = bz + P[2];
-      found = mine && bi != 0x7fffffff && (hz - top < m->pair_margin[SO100_NPAIR_BOX + k]);
-    }
-  }
-  return found;
-}
-
 }  // namespace so100

@@ -153,6 +153,46 @@ DEV float4 hull_support(const DevModel* __restrict__ m, bool cells, int k, int s
   return make_float4(bx, by, bz, __int_as_float(bi));
 }
 
+// The top-face rule's contacts (oracle table_hull_fast): for the hulls table_hull_class puts under it in some env of
+// the wave, the env's row finds the hull's lowest vertex by its support (hull_support) in the body-frame direction of
+// world -z.  Needs the link frames of fk_stage (sh.ser.xm / xp).  Lane k < SO100_NHULL returns
+// hull k's contact flag (its lowest vertex below top + margin) and its lowest vertex.
+DEV bool hull_table(const DevModel* __restrict__ m, const EnvShared& sh, int lane, int grp, bool valid, float& hx,
+                    float& hy, float& hz) {
+  bool found = false;
+  hx = hy = hz = 0.f;
+  const float top = m->table_top;
+  const bool cand = table_hull_class(m, sh, lane, valid) == 3;
+  const uint64_t cm = __ballot(cand);
+  const uint32_t env_cand = (uint32_t)(cm >> (grp * 16)) & 0xFFFFu;
+  uint32_t wave_cand = (uint32_t)((cm | (cm >> 16) | (cm >> 32) | (cm >> 48)) & 0xFFFFull);
+  while (wave_cand) {
+    const int k = __builtin_ctz(wave_cand);
+    wave_cand &= wave_cand - 1u;
+    const bool mine = (env_cand >> k) & 1u;
+    float bz = __builtin_inff(), bx = 0.f, by = 0.f;
+    int bi = 0x7fffffff;
+    if (mine) {
+      // the lowest vertex: hull k's support in the body-frame direction -R' e_z (its first maximal vertex: a whole-hull
+      // scan, 8 loads in flight per lane; the cells' lookup spilled the 3-wave build here), in hull-relative terms; the body's
+      // position is added after (compared in world z, ~0.5 m with 3e-8 m rounding, a hull face lying nearly flat
+      // tied its corners and fp32 picked another than fp64, centimetres away; round 6, oracle table_hull_fast)
+      const float* R = sh.ser.xm[m->hull_body[k] - 2];
+      const float4 v = hull_support(m, false, k, m->hull_start[k], m->hull_count[k], -R[6], -R[7], -R[8], lane);
+      const float hv[3] = {v.x, v.y, v.z};
+      float w[3];
+      mulmv3(w, R, hv);
+      bx = w[0]; by = w[1]; bz = w[2]; bi = __float_as_int(v.w);
+    }
+    if (lane == k) {
+      const float* P = sh.ser.xp[m->hull_body[k] - 2];
+      hx = bx + P[0]; hy = by + P[1]; hz = bz + P[2];
+      found = mine && bi != 0x7fffffff && (hz - top < m->pair_margin[SO100_NPAIR_BOX + k]);
+    }
+  }
+  return found;
+}
+
 DEV void mpr_support(const DevModel* __restrict__ m, const MprObj& o, const float* d, MprSup& s, int lane) {
   uint32_t id = 0u;
 #pragma unroll
@@ -885,6 +925,7 @@ DEV bool epa_penetration(const DevModel* __restrict__ m, const MprObj& o, const 
 // p = n dist on the facet (oracle epa_penetration).  In H: odir (normal), opos (xyz, the depth in w).
 DEV void epa_contact(const DevModel* __restrict__ m, const MprObj& o, uint32_t ia, uint32_t ib, uint32_t ic,
                      const float* bn, float bd, float4& odir, float4& opos) {
+#ifndef SO100_NO_FEAT   // (A/B switch: the barycentric witness alone, round 5's)
   float4 fdir, fpos;
   float fdepth = bd;
   if (epa_feature_witness(m, o, ia, ib, ic, bn, fdepth, fdir, fpos)) {
@@ -892,6 +933,7 @@ DEV void epa_contact(const DevModel* __restrict__ m, const MprObj& o, uint32_t i
     opos = make_float4(fpos.x, fpos.y, fpos.z, fdepth);
     return;
   }
+#endif
   MprSup A, B, C;
   sup_from_id(m, o, ia, A);
   sup_from_id(m, o, ib, B);
@@ -1128,12 +1170,12 @@ DEV float4 sphere_obj(const DevModel* __restrict__ m, const EnvShared& sh, int o
 // box's face normals (world axes) is that face's contact (round 6; oracle table_face_snap): EPA stops within its
 // tolerance of the face normal, and under that residual tilt a hull lying flat on the face tied its corners, fp32 and
 // fp64 taking different ones.  Restated exactly: normal the face's axis u (table -> hull), the hull's extreme vertex
-// along -u (the first in hull order among ties, compared in hull-relative coordinates: the row's 16 lanes split the
-// vertices, a (score, index) min), depth from the face plane, pos the midpoint of the vertex and its projection on the
-// face.  Row-uniform; true when the contact snapped, with its WORLD-frame position and depth (wp: xyz, -depth in w)
+// along -u (the first in hull order among ties, compared in hull-relative coordinates: the hull's support in the body-
+// frame direction, through the cube-map cells on the fused path), depth from the face plane, pos the midpoint of the
+// vertex and its projection on the face.  Row-uniform; true when the contact snapped, with its WORLD-frame position and depth (wp: xyz, -depth in w)
 // and normal (wn: xyz) in their own registers (written into dir / pos, the arrays went to scratch).
 DEV bool table_face_snap(const DevModel* __restrict__ m, const EnvShared& sh, int p, const float* dir, int lane,
-                         float4& wpo, float4& wno) {
+                         const MprObj& o, float4& wpo, float4& wno) {
   const int k = -1 - m->pair_g2[p];
   float RH[9], pH[3], wn[3];
   hull_frame(m, sh, m->hull_body[k], RH, pH);
@@ -1151,25 +1193,10 @@ DEV bool table_face_snap(const DevModel* __restrict__ m, const EnvShared& sh, in
   const float ra = ax == 0 ? RH[0] : ax == 1 ? RH[3] : RH[6];
   const float rb = ax == 0 ? RH[1] : ax == 1 ? RH[4] : RH[7];
   const float rc = ax == 0 ? RH[2] : ax == 1 ? RH[5] : RH[8];
-  const float4* __restrict__ verts = reinterpret_cast<const float4*>(m->hull_vert);
-  const int n = m->hull_count[k], s0 = m->hull_start[k];
-  float best = __builtin_inff(), bx = 0.f, by = 0.f;
-  int bi = 0x7fffffff;
-  for (int i = lane; i < n; i += kLanes) {
-    const float4 v = verts[s0 + i];
-    const float h = sgn * (ra * v.x + rb * v.y + rc * v.z);
-    if (h < best) { best = h; bx = v.x; by = v.y; bi = i; }
-  }
-  float bz = 0.f;
-  {
-    float hz = 0.f;
-    // (score, index) min over the row; the winner's body-frame x, y ride along, z from the vertex table after
-    arg_best16<true>(best, bi, bx, by, hz);
-    const float4 v = verts[s0 + (bi == 0x7fffffff ? 0 : bi)];
-    bz = v.z;
-    bx = v.x; by = v.y;
-  }
-  const float hv[3] = {bx, by, bz};
+  // the hull's extreme vertex along -u: its support in the body-frame direction -sgn (ra, rb, rc) (the first maximal
+  // vertex: the cube-map cells' candidates on the fused path, the whole hull on the split path, the same vertex)
+  const float4 v = hull_support(m, o.cells, k, o.s0, o.n, -sgn * ra, -sgn * rb, -sgn * rc, lane);
+  const float hv[3] = {v.x, v.y, v.z};
   float wb[3];
   mulmv3(wb, RH, hv);
   wb[0] += pH[0]; wb[1] += pH[1]; wb[2] += pH[2];
@@ -1187,16 +1214,7 @@ DEV void stage_convex_hit(const DevModel* __restrict__ m, EnvShared& sh, float* 
                           const float* dir_in, const float* pos_in, bool world, float4 wpo, float4 wno) {
   const int k = -1 - m->pair_g2[p];
   float RH[9], pH[3], wn[3], wp[3];
-  float4 hd = make_float4(dir_in[0], dir_in[1], dir_in[2], 0.f), hp = make_float4(pos_in[0], pos_in[1], pos_in[2], depth);
-  if (m->convex != SO100_CONVEX_MPR && !world) {
-    // GJK + EPA: the contact from the final facet's support ids (pos_in) and plane (dir_in, depth)
-    MprObj o;
-    mpr_obj_setup(m, sh, p, o);
-    epa_contact(m, o, __float_as_uint(pos_in[0]), __float_as_uint(pos_in[1]), __float_as_uint(pos_in[2]), dir_in, depth,
-                hd, hp);
-  }
-  const float dir[3] = {hd.x, hd.y, hd.z}, pos[3] = {hp.x, hp.y, hp.z};
-  depth = hp.w;
+  const float dir[3] = {dir_in[0], dir_in[1], dir_in[2]}, pos[3] = {pos_in[0], pos_in[1], pos_in[2]};
   hull_frame(m, sh, m->hull_body[k], RH, pH);
   mulmv3(wn, RH, dir);
   mulmv3(wp, RH, pos);
@@ -1419,8 +1437,22 @@ DEV int mpr_contacts(const DevModel* __restrict__ m, const Workspace& w, EnvShar
       if (!proved) {
         if (lane == 0 && c.w != 0.f) sc->w = 0.f;   // stale: invalidated (GJK stores a new one if it separates)
         hit = convex_penetration(m, o, depth, dir, pos, *reinterpret_cast<EpaPoly*>(&shm[grp].con[0]), lane, grp, sc);
-        if (hit && q >= kTableItem0 && m->convex != SO100_CONVEX_MPR)
-          world = table_face_snap(m, shm[ie], p, dir, lane, wpo, wno);
+        if (hit && m->convex != SO100_CONVEX_MPR) {
+#ifndef SO100_NO_SNAP   // (A/B switch: no table-face snap, round 5's EPA contact)
+          if (q >= kTableItem0) world = table_face_snap(m, shm[ie], p, dir, lane, o, wpo, wno);
+#endif
+          if (!world) {
+            // the contact from EPA's final facet (its support ids came out in pos, its plane in dir and depth), by the
+            // row, with the pair's MprObj still in hand (on the staging lane it had to be set up again: slower at
+            // 8,192 envs, where the step waits for the heavy envs' convex items)
+            float4 hd, hp;
+            epa_contact(m, o, __float_as_uint(pos[0]), __float_as_uint(pos[1]), __float_as_uint(pos[2]), dir, depth, hd,
+                        hp);
+            dir[0] = hd.x; dir[1] = hd.y; dir[2] = hd.z;
+            pos[0] = hp.x; pos[1] = hp.y; pos[2] = hp.z;
+            depth = hp.w;
+          }
+        }
       }
     }
     // this round's hits, row g at bit 16 g; rows earlier in the list with the same env come first

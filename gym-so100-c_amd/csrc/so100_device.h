@@ -182,7 +182,7 @@ enum NewtonHdr : int {
 };
 static_assert(N_FRAREF + 12 <= H_NCON && N_MC + 6 <= kHdrEnv, "Newton header layout");
 constexpr int kPgsEnvs = 16;      // solver: envs per wave64 (4 lanes each) = one "group"
-constexpr int kResident = 4;      // solver: contacts per env held on-chip across the sweeps
+constexpr int kResident = 6;      // solver: contacts per env held on-chip across the sweeps (round 6: 4 -> 6, +1 %, profiles/r05_ab_pgs_resident.txt)
 constexpr int kHeavyCap = 512;    // solver: groups with > kResident contacts dispatched first (cap)
 struct Workspace {
   float* hdr;

@@ -41,7 +41,11 @@ DEV int pool_acquire(const Workspace& w) {
         const int b = __builtin_ctz(~cur);
         // acquire: the entry's previous holder's accesses, released below, happen before this holder's;
         // the agent-scope acquire also drops this CU's L1 copies of the entry's lines
+#ifdef SO100_POOL_R5   // (A/B switch: round 5's relaxed take)
+        const uint32_t old = atomicOr(bm + k, 1u << b);
+#else
         const uint32_t old = __hip_atomic_fetch_or(bm + k, 1u << b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (!(old & (1u << b))) return x * kPoolSlots + 32 * k + b;
         cur = old | (1u << b);
       }
@@ -61,7 +65,11 @@ DEV void pool_release(const Workspace& w, int ent) {
   // "memory" clobber keeps the compiler from moving any of them past it (__builtin_amdgcn_s_waitcnt is not a
   // compiler barrier).  No data passes to the next holder (a holder reads only what it wrote in its own substep) and
   // both holders meet in this XCD's L2, so no L2 write-back is needed: the release orders completion, not visibility.
+#ifdef SO100_POOL_R5
+  __builtin_amdgcn_s_waitcnt(0);
+#else
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
   const int x = ent / kPoolSlots, b = ent % kPoolSlots;
   __hip_atomic_fetch_and(w.pool_bm + x * kPoolWords + (b >> 5), ~(1u << (b & 31)), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);

@@ -1067,10 +1067,10 @@ DEV void fresh_ids(int group, int n, int& lane, int& grp, int& env, int& e) {
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
 // functions on the same values.  kDebug: the instantiation that also fills the debug buffer (launched when
 // the caller passes one); the other has no debug code, which costs registers in the substep loop.
-// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, 72 B/lane of spill slots) when
-// the grid exceeds 2 waves per SIMD; a grid of at most 2 waves per SIMD (8,192 envs on 256 CUs: all waves
-// resident at once) takes the 2-wave build (186 VGPRs, no scratch; +0.8 % there, -7 % at 16,384 envs).
-// Register allocation only: both give the same results bit for bit.
+// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, no scratch since round 5) when the
+// grid exceeds 2 waves per SIMD; a grid of at most 2 waves per SIMD (8,192 envs on 256 CUs: all waves resident at
+// once) takes the 2-wave build (its own translation unit, so100_fused2.hip, under LLVM's iterative-ILP scheduler:
+// 249-256 VGPRs, no scratch).  Register allocation only: both give the same results bit for bit.
 template <bool kDebug, int kWaves = 3>
 __global__ void __launch_bounds__(kThreads, kWaves) so100_fused_kernel(const DevModel* __restrict__ model,
                                                                        StageArgs kargs) {
@@ -1589,7 +1589,12 @@ int fused_pool_recs(int n) {
   const int per_cu = std::max({occ3, occd, lds_cap});
   const int cus_per_xcd = (cus + kPoolXcd - 1) / kPoolXcd;
   const int waves = (n + kEnvsPerBlock - 1) / kEnvsPerBlock;
+#ifdef SO100_POOL_R5   // (A/B switch: round 5's pool size, 8..32 entries per XCD by the env count)
+  (void)cus_per_xcd; (void)per_cu; (void)waves;
+  return std::min(32, std::max(8, (n + 256 * kPoolXcd - 1) / (256 * kPoolXcd)));
+#else
   return std::max(1, std::min({kPoolSlots, cus_per_xcd * per_cu, waves}));
+#endif
 }
 hipError_t alloc_fused_workspace(int n, Workspace* w) {
   *w = Workspace{};

@@ -1,3 +1,4 @@
+#include <float.h>
 #include <stdio.h>
 /* so100_oracle.c — CPU restatement of the SO-ARM100 bin-a-cube hot path (TEST INFRASTRUCTURE).
  *
@@ -1270,13 +1271,20 @@ static void table_face_snap(const so100_model* m, so100o_data* d, int k, const r
   const real lo = ax == 2 ? bottom : (real)m->table_lo[ax], hi = ax == 2 ? top : (real)m->table_hi[ax];
   const real face = sgn > 0 ? hi : lo;                     /* the face's coordinate on axis ax */
   const real* R = d->xmat[b];
+  /* the hull's support in the body-frame direction -sgn R' e_ax (its first maximal vertex, as mpr_support scans) */
+  const real nd[3] = {-sgn * R[3 * ax], -sgn * R[3 * ax + 1], -sgn * R[3 * ax + 2]};
   real best = 0, wb[3] = {0, 0, 0};
+  int bi = 0;
   for (int v = 0; v < m->hull_count[k]; v++) {
-    real hv[3], w[3];
+    real hv[3];
     load3(hv, m->hull_vert[m->hull_start[k] + v]);
-    mulmv3(w, R, hv);
-    const real h = sgn * w[ax];                           /* hull-relative height along u */
-    if (v == 0 || h < best) { best = h; wb[0] = w[0]; wb[1] = w[1]; wb[2] = w[2]; }
+    const real sc = dot3(nd, hv);
+    if (v == 0 || sc > best) { best = sc; bi = v; }
+  }
+  {
+    real hv[3];
+    load3(hv, m->hull_vert[m->hull_start[k] + bi]);
+    mulmv3(wb, R, hv);
   }
   for (int t = 0; t < 3; t++) wb[t] += d->xpos[b][t];
   const real dist = sgn * wb[ax] - sgn * face;            /* < 0: the vertex lies past the face, inside the table */
@@ -1397,19 +1405,23 @@ static int table_hull_fast(const so100_model* m, so100o_data* d, int k) {
   const real D = top - zb, cx = d->xpos[b][0] + wc[0], cy = d->xpos[b][1] + wc[1], gz = d->xpos[b][2] + wg[2];
   if (!(cx - e[0] >= (real)m->table_lo[0] + D && cx + e[0] <= (real)m->table_hi[0] - D &&
         cy - e[1] >= (real)m->table_lo[1] + D && cy + e[1] <= (real)m->table_hi[1] - D && gz - bottom >= D)) return -1;
-  /* the lowest vertex by (R v).z, the hull-relative height (cm-sized: its fp32 rounding is ~1e-9 m), the body's world
-   * z added once after: compared in world z (~0.5 m, rounding 3e-8 m) a hull face lying nearly flat tied its corners,
-   * and fp32 rounding picked another lowest corner than fp64, centimetres away (tools/dev/collision_precision.py) */
-  real best = 0, bx = 0, by = 0;
+  /* the lowest vertex as the hull's support along world -z in its body frame (its first maximal vertex: hull-relative
+   * heights, cm-sized, rounding ~1e-9 m), the body's world position added once after: compared in world z (~0.5 m,
+   * rounding 3e-8 m) a hull face lying nearly flat tied its corners, and fp32 rounding picked another lowest corner
+   * than fp64, centimetres away (tools/dev/collision_precision.py) */
+  const real nd[3] = {-R[6], -R[7], -R[8]};         /* world -z in the body frame: the hull's support along it */
+  real sbest = 0;
+  int bi = 0;
   for (int v = 0; v < m->hull_count[k]; v++) {
-    real hv[3], w[3];
+    real hv[3];
     load3(hv, m->hull_vert[m->hull_start[k] + v]);
-    mulmv3(w, R, hv);
-    if (v == 0 || w[2] < best) { best = w[2]; bx = w[0]; by = w[1]; }
+    const real sc = dot3(nd, hv);
+    if (v == 0 || sc > sbest) { sbest = sc; bi = v; }
   }
-  best += d->xpos[b][2];
-  bx += d->xpos[b][0];
-  by += d->xpos[b][1];
+  real hv[3], w[3];
+  load3(hv, m->hull_vert[m->hull_start[k] + bi]);
+  mulmv3(w, R, hv);
+  const real best = w[2] + d->xpos[b][2], bx = w[0] + d->xpos[b][0], by = w[1] + d->xpos[b][1];
   if (!(best - top < margin)) return 0;
   so100o_contact con;
   memset(&con, 0, sizeof(con));
@@ -1934,15 +1946,21 @@ static void sol_pgs(const so100_model* m, so100o_data* d, const real* AR) {
  * of 1e-6 instead, which on the EE variant (the weld folded into M: a large cost) ended solves short of the minimiser:
  * EE qvel p90 5e-4 against fp64 (tools/dev/mixed_precision.py).  The decrement resolves where fp32 can (g's noise
  * enters squared) and matches fp64's iteration counts: 1.20 line searches per substep on the bench workload
- * (fp64 1.22, the relative stop 1.88), EE qvel p90 2.5e-5. */
+ * (fp64 1.22, the relative stop 1.88), EE qvel p90 2.5e-5.  And at an iteration's start, before the Hessian: every
+ * component of the gradient within 16 float epsilons of its terms' magnitudes (the Gauss row and each row block's
+ * J' f in absolute value: the gradient is at its own rounding, MuJoCo's |g| test in fp32's terms).  Without it each
+ * solve paid one more Hessian and Cholesky to find the decrement small: per substep on the bench workload, 2.15
+ * factorizations -> 1.34 (the relative stop: 1.88), line searches 1.20 either way. */
 #if defined(SO100O_FLOAT) && !defined(LS_TOL)
 #define LS_TOL ((real)1e-2)
 #define LS_STEP ((real)1e-4)
 #define NEWTON_DECREMENT 1
+#define NEWTON_GNOISE 16
 #elif !defined(LS_TOL)
 #define LS_TOL ((real)1e-12)
 #define LS_STEP ((real)0)
 #define NEWTON_DECREMENT 0
+#define NEWTON_GNOISE 0
 #endif
 
 /* cost, force (= -d cost / d jar) and cost Hessian of the constraint block at row i; returns its rows */
@@ -2103,6 +2121,8 @@ static real line_search(const so100o_data* d, const real a[NV], const real s[NV]
   return alpha;
 }
 
+/* tools/dev: Newton work counters (gradient evaluations, Hessian + Cholesky factorizations, line searches) */
+long so100o_newton_counts[3];
 static void sol_newton(const so100_model* m, so100o_data* d) {
   const int nefc = d->nefc;
   const real scale = 1 / ((real)m->meaninertia * (real)NV);
@@ -2119,17 +2139,25 @@ static void sol_newton(const so100_model* m, so100o_data* d) {
   d->solver_improvement = 0;
   for (int it = 0; it < m->iterations; it++) {
     /* gradient and Hessian at a */
-    real grad[NV], H[NV][NV];
+    /* gabs: the gradient's terms in absolute value, one per term (the Gauss row, each row block's J' f): the scale of
+     * the gradient's own rounding (NEWTON_GNOISE) */
+    real grad[NV], H[NV][NV], gabs[NV];
     for (int i = 0; i < NV; i++) {
       real t = 0;
       for (int j = 0; j < NV; j++) { t += d->qM[i][j] * (a[j] - d->qacc_smooth[j]); H[i][j] = d->qM[i][j]; }
       grad[i] = t;
+      gabs[i] = (real)fabs((double)t);
     }
     for (int i = 0; i < nefc;) {
       real cb, fb[4], Hb[4][4];
       const int dim = block_eval(d, i, jar + i, &cb, fb, Hb);
+      for (int v = 0; v < NV; v++) {
+        real t = 0;
+        for (int k = 0; k < dim; k++) t += d->efc_J[i + k][v] * fb[k];
+        grad[v] -= t;
+        gabs[v] += (real)fabs((double)t);
+      }
       for (int k = 0; k < dim; k++) {
-        for (int v = 0; v < NV; v++) grad[v] -= d->efc_J[i + k][v] * fb[k];
         for (int l = 0; l < dim; l++) {
           if (Hb[k][l] == 0) continue;
           for (int p = 0; p < NV; p++)
@@ -2138,17 +2166,25 @@ static void sol_newton(const so100_model* m, so100o_data* d) {
       }
       i += dim;
     }
+    so100o_newton_counts[0]++;
     real gn = 0;
-    for (int k = 0; k < NV; k++) gn += grad[k] * grad[k];
+    int gnoise = 1;
+    for (int k = 0; k < NV; k++) {
+      gn += grad[k] * grad[k];
+      gnoise &= (real)fabs((double)grad[k]) <= (real)NEWTON_GNOISE * (real)FLT_EPSILON * gabs[k];
+    }
     if (scale * (real)sqrt((double)gn) < (real)m->tolerance) break;
+    if (NEWTON_GNOISE > 0 && gnoise) break;
     real s[NV], mg[NV];
     for (int k = 0; k < NV; k++) mg[k] = -grad[k];
+    so100o_newton_counts[1]++;
     if (!chol_solve(H, mg, s)) break;
     if (NEWTON_DECREMENT) {
       real gs = 0;
       for (int k = 0; k < NV; k++) gs += grad[k] * s[k];
       if (scale * (real)-0.5 * gs < (real)m->tolerance) break;
     }
+    so100o_newton_counts[2]++;
     const real alpha = line_search(d, a, s, jar);
     d->solver_iter = it + 1;
     if (alpha == 0) break;
