@@ -52,9 +52,10 @@ DEV float nsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 DEV float nrcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // MuJoCo mj_constraintUpdate (primal), elliptic contact block at jar: cost, force f = -dc/djar, and the
-// cost Hessian (upper triangle 00 01 02 03 11 12 13 22 23 33).  Oracle block_eval.
-DEV void cone_eval(const float* jar, const float* D, float Dm, float mu, float fr0, float fr1, float& cost, float* f,
-                   float* h) {
+// cost Hessian (upper triangle 00 01 02 03 11 12 13 22 23 33); returns the cone zone: 0 top (no force), 1 bottom
+// (quadratic), 2 middle.  Oracle block_eval.
+DEV int cone_eval(const float* jar, const float* D, float Dm, float mu, float fr0, float fr1, float& cost, float* f,
+                  float* h) {
   const float fr[4] = {mu, fr0, fr0, fr1};
   float U[4];
 #pragma unroll
@@ -66,12 +67,12 @@ DEV void cone_eval(const float* jar, const float* D, float Dm, float mu, float f
   for (int k = 0; k < 4; k++) f[k] = 0.f;
 #pragma unroll
   for (int k = 0; k < 10; k++) h[k] = 0.f;
-  if (N >= mu * T || (T <= 0.f && N >= 0.f)) return;                          // top zone: no force
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) return 0;                        // top zone: no force
   if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {                            // bottom zone: quadratic
 #pragma unroll
     for (int k = 0; k < 4; k++) { f[k] = -D[k] * jar[k]; cost += 0.5f * D[k] * jar[k] * jar[k]; }
     h[0] = D[0]; h[4] = D[1]; h[7] = D[2]; h[9] = D[3];
-    return;
+    return 1;
   }
   // middle zone: c = 1/2 Dm (N - mu T)^2, g = d(N - mu T)/djar
   const float NmT = N - mu * T, invT = nrcp(T);
@@ -92,23 +93,24 @@ DEV void cone_eval(const float* jar, const float* D, float Dm, float mu, float f
       if (k >= 1) v += c2 * fr[k] * fr[l] * ((k == l ? invT : 0.f) - U[k] * U[l] * invT3);
       h[q] = v;
     }
+  return 2;
 }
 // The line search's view of a contact block: the cost's first and second derivatives at jar along v, as
 // -f . v and v' H v, without forming H (in the middle zone H is rank one plus the friction rows' curvature, so
 // v' H v = Dm (g.v)^2 + c2 (|fr v|^2 / T - (sum U_k fr_k v_k)^2 / T^3)): the same zones and the same values as
-// cone_eval followed by f . v and v' sym4(h, v), in a third of the dependent operations.
-DEV void cone_dir(const float* jar, const float* v, const float* D, float Dm, float mu, float fr0, float fr1,
-                  float& fv, float& vhv) {
+// cone_eval followed by f . v and v' sym4(h, v), in a third of the dependent operations; returns the zone as cone_eval.
+DEV int cone_dir(const float* jar, const float* v, const float* D, float Dm, float mu, float fr0, float fr1,
+                 float& fv, float& vhv) {
   const float U1 = jar[1] * fr0, U2 = jar[2] * fr0, U3 = jar[3] * fr1;
   const float T = nsqrt(U1 * U1 + U2 * U2 + U3 * U3);
   const float N = jar[0] * mu;
   fv = 0.f;
   vhv = 0.f;
-  if (N >= mu * T || (T <= 0.f && N >= 0.f)) return;                          // top zone: no force
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) return 0;                        // top zone: no force
   if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {                            // bottom zone: quadratic
 #pragma unroll
     for (int k = 0; k < 4; k++) { fv -= D[k] * jar[k] * v[k]; vhv += D[k] * v[k] * v[k]; }
-    return;
+    return 1;
   }
   const float NmT = N - mu * T, invT = nrcp(T);
   const float w1 = fr0 * v[1], w2 = fr0 * v[2], w3 = fr1 * v[3];
@@ -116,18 +118,22 @@ DEV void cone_dir(const float* jar, const float* v, const float* D, float Dm, fl
   const float gv = mu * v[0] - mu * invT * s2;                               // g . v
   fv = -Dm * NmT * gv;
   vhv = Dm * gv * gv - Dm * NmT * mu * (invT * s1 - invT * invT * invT * s2 * s2);
+  return 2;
 }
-// frictionloss row (Huber) and joint-limit row (one-sided quadratic) at jar x
-DEV void fr_eval(float x, float fl, float R, float D, float& cost, float& f, float& h) {
-  if (x >= R * fl) { f = -fl; cost = fl * x - 0.5f * R * fl * fl; h = 0.f; }
-  else if (x <= -R * fl) { f = fl; cost = -fl * x - 0.5f * R * fl * fl; h = 0.f; }
-  else { f = -D * x; cost = 0.5f * D * x * x; h = D; }
+// frictionloss row (Huber) and joint-limit row (one-sided quadratic) at jar x; they return their zone (frictionloss:
+// 2 linear above, 0 linear below, 1 quadratic; limit: 1 active)
+DEV int fr_eval(float x, float fl, float R, float D, float& cost, float& f, float& h) {
+  if (x >= R * fl) { f = -fl; cost = fl * x - 0.5f * R * fl * fl; h = 0.f; return 2; }
+  if (x <= -R * fl) { f = fl; cost = -fl * x - 0.5f * R * fl * fl; h = 0.f; return 0; }
+  f = -D * x; cost = 0.5f * D * x * x; h = D;
+  return 1;
 }
-DEV void lim_eval(float x, bool on, float D, float& cost, float& f, float& h) {
+DEV int lim_eval(float x, bool on, float D, float& cost, float& f, float& h) {
   const bool act = on && x < 0.f;
   f = act ? -D * x : 0.f;
   cost = act ? 0.5f * D * x * x : 0.f;
   h = act ? D : 0.f;
+  return act;
 }
 // h (upper triangle) times v
 DEV float4 sym4(const float* h, float4 v) {
@@ -467,9 +473,12 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
     if (!done) {
       // ---- rows at the current point: forces and Hessians
       float c0, f_fr = 0.f, h_fr = 0.f, f_lim, h_lim, fc[4], hc[10];
-      if (dof) fr_eval(jfr, fr_fl, fr_R, fr_D, c0, f_fr, h_fr);
-      lim_eval(jlim, lim_on, lim_D, c0, f_lim, h_lim);
-      cone_eval(jc, c_D, c_Dm, c_mu, c_fr0, c_fr1, c0, fc, hc);
+      int zf = 0;
+      if (dof) zf = fr_eval(jfr, fr_fl, fr_R, fr_D, c0, f_fr, h_fr);
+      const int zl = lim_eval(jlim, lim_on, lim_D, c0, f_lim, h_lim);
+      const int zc = cone_eval(jc, c_D, c_Dm, c_mu, c_fr0, c_fr1, c0, fc, hc);
+      // the rows' zones at the iterate, for the quadratic-exact stop (frictionloss rows only where they exist)
+      const int z0 = (fr_fl > 0.f ? zf : 0) | zl << 2 | (own ? zc : 0) << 3;
       if (!own) {
 #pragma unroll
         for (int k = 0; k < 4; k++) fc[k] = 0.f;
@@ -519,14 +528,17 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
       }
       grad = dof ? grad : 0.f;
       const float gn = nsqrt(rowsum16(grad * grad));
-      // the gradient at its own rounding (round 6; oracle NEWTON_GNOISE): every dof's within 16 float epsilons of its
-      // terms' magnitudes.  MuJoCo's |g| test in fp32's terms: it ends the solve before the Hessian and the Cholesky
-      // that the Newton decrement below would otherwise pay to find the step negligible (1.34 instead of 2.15
-      // factorizations per substep on the bench workload)
-#ifdef SO100_NEWTON_RELSTOP
-      const bool gquiet = false;
+      // (A/B switch, measured and not kept: -DSO100_GNOISE_K=k stops at the gradient's own rounding, every dof's within
+      // k float epsilons of its terms' magnitudes, before the Hessian and the Cholesky: 1.34 instead of 2.15
+      // factorizations per substep on the bench workload and +2 % env steps/s at 65,536 envs, but blind to the
+      // curvature — in the deep Base folds a gradient at the rounding of centimetre-deep contact forces still moved the
+      // light dofs, and the GPU's qvel p99 there went 1.8e-3 -> 1.4e-2 against a floor of 2.7e-3)
+#ifdef SO100_GNOISE_K
+      const bool gquiet =
+          rowsum16((dof && !(fabsf(grad) <= SO100_GNOISE_K * 1.1920929e-7f * gab)) ? 1.f : 0.f) == 0.f;
 #else
-      const bool gquiet = rowsum16((dof && !(fabsf(grad) <= 16.f * 1.1920929e-7f * gab)) ? 1.f : 0.f) == 0.f;
+      const bool gquiet = false;
+      (void)gab;
 #endif
       STAMP(2);
       if (scale * gn < tolerance || gquiet) {
@@ -645,19 +657,22 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             }
           }
         }
-        auto derivs = [&](float al, float& d1, float& d2) {
+        // (returns the rows' zones at alpha, as z0)
+        auto derivs = [&](float al, float& d1, float& d2) -> int {
           float l1 = 0.f, l2 = 0.f, cc, f, h;
-          if (dof) { fr_eval(jfr + al * sfr, fr_fl, fr_R, fr_D, cc, f, h); l1 -= f * sfr; l2 += h * sfr * sfr; }
-          lim_eval(jlim + al * slim, lim_on, lim_D, cc, f, h);
+          int zf = 0, zc = 0;
+          if (dof) { zf = fr_eval(jfr + al * sfr, fr_fl, fr_R, fr_D, cc, f, h); l1 -= f * sfr; l2 += h * sfr * sfr; }
+          const int zl = lim_eval(jlim + al * slim, lim_on, lim_D, cc, f, h);
           l1 -= f * slim; l2 += h * slim * slim;
           if (own) {
             float x[4], fv, vhv;
 #pragma unroll
             for (int k = 0; k < 4; k++) x[k] = jc[k] + al * jsc[k];
-            cone_dir(x, jsc, c_D, c_Dm, c_mu, c_fr0, c_fr1, fv, vhv);
+            zc = cone_dir(x, jsc, c_D, c_Dm, c_mu, c_fr0, c_fr1, fv, vhv);
             l1 -= fv;
             l2 += vhv;
           }
+
           if (kOvf && ncon_max > kMaxCon) {
             float* crec = rec();
             for (int c = kMaxCon + lane; c < ncon; c += kLanes) {
@@ -675,6 +690,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           }
           d1 = rowsum16(l1) + A1 + al * A2;
           d2 = rowsum16(l2) + A2;
+          return (fr_fl > 0.f ? zf : 0) | zl << 2 | zc << 3;
         };
         // c'(0) from the forces already evaluated at the current point (= derivs(0)'s d1)
         float d10;
@@ -696,6 +712,7 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
         const bool converged = scale * (-0.5f * d10) < tolerance;
 #endif
         float alpha = 0.f;
+        int z1 = -1;                           // the line search took alpha = 1 at its first evaluation: the zones there
         if (!converged && d10 < 0.f) {
           // fp32 stops (oracle LS_TOL / LS_STEP): MuJoCo's ls_tolerance 0.01 on |c'|, or a relative step 1e-4
           const float tol_ls = 1e-2f * -d10;
@@ -703,8 +720,8 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           alpha = 1.f;
           for (int ls = 0; ls < 50; ls++) {
             float d1, d2;
-            derivs(alpha, d1, d2);
-            if (fabsf(d1) <= tol_ls) break;
+            const int z = derivs(alpha, d1, d2);
+            if (fabsf(d1) <= tol_ls) { if (ls == 0) z1 = z; break; }
             if (d1 < 0.f) lo = alpha; else hi = alpha;
             float nxt = d2 > 0.f ? alpha - d1 * nrcp(d2) : -1.f;
             if (hi >= 0.f) { if (!(nxt > lo && nxt < hi)) nxt = 0.5f * (lo + hi); }
@@ -714,6 +731,12 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
             alpha = nxt;
           }
         }
+        // the quadratic-exact stop (round 6; oracle NEWTON_QUADSTOP): a full step (alpha = 1 accepted at once) along
+        // which no row changed zone and no contact is in the cone's middle zone (an env with contacts beyond kMaxCon
+        // keeps MuJoCo's stops: its record's zones are not tracked).  The cost is then one quadratic on the whole
+        // segment and the step, along its exact Hessian, lands on that quadratic's minimiser: the next gradient is
+        // zero up to rounding, and evaluating it (a Hessian and a Cholesky for the decrement to confirm) is skipped
+        const bool quad = rowsum16(z1 == z0 && (z0 >> 3) != 2 && ncon <= kMaxCon ? 0.f : 1.f) == 0.f;
         if (!converged) iters = it + 1;
         STAMP(5);
         if (alpha == 0.f) {
@@ -753,6 +776,9 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           if (improvement < tolerance || improvement < 1e-6f * scale * fabsf(cost)) done = true;
 #else
           if (improvement < tolerance) done = true;
+#endif
+#ifndef SO100_NO_QUADSTOP
+          if (quad) done = true;
 #endif
         }
         STAMP(6);

@@ -1067,7 +1067,8 @@ DEV void fresh_ids(int group, int n, int& lane, int& grp, int& env, int& e) {
 // Results are those of the split path (so100_stage_kernel + so100_newton_kernel): the same device
 // functions on the same values.  kDebug: the instantiation that also fills the debug buffer (launched when
 // the caller passes one); the other has no debug code, which costs registers in the substep loop.
-// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs, no scratch since round 5) when the
+// kWaves: the waves per SIMD the register budget is sized for.  3 (168 VGPRs; 8 B/lane of scratch since round 6's
+// quadratic-exact Newton stop: two floats of the arm's M row, reloaded twice per Newton step) when the
 // grid exceeds 2 waves per SIMD; a grid of at most 2 waves per SIMD (8,192 envs on 256 CUs: all waves resident at
 // once) takes the 2-wave build (its own translation unit, so100_fused2.hip, under LLVM's iterative-ILP scheduler:
 // 249-256 VGPRs, no scratch).  Register allocation only: both give the same results bit for bit.

@@ -1946,21 +1946,22 @@ static void sol_pgs(const so100_model* m, so100o_data* d, const real* AR) {
  * of 1e-6 instead, which on the EE variant (the weld folded into M: a large cost) ended solves short of the minimiser:
  * EE qvel p90 5e-4 against fp64 (tools/dev/mixed_precision.py).  The decrement resolves where fp32 can (g's noise
  * enters squared) and matches fp64's iteration counts: 1.20 line searches per substep on the bench workload
- * (fp64 1.22, the relative stop 1.88), EE qvel p90 2.5e-5.  And at an iteration's start, before the Hessian: every
- * component of the gradient within 16 float epsilons of its terms' magnitudes (the Gauss row and each row block's
- * J' f in absolute value: the gradient is at its own rounding, MuJoCo's |g| test in fp32's terms).  Without it each
- * solve paid one more Hessian and Cholesky to find the decrement small: per substep on the bench workload, 2.15
- * factorizations -> 1.34 (the relative stop: 1.88), line searches 1.20 either way. */
+ * (fp64 1.22, the relative stop 1.88), EE qvel p90 2.5e-5.  (NEWTON_GNOISE k, measured and not kept: stop at an
+ * iteration's start when every gradient component lies within k float epsilons of its terms' magnitudes, before the
+ * Hessian: 2.15 -> 1.34 factorizations per substep on the bench workload at k = 16, but blind to the curvature: on
+ * the GPU the deep Base folds' qvel p99 went 1.8e-3 -> 1.4e-2) */
 #if defined(SO100O_FLOAT) && !defined(LS_TOL)
 #define LS_TOL ((real)1e-2)
 #define LS_STEP ((real)1e-4)
 #define NEWTON_DECREMENT 1
-#define NEWTON_GNOISE 16
+#define NEWTON_GNOISE 0
+#define NEWTON_QUADSTOP 1
 #elif !defined(LS_TOL)
 #define LS_TOL ((real)1e-12)
 #define LS_STEP ((real)0)
 #define NEWTON_DECREMENT 0
 #define NEWTON_GNOISE 0
+#define NEWTON_QUADSTOP 0
 #endif
 
 /* cost, force (= -d cost / d jar) and cost Hessian of the constraint block at row i; returns its rows */
@@ -2093,7 +2094,7 @@ static void line_derivs(const so100o_data* d, const real e[NV], const real s[NV]
   *d1 = g1;
   *d2 = g2;
 }
-static real line_search(const so100o_data* d, const real a[NV], const real s[NV], const real* jar0) {
+static real line_search(const so100o_data* d, const real a[NV], const real s[NV], const real* jar0, int* first) {
   real e[NV], Js[NEFC];
   for (int k = 0; k < NV; k++) e[k] = a[k] - d->qacc_smooth[k];
   for (int i = 0; i < d->nefc; i++) {
@@ -2102,6 +2103,7 @@ static real line_search(const so100o_data* d, const real a[NV], const real s[NV]
     Js[i] = t;
   }
   real d10, d20;
+  *first = 0;
   line_derivs(d, e, s, jar0, Js, 0, &d10, &d20);
   if (!(d10 < 0)) return 0;
   const real tol = LS_TOL * -d10;
@@ -2109,7 +2111,7 @@ static real line_search(const so100o_data* d, const real a[NV], const real s[NV]
   for (int it = 0; it < 50; it++) {
     real d1, d2;
     line_derivs(d, e, s, jar0, Js, alpha, &d1, &d2);
-    if ((real)fabs((double)d1) <= tol) break;
+    if ((real)fabs((double)d1) <= tol) { *first = it == 0; break; }
     if (d1 < 0) lo = alpha; else hi = alpha;
     real nxt = d2 > 0 ? alpha - d1 / d2 : -1;
     if (hi >= 0) { if (!(nxt > lo && nxt < hi)) nxt = (real)0.5 * (lo + hi); }
@@ -2119,6 +2121,43 @@ static real line_search(const so100o_data* d, const real a[NV], const real s[NV]
     alpha = nxt;
   }
   return alpha;
+}
+
+/* the zone of the row block at row i at jar (mj_constraintUpdate's cases): frictionloss 0 / 1 / 2 (linear below,
+ * quadratic, linear above), joint limit 0 / 1 (inactive, quadratic), contact 0 / 1 / 2 (top: no force, bottom:
+ * quadratic, middle: the cone's non-quadratic zone); its row count in *dim */
+static int block_zone(const so100o_data* d, int i, const real* jar, int* dim) {
+  const int t = d->efc_type[i];
+  *dim = 1;
+  if (t == SO100O_EFC_FRICTION) {
+    const real x = jar[0], rf = d->efc_R[i] * d->efc_frictionloss[i];
+    return x >= rf ? 2 : (x <= -rf ? 0 : 1);
+  }
+  if (t == SO100O_EFC_LIMIT) return jar[0] < 0 ? 1 : 0;
+  const int n = d->efc_dim[i];
+  *dim = n;
+  const real mu = d->efc_mu[i][0] * (real)sqrt((double)(d->efc_R[i + 1] / d->efc_R[i]));
+  real T = 0;
+  for (int k = 1; k < n; k++) { const real u = jar[k] * d->efc_mu[i][k - 1]; T += u * u; }
+  T = (real)sqrt((double)T);
+  const real N = jar[0] * mu;
+  if (N >= mu * T || (T <= 0 && N >= 0)) return 0;
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) return 1;
+  return 2;
+}
+/* the cost is exactly quadratic between two iterates when no row block changed zone and no contact is in the middle
+ * zone: then a full Newton step along the exact Hessian lands on the quadratic's stationary point, the minimiser.
+ * As the kernel (so100_newton.h, the quadratic-exact stop): lists longer than the kMaxCon contacts the kernel holds on
+ * chip (SO100_MAXCON) keep MuJoCo's stops */
+static int same_quadratic(const so100o_data* d, const real* jar0, const real* jar1) {
+  if (d->ncon > SO100_MAXCON) return 0;
+  for (int i = 0; i < d->nefc;) {
+    int n;
+    const int z0 = block_zone(d, i, jar0 + i, &n), z1 = block_zone(d, i, jar1 + i, &n);
+    if (z0 != z1 || (d->efc_type[i] == SO100O_EFC_CONTACT && z0 == 2)) return 0;
+    i += n;
+  }
+  return 1;
 }
 
 /* tools/dev: Newton work counters (gradient evaluations, Hessian + Cholesky factorizations, line searches) */
@@ -2185,11 +2224,21 @@ static void sol_newton(const so100_model* m, so100o_data* d) {
       if (scale * (real)-0.5 * gs < (real)m->tolerance) break;
     }
     so100o_newton_counts[2]++;
-    const real alpha = line_search(d, a, s, jar);
+    int first = 0;
+    const real alpha = line_search(d, a, s, jar, &first);
     d->solver_iter = it + 1;
     if (alpha == 0) break;
+    static __thread real jar_prev[NEFC];
+    if (NEWTON_QUADSTOP) memcpy(jar_prev, jar, sizeof(real) * (size_t)nefc);
     for (int k = 0; k < NV; k++) a[k] += alpha * s[k];
     jar_at(d, a, jar);
+    /* the quadratic-exact stop (fp32, round 6): the line search accepted alpha = 1 at its first evaluation over a
+     * segment on which the cost is one quadratic (same_quadratic): the step is that quadratic's minimiser, the next
+     * gradient zero up to rounding, and the decrement's confirming factorization is skipped */
+    if (NEWTON_QUADSTOP && first && alpha == 1 && same_quadratic(d, jar_prev, jar)) {
+      cost = gauss_cost(d, a) + constraint_cost(d, jar, f);
+      break;
+    }
     const real nc = gauss_cost(d, a) + constraint_cost(d, jar, f);
     const real improvement = scale * (cost - nc);
     cost = nc;

@@ -122,6 +122,9 @@ def states_for(cls, model, o64, nstates, seed):
         o64.call("so100o_fwd_position", model, d)
         if cls == "table_edge":
             ok = any(table(d.con[i].pair) and abs(d.con[i].frame[2]) < 0.99 for i in range(d.ncon))
+        elif cls == "base":            # test_base_contact_parity's class: a link against the static Base's hull
+            from gym_so100.model import PAIR_BASE0, PAIR_PADLINK0
+            ok = any(PAIR_BASE0 <= d.con[i].pair < PAIR_PADLINK0 for i in range(d.ncon)) and not d.ncon_dropped
         else:
             ok = True
         if ok:
@@ -160,7 +163,7 @@ def set_mocap(d, mocap):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cls", default="table_edge", choices=["table_edge", "ee"])
+    ap.add_argument("--cls", default="table_edge", choices=["table_edge", "ee", "base"])
     ap.add_argument("--states", type=int, default=48)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--lib32", default=None, help="another fp32 build of the oracle (experiments)")
@@ -180,9 +183,10 @@ def main():
                 for t in range(args.steps)]
         episodes = [(q, mocap, [acts[t][i] for t in range(args.steps)]) for i, (q, mocap) in enumerate(eps)]
     else:
-        rng = np.random.default_rng(31)
+        seed = {"table_edge": 31, "base": 19}[args.cls]
+        rng = np.random.default_rng(seed)
         episodes = [(q, None, [np.clip(target + rng.normal(0, 0.02, 6), -1, 1) for _ in range(args.steps)])
-                    for q, target in states_for(args.cls, model, o64, args.states, 31)]
+                    for q, target in states_for(args.cls, model, o64, args.states, seed)]
     mixes = [("all fp64", [64] * 8), ("all fp32", [32] * 8)]
     for k, s in enumerate(STAGES):
         mixes.append((f"fp32, {s} in fp64", [64 if j == k else 32 for j in range(8)]))
