@@ -1386,6 +1386,10 @@ static void convex_pair(const so100_model* m, so100o_data* d, int p) {
  * ties) and its projection on the top: pos = their midpoint, normal +z (table, geom1 -> hull, geom2).  Otherwise (a
  * hull at the table's edges or side faces, or deep in it) the pair goes through the convex collider after pairs
  * 23..151 (the kernels' order).  Returns 1: contact added, 0: no contact, -1: the convex collider. */
+/* test hook (tests/test_oracle_epa.py): nonzero sends every candidate hull-table pair through the convex collider (GJK
+ * + EPA + the table face snap) instead of the top-face rule, to check that both give the same contact where the rule
+ * applies (the kernel classifies in fp32, the fp64 oracle in fp64, near the rule's bounds) */
+int so100o_table_force_slow = 0;
 static int table_hull_fast(const so100_model* m, so100o_data* d, int k) {
   const int p = SO100_NPAIR_BOX + k, b = m->hull_body[k], g = m->pair_geom1[p];
   const real top = (real)m->table_top, margin = (real)m->pair_margin[p];
@@ -1400,6 +1404,7 @@ static int table_hull_fast(const so100_model* m, so100o_data* d, int k) {
            (real)fabs((double)R[3 * i + 2]) * (real)m->hull_half[k][2];
   const real zb = d->xpos[b][2] + wc[2] - e[2];
   if (!(zb < top + margin)) return 0;
+  if (so100o_table_force_slow) return -1;
   load3(cg, m->hull_centroid[k]);
   mulmv3(wg, R, cg);
   const real D = top - zb, cx = d->xpos[b][0] + wc[0], cy = d->xpos[b][1] + wc[1], gz = d->xpos[b][2] + wg[2];

@@ -217,3 +217,53 @@ def test_table_pairs_are_the_minimum_penetration(oracle64):
     print(f"\ntable contacts {n}, side-face contacts {side}")
     assert n["hull"] >= 200 and n["pad"] >= 200 and n["cube"] >= 50, n
     assert side["hull"] >= 5 and side["pad"] >= 5, side
+
+
+@pytest.mark.parametrize("bits", [64, 32])
+def test_top_face_rule_and_collider_agree(bits, oracle64, oracle32):
+    """Where the top-face rule applies (a hull over the table's top face, provably its minimum penetration along +z),
+    the convex collider gives the same contact (DESIGN.md §3.2 S3a'): GJK + EPA's final facet lies within 1e-5 rad of
+    the top face's normal, so the table face snap takes that face's contact, the hull's support vertex along -z and its
+    projection, as the rule does.  The kernel decides rule or collider in fp32 and the oracle in fp64, so near the
+    rule's bounds the two can take different paths; this pins that the paths agree on depth, normal and
+    position, in the fp64 and the fp32 restatement.  so100o_table_force_slow sends every candidate through the
+    collider; random arm poses over the table (the generator of test_table_pairs_are_the_minimum_penetration)."""
+    import ctypes
+    from gym_so100.model import NPAIR_BOX, NHULL
+    o = oracle64 if bits == 64 else oracle32
+    force = ctypes.c_int.in_dll(o.lib, "so100o_table_force_slow")
+    m = build_model()
+    d = o.new_data()
+    rng = np.random.default_rng(23)
+    lo = np.array([r[0] for r in m.jnt_range]); hi = np.array([r[1] for r in m.jnt_range])
+    pairs = set(range(NPAIR_BOX, NPAIR_BOX + NHULL))
+    tol_pos, tol_depth = (1e-9, 1e-6) if bits == 64 else (2e-6, 2e-6)
+    compared = 0
+    try:
+        for _ in range(600):
+            arm = rng.uniform(lo, hi)
+            box = np.array([rng.uniform(-0.62, -0.15), rng.uniform(0.2, 0.75), 0.1, 1, 0, 0, 0])
+            out = []
+            for f in (0, 1):
+                force.value = f
+                o.reset(m, d, box)
+                for k in range(6):
+                    d.qpos[k] = arm[k]
+                o.call("so100o_fwd_position", m, d)
+                out.append({d.con[i].pair: (d.con[i].dist, np.array(d.con[i].frame[:3]), np.array(d.con[i].pos[:]))
+                            for i in range(d.ncon) if d.con[i].pair in pairs})
+            fast, slow = out
+            for p, (dist, nrm, pos) in fast.items():
+                if abs(nrm[2] - 1.0) > 0 or p not in slow:
+                    continue                      # not a top-face-rule contact (the collider's in both runs), or see below
+                sd, sn, sp = slow[p]
+                assert abs(sd - dist) <= tol_depth, (p, dist, sd)
+                assert np.abs(sn - nrm).max() <= 1e-5, (p, sn)
+                assert np.abs(sp - pos).max() <= tol_pos, (p, pos, sp)
+                compared += 1
+            # every rule contact has its collider twin, and the collider finds no contact the rule missed
+            assert set(fast) == set(slow), (sorted(fast), sorted(slow))
+    finally:
+        force.value = 0
+    print(f"\n{bits}-bit: {compared} top-face-rule contacts matched by the collider")
+    assert compared >= 100, compared
