@@ -745,25 +745,13 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
           done = true;
         } else {
           // ---- move; the new cost gives MuJoCo's improvement test
-          // (explicit FMAs: the builds differ in what follows the move — the quadratic-exact stop's skipped cost below —
-          // and the backend's contraction of a separate multiply and add followed the code around it, so the 2- and 3-wave
-          // builds left the bitwise agreement every build keeps)
-          qacc = __builtin_fmaf(alpha, sv, qacc);
-          ev = __builtin_fmaf(alpha, sv, ev);
-          Me = __builtin_fmaf(alpha, Ms, Me);
-          jfr = __builtin_fmaf(alpha, sfr, jfr);
-          jlim = __builtin_fmaf(alpha, slim, jlim);
+          qacc += alpha * sv;
+          ev += alpha * sv;
+          Me += alpha * Ms;
+          jfr += alpha * sfr;
+          jlim += alpha * slim;
 #pragma unroll
-          for (int k = 0; k < 4; k++) jc[k] = __builtin_fmaf(alpha, jsc[k], jc[k]);
-#ifndef SO100_NO_QUADSTOP
-          if (quad && !want_diag) {
-            // the quadratic-exact stop (below): the new cost would serve only MuJoCo's improvement test, which this stop
-            // makes moot; the debug build evaluates it for its record (last_impr), the iterate is the same either way
-            // (+2.8 % at 65,536 envs, profiles/r06_ab_round.txt item 7)
-            done = true;
-          } else
-#endif
-          {
+          for (int k = 0; k < 4; k++) jc[k] += alpha * jsc[k];
           gauss += alpha * A1 + 0.5f * alpha * alpha * A2;
           float ncl = rows_cost(jfr, jlim, jc);
           if (kOvf && ncon_max > kMaxCon) {
@@ -794,7 +782,6 @@ DEV float newton_solve(const DevModel* __restrict__ m, const NewtonRows& r, int 
 #ifndef SO100_NO_QUADSTOP
           if (quad) done = true;
 #endif
-          }
         }
         STAMP(6);
       }
